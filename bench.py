@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""bench.py -- primary rays/s of the MI355X BIH ray tracer.
+
+Workload (BASELINE.json configs[2]): 1,000,000-triangle
+random soup (splitmix64 seed 1), 1920x1080, 4 jittered primary rays per
+pixel, reference camera, cuRAND-XORWOW seed 1984.  One step = one frame:
+the render kernel over this rank's interleaved 8-row bands plus, for N > 1,
+the RCCL all-gather that assembles the frame on every rank.  The BIH is
+built once before the timed region (its device time is reported as build_ms;
+the reference rebuilds it every frame, Renderer.cpp:415-503).
+
+Single process:   python bench.py
+Multi-GPU:        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bih-gpu-raytracer_amd"))
+
+METRIC = "primary rays/sec at 1920×1080, 1M-tri scene; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+NODE_B, LEAF_B, TRI_B = 16, 8, 40   # SURVEY.md 8d algorithmic bytes
+FB_B, RNG_B = 4, 48
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=4)
+    ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on rank 0 (N=1)")
+    ap.add_argument("--cpu-row-step", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-reference-leg", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import bihrt
+    from bihrt.tiling import band_rows, max_rows, rows_of_rank
+
+    W, H, SPP = args.width, args.height, args.spp
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    # scene: generated on the host (deterministic), resident in HBM before timing
+    tris = bihrt.scenes.soup(args.tris, seed=1)
+    d_tris = torch.from_numpy(tris).to(f"cuda:{local}")
+    arrays = bihrt.GPUArrayManager.from_device(d_tris.data_ptr(), tris.shape[0], device=local,
+                                               stream=sptr)
+    info = arrays.info()
+    cam = bihrt.camera_reference(W, H)
+    r = bihrt.Renderer(arrays, W, H, spp=SPP, seed=1984, camera=cam)
+    rows = band_rows(H, args.band, rank, world)
+    mrows = max_rows(H, args.band, world)
+    out = torch.zeros(mrows * W, dtype=torch.int32, device="cuda")
+    gathered = torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") if world > 1 else None
+    if world > 1:
+        perm = []
+        for rr in range(world):
+            ys = rows_of_rank(H, args.band, rr, world)
+            perm.append(torch.as_tensor(ys, dtype=torch.long))
+        order = torch.empty(H, dtype=torch.long)
+        for rr in range(world):
+            order[perm[rr]] = torch.arange(perm[rr].numel()) + rr * mrows
+        order = order.cuda()
+        frame_img = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
+
+    def step(frame, traverse, ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        r.render_device(out.data_ptr(), frame, rows=rows, traverse=traverse, stream=sptr)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+            torch.index_select(gathered.view(world * mrows, W), 0, order,
+                               out=frame_img.view(H, W))
+
+    def timed(traverse, first_frame):
+        for k in range(args.warmup):
+            step(first_frame + k, traverse)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(first_frame + args.warmup + k, traverse, evs[k])
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        kms = [a.elapsed_time(b) for a, b in evs]
+        return float(t.item()), kms
+
+    elapsed, kms = timed(trav, 0)
+    rays_per_frame = W * H * SPP
+    value = rays_per_frame * args.steps / elapsed
+    kernel_ms = sum(kms) / len(kms)
+
+    ref_leg = None
+    if not args.no_reference_leg:
+        other = bihrt.TRAVERSE_REFERENCE if trav == bihrt.TRAVERSE_ANYHIT else bihrt.TRAVERSE_ANYHIT
+        el2, kms2 = timed(other, 1000)
+        ref_leg = {"traverse": "reference" if other == bihrt.TRAVERSE_REFERENCE else "anyhit",
+                   "value": rays_per_frame * args.steps / el2,
+                   "ms_per_step": 1e3 * el2 / args.steps,
+                   "kernel_ms": sum(kms2) / len(kms2)}
+
+    # per-ray work counters of one frame (untimed): exact integers, equal to
+    # the oracle's (tests/test_gpu_parity.py::test_per_ray_counters_match_oracle)
+    stat_frame = args.warmup
+    nloc = rows.nrows * W * SPP
+    st = torch.zeros(3 * nloc, dtype=torch.int32, device="cuda")
+    r.render_device(out.data_ptr(), stat_frame, rows=rows, traverse=trav, stats_ptr=st.data_ptr(),
+                    stream=sptr)
+    torch.cuda.synchronize()
+    sums = st.view(-1, 3).to(torch.int64).sum(0)
+    if dist is not None:
+        dist.all_reduce(sums)
+    n_node, n_leaf, n_tri = [int(x) for x in sums.tolist()]
+    rays_all = rays_per_frame
+    b_ray = (NODE_B * n_node + LEAF_B * n_leaf + TRI_B * n_tri) / rays_all + (FB_B + RNG_B) / SPP
+    launch_rays = rows.nrows * W * SPP
+    achieved = b_ray * launch_rays / (kernel_ms * 1e-3) / 1e9
+
+    cpu = None
+    parity_rows = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu, parity_rows = cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np)
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: 1M-triangle soup, splitmix64 seed 1, centroids U([0,2.667]x[-1,1]x[0,2]) "
+                    "+ U(-0.02,0.02)^3 vertices (SURVEY.md 8d C3)",
+            "config": {
+                "workload": f"{args.tris}-triangle random soup, {W}x{H}, {SPP} spp primary rays, "
+                            "reference camera, XORWOW seed 1984",
+                "tris": args.tris, "unique_codes": info.n_unique, "width": W, "height": H,
+                "spp": SPP, "traverse": args.traverse,
+                "parallelism": f"row bands of {args.band} rows interleaved over {world} GPU(s)"
+                               + (" + RCCL all_gather" if world > 1 else ""),
+            },
+            "kernel_ms": kernel_ms,
+            "build_ms": info.build_ms,
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "bytes_per_ray": b_ray,
+                "counters_per_ray": {"nodes": n_node / rays_all, "leaves": n_leaf / rays_all,
+                                     "tris": n_tri / rays_all},
+                "kernel": f"k_render<{'anyhit' if trav == 0 else 'reference'}>",
+            },
+            "cpu_baseline": cpu,
+            "other_traversal": ref_leg,
+        }
+        if parity_rows is not None:
+            res["parity_sample_rows_equal"] = parity_rows
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
+    """The oracle (strict-IEEE C restatement, OpenMP) on a bounded row sample
+    of the same frame; also checks those rows of the GPU frame bit-exactly."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
+        min(16, os.cpu_count() or 1)
+    ot = oracle.OracleTree(tris)
+    step = args.cpu_row_step
+    nrows = math.ceil(H / step)
+    mode = oracle.MODE_GPU_ANYHIT if trav == 0 else oracle.MODE_GPU_REF
+    img, st = ot.render(W, H, spp=SPP, frame=0, rows=(0, nrows, step), mode=mode, threads=threads)
+    # GPU frame 0, untimed, same rows
+    full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    r.render_device(full.data_ptr(), 0, traverse=trav, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    g = full.cpu().numpy().view(np.uint32).reshape(H, W)
+    same = bool(np.array_equal(g[0:H:step], img))
+    res = {"value": st.rays / st.render_seconds, "unit": "rays/s", "cores": st.threads,
+           "kind": "port",
+           "sample": f"every {step}th row of frame 0 ({nrows} rows x {W} px x {SPP} spp = "
+                     f"{st.rays} rays), oracle/bih_oracle.c "
+                     f"{'any-hit' if trav == 0 else 'reference'} traversal, OpenMP",
+           "seconds": st.render_seconds}
+    return res, same
+
+
+if __name__ == "__main__":
+    main()

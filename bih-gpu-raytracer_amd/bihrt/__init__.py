@@ -1,0 +1,170 @@
+"""bihrt -- Python host side of the MI355X BIH ray tracer.
+
+Mirrors the reference's host interface for the hot path
+(rehakvoj1/BIH-GPU-Raytracer, BIH_Raytracer/BIH_Raytracer/src):
+
+  GPUArrayManager  (GPUArrayManager.h:6-56)  -> bihrt.GPUArrayManager: owns the
+                   scene soup and the BIH on one device (bih_build/bih_rebuild)
+  Renderer.Init / Render / Launch_cudaRender (Renderer.h:18-27) ->
+                   bihrt.Renderer: camera, framebuffer, persistent RNG state,
+                   render(g_odata) per frame
+
+Everything runs through libbih_amd.so (HIP, gfx950); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import scenes  # noqa: F401
+from ._lib import (TRAVERSE_ANYHIT, TRAVERSE_REFERENCE, BihError, Camera, Framebuffer, Rows, Scene,
+                   TreeInfo, check, load)
+from . import _lib
+
+SCREEN_WIDTH, SCREEN_HEIGHT, RAYS_PER_PIXEL, SEED = 640, 480, 4, 1984   # Constants.h:4-8, :458
+
+
+def device_count() -> int:
+    return load().bih_device_count()
+
+
+def camera_reference(w: int, h: int) -> Camera:
+    cam = Camera()
+    check(load().bih_camera_reference(w, h, C.byref(cam)), "bih_camera_reference")
+    return cam
+
+
+class GPUArrayManager:
+    """Scene + BIH on one device.  `tris` is a float32 (n, 9) soup."""
+
+    def __init__(self, tris: np.ndarray, device: int = 0):
+        self.tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        self.scene = Scene(self.tris.shape[0], self.tris.ctypes.data)
+        self.device = device
+        self._tree = C.c_void_p()
+        check(load().bih_build(C.byref(self.scene), device, C.byref(self._tree)), "bih_build")
+
+    @classmethod
+    def from_device(cls, ptr: int, n_tris: int, device: int = 0, stream: int | None = None):
+        """Builds from a device-resident soup (e.g. a torch tensor's data_ptr())."""
+        self = cls.__new__(cls)
+        self.tris, self.scene, self.device = None, None, device
+        self._tree = C.c_void_p()
+        check(load().bih_build_device(C.c_void_p(ptr), n_tris, device, C.c_void_p(stream or 0),
+                                      C.byref(self._tree)), "bih_build_device")
+        return self
+
+    @property
+    def handle(self):
+        return self._tree
+
+    def rebuild(self):
+        check(load().bih_rebuild(self._tree), "bih_rebuild")
+
+    def info(self) -> TreeInfo:
+        inf = TreeInfo()
+        check(load().bih_tree_get_info(self._tree, C.byref(inf)), "bih_tree_get_info")
+        return inf
+
+    def export(self, which: int, dtype) -> np.ndarray:
+        n = C.c_size_t(0)
+        check(load().bih_tree_export(self._tree, which, None, C.byref(n)), "bih_tree_export")
+        out = np.zeros(n.value // np.dtype(dtype).itemsize, dtype)
+        check(load().bih_tree_export(self._tree, which, out.ctypes.data, C.byref(n)), "bih_tree_export")
+        return out
+
+    def arrays(self) -> dict:
+        """Canonical arrays under the oracle's names (OracleTree attributes)."""
+        a = {
+            "morton": self.export(_lib.ARR_MORTON_SORTED, np.uint32),
+            "tri_idx": self.export(_lib.ARR_TRI_INDEX, np.uint32),
+            "unique_mc": self.export(_lib.ARR_UNIQUE_MC, np.uint32),
+            "dup_cnt": self.export(_lib.ARR_DUP_COUNT, np.uint32),
+            "first_idx": self.export(_lib.ARR_FIRST_IDX, np.int32),
+            "leaf_parent": self.export(_lib.ARR_LEAF_PARENT, np.int32),
+            "clip": self.export(_lib.ARR_CLIP, np.float32).reshape(-1, 2),
+            "axis": self.export(_lib.ARR_AXIS, np.int32),
+            "children": self.export(_lib.ARR_CHILDREN, np.int32).reshape(-1, 2),
+            "is_leaf": self.export(_lib.ARR_IS_LEAF, np.uint8).reshape(-1, 2),
+            "parent": self.export(_lib.ARR_PARENT, np.int32),
+            "lo": self.export(_lib.ARR_TRI_LO, np.float32).reshape(-1, 3),
+            "hi": self.export(_lib.ARR_TRI_HI, np.float32).reshape(-1, 3),
+        }
+        inf = self.info()
+        a["scene_lo"] = np.array(inf.scene_lo[:], np.float32)
+        a["scene_hi"] = np.array(inf.scene_hi[:], np.float32)
+        return a
+
+    def close(self):
+        if getattr(self, "_tree", None) and self._tree.value:
+            load().bih_free(self._tree)
+            self._tree = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """Per-frame renderer over a GPUArrayManager (Renderer::Render, Renderer.cpp:415)."""
+
+    def __init__(self, arrays: GPUArrayManager, w: int = SCREEN_WIDTH, h: int = SCREEN_HEIGHT,
+                 spp: int = RAYS_PER_PIXEL, seed: int = SEED, camera: Camera | None = None):
+        self.arrays, self.w, self.h, self.spp, self.seed = arrays, w, h, spp, seed
+        self.camera = camera if camera is not None else camera_reference(w, h)
+        self.frame = 0
+
+    def render(self, frame: int | None = None, rows: tuple[int, int] | None = None) -> np.ndarray:
+        """One frame into a host (h, w) uint32 image (0x00BBGGRR, row 0 = bottom)."""
+        f = self.frame if frame is None else frame
+        row0, nrows = rows if rows is not None else (0, self.h)
+        out = np.zeros((nrows, self.w), np.uint32)
+        fb = Framebuffer(self.w, self.h, self.spp, f, self.seed, out.ctypes.data)
+        sc = C.byref(self.arrays.scene) if self.arrays.scene is not None else None
+        if rows is None:
+            check(load().bih_render(sc, self.arrays.handle, C.byref(self.camera), C.byref(fb)), "bih_render")
+        else:
+            check(load().bih_render_rows(sc, self.arrays.handle, C.byref(self.camera), C.byref(fb),
+                                         row0, nrows), "bih_render_rows")
+        self.frame = f + 1
+        return out
+
+    def render_device(self, out_ptr: int, frame: int, rows: Rows | None = None,
+                      traverse: int = TRAVERSE_ANYHIT, stats_ptr: int | None = None,
+                      stream: int | None = None):
+        """Asynchronous device-resident render into out_ptr (u32, nrows*w)."""
+        check(load().bih_render_device(self.arrays.handle, C.byref(self.camera), self.w, self.h,
+                                       self.spp, frame, self.seed,
+                                       C.byref(rows) if rows is not None else None, traverse,
+                                       C.c_void_p(out_ptr), C.c_void_p(stats_ptr or 0),
+                                       C.c_void_p(stream or 0)), "bih_render_device")
+
+    def sync(self, stream: int | None = None):
+        check(load().bih_sync(self.arrays.handle, C.c_void_p(stream or 0)), "bih_sync")
+
+    def last_render_ms(self) -> float:
+        ms = C.c_double(0.0)
+        check(load().bih_last_render_ms(self.arrays.handle, C.byref(ms)), "bih_last_render_ms")
+        return ms.value
+
+
+def unpack_rgba(img: np.ndarray) -> np.ndarray:
+    """0x00BBGGRR -> (..., 4) uint8 RGBA (alpha byte as stored, 0)."""
+    return img.astype("<u4").view(np.uint8).reshape(img.shape + (4,))
+
+
+def write_ppm(path: str, img: np.ndarray):
+    """PPM (P6) with row 0 at the bottom, as the GL quad shows it."""
+    rgb = unpack_rgba(img)[::-1, :, :3]
+    h, w = img.shape
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h))
+        f.write(np.ascontiguousarray(rgb).tobytes())
+
+
+__all__ = ["GPUArrayManager", "Renderer", "Camera", "Rows", "BihError", "camera_reference",
+           "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
+           "TRAVERSE_REFERENCE"]

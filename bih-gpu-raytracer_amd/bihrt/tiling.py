@@ -1,0 +1,38 @@
+"""Row tiling of one frame across ranks (one process per GPU).
+
+The frame is cut into bands of B rows dealt round-robin to the ranks
+("interleaved row bands"): the scene sits in the middle of the reference
+camera's view, so contiguous row blocks would leave the outer ranks idle.
+Every rank renders its rows with the GLOBAL pixel index (RNG subsequence and
+jitter), so the gathered frame is byte-identical to a one-GPU render.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import Rows
+
+
+def rows_of_rank(h: int, band: int, rank: int, world: int) -> np.ndarray:
+    y = np.arange(h)
+    return y[(y // band) % world == rank]
+
+
+def band_rows(h: int, band: int, rank: int, world: int) -> Rows:
+    """bih_rows for rank `rank`: local row r -> y = rank*band + (r//band)*band*world + r%band."""
+    n = int(rows_of_rank(h, band, rank, world).size)
+    return Rows(rank * band, n, band, world)
+
+
+def max_rows(h: int, band: int, world: int) -> int:
+    return max(int(rows_of_rank(h, band, r, world).size) for r in range(world))
+
+
+def assemble(parts, h: int, band: int, world: int) -> np.ndarray:
+    """Inverse of the tiling: parts[r] holds rank r's rows (padded rows ignored)."""
+    w = parts[0].shape[1]
+    out = np.zeros((h, w), parts[0].dtype)
+    for r in range(world):
+        ys = rows_of_rank(h, band, r, world)
+        out[ys] = parts[r][: ys.size]
+    return out

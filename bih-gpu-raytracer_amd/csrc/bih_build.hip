@@ -1,0 +1,654 @@
+// bih_build.hip -- per-frame BIH builder for gfx950 (MI355X).
+//
+// Replaces Renderer::Render steps 1-7 (reference src/Renderer.cpp:422-503):
+//   k_prep        per-triangle AABB + scene AABB        (App.cpp:103-142)
+//   k_morton      normalised centroid -> 30-bit Morton  (App.cpp:144-156,
+//                                                       Renderer.cpp:114-145)
+//   radix sort    stable LSD sort of (code, tri idx)    (Renderer.cpp:441-445)
+//   k_runs*       reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
+//   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710)
+//   k_fit         clip planes, bottom-up, one arrival
+//                 counter per node instead of the leaf->root atomics of
+//                 FindClipPlanes (CUDAKernels.cu:497-549): same max/min, no
+//                 root contention
+//   k_pack        16-B render nodes + sorted {v0,e1,e2} triangles
+// Everything is integer/byte work or exact f32 compares; all arithmetic is
+// compiled with -ffp-contract=off so it matches the strict-IEEE oracle.
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+#include "bih_internal.h"
+
+namespace bih {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kThreads * kScanItems;     // 2048
+constexpr int kRsItems = 16;
+constexpr int kRsTile = kThreads * kRsItems;          // 4096
+
+__device__ __forceinline__ int clz32(uint32_t x) { return x ? __clz((int)x) : 32; }
+
+// IEEE totalOrder key (-0 < +0): the order atomicMaxFloat/atomicMinFloat
+// implement (CUDAKernels.cu:52-66).
+__device__ __forceinline__ int32_t tkey(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ((int32_t)(~u) ^ (int32_t)0x80000000) : (int32_t)u;
+}
+__device__ __forceinline__ float tmax(float a, float b) { return tkey(b) > tkey(a) ? b : a; }
+__device__ __forceinline__ float tmin(float a, float b) { return tkey(b) < tkey(a) ? b : a; }
+
+// Monotone u32 key with +-0 merged: the `<` that std::minmax uses.
+__device__ __forceinline__ uint32_t lt_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) == 0u) u = 0u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// ---------------------------------------------------------------------------
+// k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
+// the scene AABB.  The reference folds triangles sequentially with
+// std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
+// as the lo of the LAST triangle attaining the minimum and sceneHi as the hi
+// of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
+// Ties only differ in the sign of zero; we reduce (value, index) keys.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
+                                                   float *__restrict__ lo, float *__restrict__ hi,
+                                                   TreeHeader *hdr) {
+    unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
+    uint32_t bad = 0;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const float *p = v + 9ull * i;
+        float q[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = p[k];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
+            bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
+            float m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
+            float M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
+            lo[3ull * i + a] = m;
+            hi[3ull * i + a] = M;
+            unsigned long long tie = 0xFFFFFFFFull - i;
+            unsigned long long km = ((unsigned long long)lt_key(m) << 32) | tie;
+            unsigned long long kM = ((unsigned long long)lt_key(M) << 32) | tie;
+            kmin[a] = km < kmin[a] ? km : kmin[a];   // smallest value, ties -> largest i
+            kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
+        }
+    }
+    // wave reduce then one atomic per wave
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long om = __shfl_xor(kmin[a], off);
+            unsigned long long oM = __shfl_xor(kmax[a], off);
+            kmin[a] = om < kmin[a] ? om : kmin[a];
+            kmax[a] = oM > kmax[a] ? oM : kmax[a];
+        }
+    }
+    unsigned long long anybad = __ballot(bad);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            atomicMin(&hdr->lo_key[a], kmin[a]);
+            atomicMax(&hdr->hi_key[a], kmax[a]);
+        }
+        if (anybad) atomicOr(&hdr->nonfinite, 1u);
+    }
+}
+
+__global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
+    int a = threadIdx.x;
+    if (a < 3) {
+        hdr->scene_lo[a] = 0.f;
+        hdr->scene_hi[a] = 0.f;
+        hdr->lo_key[a] = ~0ull;
+        hdr->hi_key[a] = 0ull;
+    }
+    if (a == 0) {
+        hdr->n_tris = n;
+        hdr->n_unique = 0;
+        hdr->nonfinite = 0;
+        hdr->pad0 = 0;
+    }
+}
+
+__global__ void k_prep_final(const float *__restrict__ v, const float *__restrict__ lo,
+                             const float *__restrict__ hi, TreeHeader *hdr, uint32_t n) {
+    int a = threadIdx.x;
+    if (a >= 3) return;
+    if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
+    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(hdr->lo_key[a] & 0xFFFFFFFFull);
+    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(hdr->hi_key[a] & 0xFFFFFFFFull);
+    hdr->scene_lo[a] = lo[3ull * ilo + a];
+    float mx = hi[3ull * ihi + a];
+    float seed = v[a];                         // first vertex (App.cpp:103-106)
+    hdr->scene_hi[a] = (seed < mx) ? mx : seed;
+    hdr->n_tris = n;
+}
+
+// ---------------------------------------------------------------------------
+// k_morton: centre (App.cpp:128-131), normalise (:144-156), morton3D
+// (Renderer.cpp:127-136).  Writes (code, index) pairs for the sort.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ lo,
+                                                     const float *__restrict__ hi,
+                                                     const TreeHeader *__restrict__ hdr, uint32_t n,
+                                                     uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float c = (lo[3ull * i + a] + hi[3ull * i + a]) / 2.0f;
+        float num = c - hdr->scene_lo[a];
+        float den = hdr->scene_hi[a] - hdr->scene_lo[a];
+        float x = (num / den) * 1024.0f;
+        q[a] = fminf(fmaxf(x, 0.0f), 1023.0f);
+    }
+    keys[i] = expand_bits((uint32_t)q[0]) * 4 + expand_bits((uint32_t)q[1]) * 2 +
+              expand_bits((uint32_t)q[2]);
+    vals[i] = i;
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scan of u32 (reduce-then-scan, 3 launches).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *lds, uint32_t *total) {
+    // 256 threads = 4 waves
+    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) lds[wave] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t s = lds[w];
+        wbase += (w < wave) ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + inc - x;
+}
+
+__global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t *__restrict__ in, uint32_t n,
+                                                          uint32_t *__restrict__ partials) {
+    __shared__ uint32_t lds[4];
+    uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        uint64_t i = base + (uint64_t)k * kThreads + threadIdx.x;
+        s += (i < n) ? in[i] : 0u;
+    }
+    uint32_t tot;
+    block_exclusive_scan(s, lds, &tot);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kThreads) k_scan_partials(uint32_t *partials, uint32_t nparts,
+                                                            uint32_t *total_out) {
+    __shared__ uint32_t lds[4];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nparts; base += kThreads) {
+        uint32_t i = base + threadIdx.x;
+        uint32_t x = i < nparts ? partials[i] : 0u;
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(x, lds, &tot);
+        if (i < nparts) partials[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+__global__ void __launch_bounds__(kThreads) k_scan_down(const uint32_t *in, uint32_t *out, uint32_t n,
+                                                        const uint32_t *__restrict__ partials) {
+    __shared__ uint32_t lds[4];
+    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint32_t x[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        uint64_t i = base + k;
+        x[k] = (i < n) ? in[i] : 0u;
+        s += x[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan(s, lds, &tot) + partials[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        uint64_t i = base + k;
+        if (i < n) out[i] = run;
+        run += x[k];
+    }
+}
+
+hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
+                          uint32_t *total_dev, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kThreads), 0, st, in, n, partials);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kThreads), 0, st, partials, nb, total_dev);
+    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(kThreads), 0, st, in, out, n, partials);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort of (key, value), 8-bit digits; 30-bit keys need
+// 4 passes.  Stability = thrust::stable_sort_by_key semantics.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_rs_hist(const uint32_t *__restrict__ keys, uint32_t n,
+                                                      int shift, uint32_t *__restrict__ hist,
+                                                      uint32_t nblocks) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+#pragma unroll 4
+    for (int k = 0; k < kRsItems; ++k) {
+        uint64_t i = base + (uint64_t)k * kThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kThreads) k_rs_scatter(const uint32_t *__restrict__ kin,
+                                                         const uint32_t *__restrict__ vin, uint32_t n,
+                                                         int shift,
+                                                         const uint32_t *__restrict__ hist_scan,
+                                                         uint32_t nblocks, uint32_t *__restrict__ kout,
+                                                         uint32_t *__restrict__ vout) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[4][256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    run[tid] = hist_scan[(uint64_t)tid * nblocks + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+    for (int r = 0; r < kRsItems; ++r) {
+        uint64_t i = base + (uint64_t)r * kThreads + tid;
+        bool valid = i < n;
+        uint32_t key = valid ? kin[i] : 0u;
+        uint32_t val = valid ? vin[i] : 0u;
+        uint32_t dg = (key >> shift) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            bool bit = (dg >> b) & 1u;
+            unsigned long long bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        uint32_t rank = __popcll(peers & lt);
+        if (valid && rank == 0) wcnt[wave][dg] = __popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t off = run[dg] + rank;
+            for (int w = 0; w < wave; ++w) off += wcnt[w][dg];
+            kout[off] = key;
+            vout[off] = val;
+        }
+        __syncthreads();
+        run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Runs of equal codes: flags, scan, compaction (reduce_by_key +
+// unique_by_key_copy, Renderer.cpp:450-472).
+// ---------------------------------------------------------------------------
+__global__ void k_run_flags(const uint32_t *__restrict__ keys, uint32_t n, uint32_t *__restrict__ flags) {
+    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_run_compact(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ flags,
+                              const uint32_t *__restrict__ pos, uint32_t n,
+                              uint32_t *__restrict__ umc, int32_t *__restrict__ first) {
+    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n && flags[i]) {
+        umc[pos[i]] = keys[i];
+        first[pos[i]] = (int32_t)i;
+    }
+}
+
+__global__ void k_run_counts(const int32_t *__restrict__ first, const TreeHeader *__restrict__ hdr,
+                             uint32_t n, uint32_t *__restrict__ cnt, int32_t *__restrict__ leaf_parent) {
+    uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    uint32_t U = hdr->n_unique;
+    if (k >= U) return;
+    int32_t e = (k + 1 < U) ? first[k + 1] : (int32_t)n;
+    cnt[k] = (uint32_t)(e - first[k]);
+    leaf_parent[k] = -1;
+}
+
+// ---------------------------------------------------------------------------
+// k_karras: BuildTree, CUDAKernels.cu:591-710, with its uint32/int mixing.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict__ umc,
+                                                     const TreeHeader *__restrict__ hdr,
+                                                     int32_t *__restrict__ children,
+                                                     uint8_t *__restrict__ is_leaf,
+                                                     int32_t *__restrict__ axis_out,
+                                                     int32_t *__restrict__ parent,
+                                                     int32_t *__restrict__ leaf_parent) {
+    const int U = (int)hdr->n_unique;
+    uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
+    if (U < 2 || idx > (uint32_t)(U - 2)) return;
+    uint32_t cur = umc[idx];
+    uint32_t pre0 = 0xFFFFFFFFu, pre1 = 0xFFFFFFFFu;
+    if (idx) pre0 = (uint32_t)clz32(cur ^ umc[idx - 1]);
+    if (idx < (uint32_t)(U - 1)) pre1 = (uint32_t)clz32(cur ^ umc[idx + 1]);
+    int32_t diff = (int32_t)(pre1 - pre0);
+    int d = (0 < diff) - (diff < 0);
+    int lcp_min = (int32_t)(((d + 1) / 2) ? pre0 : pre1);   // pre[1 - (d+1)/2]
+    int lmax = 1, lcp, li;
+    do {
+        lmax *= 2;
+        li = (int32_t)(idx + (uint32_t)(lmax * d));
+        lcp = (li < 0 || li > U - 1) ? -1 : clz32(cur ^ umc[li]);
+    } while (lcp > lcp_min);
+    int l = 0;
+    for (int t = lmax / 2; t >= 1; t /= 2) {
+        int ti = (int32_t)(idx + (uint32_t)((l + t) * d));
+        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ umc[ti]);
+        if (lcp > lcp_min) l += t;
+    }
+    int other = (int32_t)(idx + (uint32_t)(l * d));
+    int lcp_ends = clz32(cur ^ umc[other]);
+    int s = 0, t = l;
+    for (;;) {
+        t = (int)ceilf((float)t / 2.0f);           // __float2int_ru(t / 2.0f)
+        int ti = (int32_t)(idx + (uint32_t)((s + t) * d));
+        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ umc[ti]);
+        if (lcp > lcp_ends) s += t;
+        if (t == 1) break;
+    }
+    int split = (int32_t)(idx + (uint32_t)(s * d)) + (d < 0 ? d : 0);
+    children[2 * idx] = split;
+    children[2 * idx + 1] = split + 1;
+    uint32_t mn = idx < (uint32_t)other ? idx : (uint32_t)other;
+    uint32_t mx = idx > (uint32_t)other ? idx : (uint32_t)other;
+    uint8_t l0 = (mn == (uint32_t)split), l1 = (mx == (uint32_t)(split + 1));
+    is_leaf[2 * idx] = l0;
+    is_leaf[2 * idx + 1] = l1;
+    if (l0) leaf_parent[split] = (int32_t)idx; else parent[split] = (int32_t)idx;
+    if (l1) leaf_parent[split + 1] = (int32_t)idx; else parent[split + 1] = (int32_t)idx;
+    axis_out[idx] = (clz32(umc[split] ^ umc[split + 1]) + 1) % 3;
+}
+
+// ---------------------------------------------------------------------------
+// k_fit: clip planes.  Reference: every leaf walks to the root doing
+// atomicMaxFloat(clip[0], leafHi[axis]) / atomicMinFloat(clip[1],
+// leafLo[axis]) (CUDAKernels.cu:511-547), i.e. clip[0] = max over the left
+// subtree's leaves, clip[1] = min over the right subtree's leaves.  Here each
+// subtree's full AABB climbs once: a child deposits its box in the parent's
+// slot with device-scope atomics, then bumps the parent's arrival counter;
+// the second arriver reads both slots (atomics, so no cross-XCD cache
+// hand-off is involved), writes the parent's clips and climbs on.  The
+// result is the same max/min, independent of arrival order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void box_put(int32_t *slot, const float lo[3], const float hi[3]) {
+    // returning atomics whose results are consumed: the wave waits for all six
+    // to be performed before the arrival counter is bumped
+    int32_t acc = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        acc ^= atomicExch(slot + a, __float_as_int(lo[a]));
+        acc ^= atomicExch(slot + 3 + a, __float_as_int(hi[a]));
+    }
+    asm volatile("" ::"v"(acc) : "memory");
+}
+__device__ __forceinline__ void box_get(int32_t *slot, float lo[3], float hi[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = __int_as_float(atomicOr(slot + a, 0));
+        hi[a] = __int_as_float(atomicOr(slot + 3 + a, 0));
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
+                                                  const uint32_t *__restrict__ tri_idx,
+                                                  const float *__restrict__ lo,
+                                                  const float *__restrict__ hi,
+                                                  const int32_t *__restrict__ first,
+                                                  const uint32_t *__restrict__ cnt,
+                                                  const int32_t *__restrict__ leaf_parent,
+                                                  const int32_t *__restrict__ parent,
+                                                  const int32_t *__restrict__ children,
+                                                  const int32_t *__restrict__ axis,
+                                                  uint32_t *__restrict__ arrive, int32_t *box,
+                                                  float *__restrict__ clip) {
+    const uint32_t U = hdr->n_unique;
+    uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (U < 2 || k >= U) return;
+    // leaf AABB (CUDAKernels.cu:511-529)
+    int32_t f = first[k];
+    uint32_t c = cnt[k];
+    float blo[3], bhi[3];
+    uint32_t t0 = tri_idx[f];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { blo[a] = lo[3ull * t0 + a]; bhi[a] = hi[3ull * t0 + a]; }
+    for (uint32_t i = 1; i < c; ++i) {
+        uint32_t t = tri_idx[f + i];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = tmin(blo[a], lo[3ull * t + a]);
+            bhi[a] = tmax(bhi[a], hi[3ull * t + a]);
+        }
+    }
+    int32_t prev = (int32_t)k;
+    int32_t p = leaf_parent[k];
+    while (p >= 0) {
+        int side = (children[2 * p] == prev) ? 0 : 1;
+        box_put(box + (size_t)p * 12 + side * 6, blo, bhi);
+        uint32_t old = atomicAdd(arrive + p, 1u);
+        if (old == 0u) return;                      // first arriver stops
+        float slo[3], shi[3];
+        box_get(box + (size_t)p * 12 + (1 - side) * 6, slo, shi);
+        const float *lhi = side ? shi : bhi;    // left child's box is the sibling's when side==1
+        const float *rlo = side ? blo : slo;
+        int ax = axis[p];
+        clip[2 * p] = tmax(-FLT_MAX, lhi[ax]);        // initial values GPUArrayManager.cpp:79-80
+        clip[2 * p + 1] = tmin(FLT_MAX, rlo[ax]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { blo[a] = tmin(blo[a], slo[a]); bhi[a] = tmax(bhi[a], shi[a]); }
+        prev = p;
+        p = parent[p];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_pack_*: render layout (see bih_internal.h).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__restrict__ hdr,
+                                                         const float *__restrict__ clip,
+                                                         const int32_t *__restrict__ axis,
+                                                         const int32_t *__restrict__ children,
+                                                         const uint8_t *__restrict__ is_leaf,
+                                                         const int32_t *__restrict__ first,
+                                                         const uint32_t *__restrict__ cnt,
+                                                         uint4 *__restrict__ nodes) {
+    const uint32_t U = hdr->n_unique;
+    uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (U < 2 || p >= U - 1) return;
+    uint32_t split = (uint32_t)children[2 * p];
+    uint32_t lL = is_leaf[2 * p], lR = is_leaf[2 * p + 1];
+    uint32_t mid = (uint32_t)first[split + 1];
+    uint32_t cL = lL ? cnt[split] : 0u, cR = lR ? cnt[split + 1] : 0u;
+    uint32_t codeL = (cL >= 1 && cL <= 3) ? cL : 0u;
+    uint32_t codeR = (cR >= 1 && cR <= 3) ? cR : 0u;
+    uint4 nd;
+    nd.x = __float_as_uint(clip[2 * p]);
+    nd.y = __float_as_uint(clip[2 * p + 1]);
+    nd.z = split | ((uint32_t)axis[p] << 27) | (lL << 29) | (lR << 30);
+    nd.w = mid | (codeL << 27) | (codeR << 29);
+    nodes[p] = nd;
+}
+
+__global__ void __launch_bounds__(kThreads) k_pack_tris(const float *__restrict__ v,
+                                                        const uint32_t *__restrict__ tri_idx, uint32_t n,
+                                                        float *__restrict__ out) {
+    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float *p = v + 9ull * tri_idx[i];
+    float *o = out + 9ull * i;
+    float v0x = p[0], v0y = p[1], v0z = p[2];
+    o[0] = v0x; o[1] = v0y; o[2] = v0z;
+    o[3] = p[3] - v0x; o[4] = p[4] - v0y; o[5] = p[5] - v0z;   // v0v1, CUDAKernels.cu:18
+    o[6] = p[6] - v0x; o[7] = p[7] - v0y; o[8] = p[8] - v0z;   // v0v2, :19
+}
+
+inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kThreads - 1) / kThreads); }
+
+}  // namespace
+
+#define BIH_TRY(x)                                  \
+    do {                                            \
+        hipError_t e__ = (x);                       \
+        if (e__ != hipSuccess) return (int)e__;     \
+    } while (0)
+
+template <class T>
+static hipError_t dalloc(T **p, size_t count, size_t &bytes) {
+    size_t b = count * sizeof(T);
+    if (b == 0) b = 16;
+    bytes += b;
+    return hipMalloc((void **)p, b);
+}
+
+void free_tree_device(DeviceTree &t) {
+    void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
+                    t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,
+                    t.children, t.parent, t.is_leaf, t.fit_cnt, t.fit_box, t.nodes, t.tris_s,
+                    t.hist, t.partials};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    if (t.owns_v && t.v) (void)hipFree(t.v);
+    DeviceTree blank;
+    blank.device = t.device;
+    t = blank;
+}
+
+// Allocates (first call) and runs the whole build on `stream`; synchronises
+// at the end to read U back (Renderer.cpp:459 also reads the reduce_by_key
+// end pointer on the host).
+int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t n = t.n;
+    const uint64_t nn = n ? n : 1;
+    const uint32_t rs_blocks = (uint32_t)((nn + kRsTile - 1) / kRsTile);
+    const uint64_t hist_n = 256ull * rs_blocks;
+    const uint32_t max_parts =
+        (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
+    if (!t.hdr) {
+        size_t &b = t.bytes;
+        BIH_TRY(dalloc(&t.hdr, 1, b));
+        BIH_TRY(dalloc(&t.tri_lo, 3 * nn, b));
+        BIH_TRY(dalloc(&t.tri_hi, 3 * nn, b));
+        BIH_TRY(dalloc(&t.keys, nn, b));
+        BIH_TRY(dalloc(&t.vals, nn, b));
+        BIH_TRY(dalloc(&t.keys2, nn, b));
+        BIH_TRY(dalloc(&t.vals2, nn, b));
+        BIH_TRY(dalloc(&t.scan_tmp, nn + 1, b));
+        BIH_TRY(dalloc(&t.flags, nn + 1, b));
+        BIH_TRY(dalloc(&t.unique_mc, nn, b));
+        BIH_TRY(dalloc(&t.dup_cnt, nn, b));
+        BIH_TRY(dalloc(&t.first_idx, nn, b));
+        BIH_TRY(dalloc(&t.leaf_parent, nn, b));
+        BIH_TRY(dalloc(&t.clip, 2 * nn, b));
+        BIH_TRY(dalloc(&t.axis, nn, b));
+        BIH_TRY(dalloc(&t.children, 2 * nn, b));
+        BIH_TRY(dalloc(&t.parent, nn, b));
+        BIH_TRY(dalloc(&t.is_leaf, 2 * nn, b));
+        BIH_TRY(dalloc(&t.fit_cnt, nn, b));
+        BIH_TRY(dalloc(&t.fit_box, 12 * nn, b));
+        BIH_TRY(dalloc(&t.nodes, nn, b));
+        BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
+        BIH_TRY(dalloc(&t.hist, hist_n, b));
+        BIH_TRY(dalloc(&t.partials, (uint64_t)max_parts + 1, b));
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    BIH_TRY(hipEventCreate(&e0));
+    BIH_TRY(hipEventCreate(&e1));
+    BIH_TRY(hipEventRecord(e0, st));
+
+    // header reset: keys to their identities, counters to zero
+    hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
+
+    if (n > 0) {
+        uint32_t prep_blocks = blocks_for(n) < 4096u ? blocks_for(n) : 4096u;
+        hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
+                           t.tri_hi, t.hdr);
+        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(64), 0, st, t.v, t.tri_lo, t.tri_hi, t.hdr, n);
+        hipLaunchKernelGGL(k_morton, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi,
+                           t.hdr, n, t.keys, t.vals);
+        // 4 stable passes over 30-bit keys
+        uint32_t *ka = t.keys, *va = t.vals, *kb = t.keys2, *vb = t.vals2;
+        for (int shift = 0; shift < 32; shift += 8) {
+            hipLaunchKernelGGL(k_rs_hist, dim3(rs_blocks), dim3(kThreads), 0, st, ka, n, shift,
+                               t.hist, rs_blocks);
+            BIH_TRY(exclusive_scan(t.hist, t.hist, (uint32_t)hist_n, t.partials, nullptr, st));
+            hipLaunchKernelGGL(k_rs_scatter, dim3(rs_blocks), dim3(kThreads), 0, st, ka, va, n, shift,
+                               t.hist, rs_blocks, kb, vb);
+            uint32_t *tk = ka, *tv = va;
+            ka = kb; va = vb; kb = tk; vb = tv;
+        }
+        // after 4 passes the result is back in t.keys / t.vals
+        hipLaunchKernelGGL(k_run_flags, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.keys, n, t.flags);
+        BIH_TRY(exclusive_scan(t.flags, t.scan_tmp, n, t.partials, &t.hdr->n_unique, st));
+        hipLaunchKernelGGL(k_run_compact, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.keys, t.flags,
+                           t.scan_tmp, n, t.unique_mc, t.first_idx);
+        hipLaunchKernelGGL(k_run_counts, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.first_idx,
+                           t.hdr, n, t.dup_cnt, t.leaf_parent);
+        BIH_TRY(hipMemsetAsync(t.parent, 0xFF, sizeof(int32_t) * nn, st));
+        BIH_TRY(hipMemsetAsync(t.fit_cnt, 0, sizeof(uint32_t) * nn, st));
+        hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr,
+                           t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent);
+        hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.tri_lo,
+                           t.tri_hi, t.first_idx, t.dup_cnt, t.leaf_parent, t.parent, t.children,
+                           t.axis, t.fit_cnt, t.fit_box, t.clip);
+        hipLaunchKernelGGL(k_pack_nodes, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.clip,
+                           t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
+        hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.v, t.vals, n,
+                           t.tris_s);
+        BIH_TRY(hipGetLastError());
+    }
+    BIH_TRY(hipEventRecord(e1, st));
+    TreeHeader h;
+    BIH_TRY(hipMemcpyAsync(&h, t.hdr, sizeof h, hipMemcpyDeviceToHost, st));
+    BIH_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ms_out) *ms_out = ms;
+    t.u = h.n_unique;
+    if (h.nonfinite) return -1000;   // mapped to BIH_ERR_NONFINITE by the C ABI
+    return 0;
+}
+
+}  // namespace bih

@@ -1,0 +1,413 @@
+// bih_capi.cpp -- the C ABI of include/bih.h over the HIP builder/renderer.
+//
+// Mirrors the reference's host seam: GPUArrayManager owns the scene/BIH
+// buffers (src/GPUArrayManager.h:46-55), Renderer owns the framebuffer and the
+// per-pixel curandState (src/Renderer.cpp:762-797).  Here a bih_tree owns
+// both, per device, and errors are returned instead of exit(99)
+// (src/Renderer.cpp:63-73).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/bih.h"
+#include "bih_internal.h"
+
+struct bih_tree {
+    bih::DeviceTree t;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double build_ms = 0.0;
+    const float *host_v = nullptr;   // scene the tree was built from (identity check)
+    // render state cache (Renderer::d_rand_state / CreateCUDABuffers)
+    mutable std::mutex mu;
+    uint32_t *rng = nullptr;
+    size_t rng_cap = 0;              // pixels
+    uint32_t *fb = nullptr;
+    size_t fb_cap = 0;               // pixels
+    bool rng_valid = false;
+    uint32_t key_w = 0, key_spp = 0, key_row0 = 0, key_nrows = 0, key_bh = 0, key_bs = 0;
+    uint64_t key_seed = 0;
+    uint32_t next_frame = 0;
+    bool timed = false;
+    bool owns_stream = false;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int map_hip(int e) {
+    if (e == 0) return BIH_OK;
+    if (e == -1000) return BIH_ERR_NONFINITE;
+    if (e == (int)hipErrorOutOfMemory || e == (int)hipErrorMemoryAllocation) return BIH_ERR_OOM;
+    if (e == (int)hipErrorInvalidDevice || e == (int)hipErrorNoDevice) return BIH_ERR_NO_DEVICE;
+    return BIH_ERR_HIP;
+}
+
+int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return BIH_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return BIH_ERR_NO_DEVICE;
+    return BIH_OK;
+}
+
+int finish_build(bih_tree *tr) {
+    float ms = 0.f;
+    int e = bih::build_tree_device(tr->t, tr->stream, &ms);
+    tr->build_ms = ms;
+    tr->rng_valid = false;   // tree changed; RNG is independent but keep it simple
+    return map_hip(e);
+}
+
+int create_tree(int device, void *stream, bih_tree **out) {
+    bih_tree *tr = new (std::nothrow) bih_tree();
+    if (!tr) return BIH_ERR_OOM;
+    tr->t.device = device;
+    hipError_t e = hipSuccess;
+    if (stream) {
+        tr->stream = (hipStream_t)stream;
+    } else {
+        e = hipStreamCreateWithFlags(&tr->stream, hipStreamNonBlocking);
+        tr->owns_stream = (e == hipSuccess);
+    }
+    if (e == hipSuccess) e = hipEventCreate(&tr->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&tr->ev1);
+    if (e == hipSuccess && bih::upload_rng_tables(device) != 0) e = hipErrorUnknown;
+    if (e != hipSuccess) {
+        delete tr;
+        return map_hip((int)e);
+    }
+    *out = tr;
+    return BIH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bih_abi_version(void) { return BIH_ABI_VERSION; }
+
+int bih_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *bih_strerror(int code) {
+    switch (code) {
+    case BIH_OK: return "ok";
+    case BIH_ERR_INVALID: return "invalid argument";
+    case BIH_ERR_NO_DEVICE: return "no HIP device (or invalid device index)";
+    case BIH_ERR_HIP: return "HIP runtime error";
+    case BIH_ERR_OOM: return "out of memory";
+    case BIH_ERR_NONFINITE: return "scene holds a non-finite coordinate";
+    case BIH_ERR_TOO_LARGE: return "too many triangles";
+    case BIH_ERR_MISMATCH: return "scene does not match the tree";
+    default: return "unknown error";
+    }
+}
+
+// Camera(vec3(2,0,-2), (float)W/H): Renderer.cpp:99; members computed in
+// double and rounded to f32 (Camera.cu:5-9).
+int bih_camera_reference(uint32_t w, uint32_t h, bih_camera *out) {
+    if (!out || w == 0 || h == 0) return BIH_ERR_INVALID;
+    const float aspect = (float)w / (float)h;
+    const float o[3] = {2.0f, 0.0f, -2.0f};
+    for (int a = 0; a < 3; ++a) out->origin[a] = o[a];
+    out->lower_left[0] = (float)((double)o[0] - 2.0);
+    out->lower_left[1] = (float)((double)o[1] - 1.0);
+    out->lower_left[2] = (float)((double)o[2] + 1.0);
+    out->horizontal[0] = (float)((double)aspect * 2.0);
+    out->horizontal[1] = 0.0f;
+    out->horizontal[2] = 0.0f;
+    out->vertical[0] = 0.0f;
+    out->vertical[1] = 2.0f;
+    out->vertical[2] = 0.0f;
+    return BIH_OK;
+}
+
+int bih_build(const bih_scene *scene, int device, bih_tree **out) {
+    if (!scene || !out || (scene->n_tris && !scene->v)) return BIH_ERR_INVALID;
+    if (scene->n_tris > BIH_MAX_TRIS) return BIH_ERR_TOO_LARGE;
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    bih_tree *tr = nullptr;
+    rc = create_tree(device, nullptr, &tr);
+    if (rc) return rc;
+    tr->t.n = scene->n_tris;
+    tr->host_v = scene->v;
+    size_t bytes = (size_t)scene->n_tris * 36;
+    hipError_t e = hipMalloc((void **)&tr->t.v, bytes ? bytes : 16);
+    if (e == hipSuccess) {
+        tr->t.owns_v = true;
+        tr->t.bytes += bytes;
+        if (bytes) e = hipMemcpy(tr->t.v, scene->v, bytes, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        bih_free(tr);
+        return map_hip((int)e);
+    }
+    rc = finish_build(tr);
+    if (rc) {
+        bih_free(tr);
+        return rc;
+    }
+    *out = tr;
+    return BIH_OK;
+}
+
+int bih_build_device(const float *d_v, uint32_t n_tris, int device, void *stream, bih_tree **out) {
+    if (!out || (n_tris && !d_v)) return BIH_ERR_INVALID;
+    if (n_tris > BIH_MAX_TRIS) return BIH_ERR_TOO_LARGE;
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    bih_tree *tr = nullptr;
+    rc = create_tree(device, stream, &tr);
+    if (rc) return rc;
+    tr->t.n = n_tris;
+    tr->t.v = const_cast<float *>(d_v);
+    tr->t.owns_v = false;
+    rc = finish_build(tr);
+    if (rc) {
+        bih_free(tr);
+        return rc;
+    }
+    *out = tr;
+    return BIH_OK;
+}
+
+int bih_rebuild(bih_tree *tr) {
+    if (!tr) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    return finish_build(tr);
+}
+
+void bih_free(bih_tree *tr) {
+    if (!tr) return;
+    DeviceGuard g(tr->t.device);
+    if (tr->stream) (void)hipStreamSynchronize(tr->stream);
+    bih::free_tree_device(tr->t);
+    if (tr->rng) (void)hipFree(tr->rng);
+    if (tr->fb) (void)hipFree(tr->fb);
+    if (tr->ev0) (void)hipEventDestroy(tr->ev0);
+    if (tr->ev1) (void)hipEventDestroy(tr->ev1);
+    if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
+    delete tr;
+}
+
+int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
+    if (!tr || !info) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    bih::TreeHeader h;
+    if (tr->t.hdr) {
+        hipError_t e = hipMemcpy(&h, tr->t.hdr, sizeof h, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return map_hip((int)e);
+    } else {
+        memset(&h, 0, sizeof h);
+    }
+    info->n_tris = tr->t.n;
+    info->n_unique = tr->t.u;
+    for (int a = 0; a < 3; ++a) {
+        info->scene_lo[a] = h.scene_lo[a];
+        info->scene_hi[a] = h.scene_hi[a];
+    }
+    info->device = tr->t.device;
+    info->device_bytes = tr->t.bytes + (tr->rng_cap * 5 + tr->fb_cap) * 4;
+    info->build_ms = tr->build_ms;
+    return BIH_OK;
+}
+
+int bih_tree_export(const bih_tree *tr, int which, void *dst, size_t *bytes) {
+    if (!tr || !bytes) return BIH_ERR_INVALID;
+    const uint64_t N = tr->t.n, U = tr->t.u, M = U > 0 ? U - 1 : 0;
+    const void *src = nullptr;
+    size_t need = 0;
+    switch (which) {
+    case BIH_ARR_MORTON_SORTED: src = tr->t.keys; need = N * 4; break;
+    case BIH_ARR_TRI_INDEX: src = tr->t.vals; need = N * 4; break;
+    case BIH_ARR_UNIQUE_MC: src = tr->t.unique_mc; need = U * 4; break;
+    case BIH_ARR_DUP_COUNT: src = tr->t.dup_cnt; need = U * 4; break;
+    case BIH_ARR_FIRST_IDX: src = tr->t.first_idx; need = U * 4; break;
+    case BIH_ARR_LEAF_PARENT: src = tr->t.leaf_parent; need = U * 4; break;
+    case BIH_ARR_CLIP: src = tr->t.clip; need = M * 8; break;
+    case BIH_ARR_AXIS: src = tr->t.axis; need = M * 4; break;
+    case BIH_ARR_CHILDREN: src = tr->t.children; need = M * 8; break;
+    case BIH_ARR_IS_LEAF: src = tr->t.is_leaf; need = M * 2; break;
+    case BIH_ARR_PARENT: src = tr->t.parent; need = M * 4; break;
+    case BIH_ARR_TRI_LO: src = tr->t.tri_lo; need = N * 12; break;
+    case BIH_ARR_TRI_HI: src = tr->t.tri_hi; need = N * 12; break;
+    default: return BIH_ERR_INVALID;
+    }
+    if (!dst) {
+        *bytes = need;
+        return BIH_OK;
+    }
+    if (*bytes < need) return BIH_ERR_INVALID;
+    *bytes = need;
+    if (need == 0) return BIH_OK;
+    DeviceGuard g(tr->t.device);
+    hipError_t e = hipMemcpy(dst, src, need, hipMemcpyDeviceToHost);
+    return map_hip((int)e);
+}
+
+// Ensures the per-pixel RNG state for this framebuffer geometry sits at the
+// start of `frame` (InitRandGPU once, then cudaRender advances it 2*spp
+// draws per frame; a non-sequential frame re-seeds with a skip-ahead).
+static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, uint64_t seed,
+                       const bih_rows &rows, hipStream_t st) {
+    const size_t P = (size_t)rows.nrows * w;
+    if (P > tr->rng_cap) {
+        if (tr->rng) (void)hipFree(tr->rng);
+        tr->rng = nullptr;
+        tr->rng_cap = 0;
+        hipError_t e = hipMalloc((void **)&tr->rng, P * 5 * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->rng_cap = P;
+        tr->rng_valid = false;
+    }
+    bool same = tr->rng_valid && tr->key_w == w && tr->key_spp == spp && tr->key_seed == seed &&
+                tr->key_row0 == rows.row0 && tr->key_nrows == rows.nrows &&
+                tr->key_bh == rows.band_h && tr->key_bs == rows.band_step && tr->next_frame == frame;
+    if (!same) {
+        uint64_t skip = (uint64_t)2 * spp * frame;
+        int e = bih::launch_rng_init(tr->rng, w, rows.row0, rows.nrows, rows.band_h, rows.band_step,
+                                     seed, skip, tr->t.device, st);
+        if (e) return map_hip(e);
+        tr->rng_valid = true;
+        tr->key_w = w;
+        tr->key_spp = spp;
+        tr->key_seed = seed;
+        tr->key_row0 = rows.row0;
+        tr->key_nrows = rows.nrows;
+        tr->key_bh = rows.band_h;
+        tr->key_bs = rows.band_step;
+    }
+    tr->next_frame = frame + 1;
+    return BIH_OK;
+}
+
+int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
+                      uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
+                      uint32_t *d_out, uint32_t *d_ray_stats, void *stream) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0 || traverse > 1) return BIH_ERR_INVALID;
+    bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
+    if (rows.nrows == 0) return BIH_OK;
+    if (rows.band_h == 0 || rows.band_step == 0) return BIH_ERR_INVALID;
+    // the last local row must map inside the frame
+    uint64_t lr = rows.nrows - 1;
+    uint64_t ylast = rows.row0 + (lr / rows.band_h) * (uint64_t)rows.band_h * rows.band_step +
+                     (lr % rows.band_h);
+    if (ylast >= h) return BIH_ERR_INVALID;
+    if ((uint64_t)h * w > 0xFFFFFFFFull) return BIH_ERR_TOO_LARGE;
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+    int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
+    if (rc) return rc;
+    bih::RenderArgs a;
+    memcpy(a.cam, cam, sizeof a.cam);
+    a.w = w;
+    a.h = h;
+    a.spp = spp;
+    a.row0 = rows.row0;
+    a.nrows = rows.nrows;
+    a.band_h = rows.band_h;
+    a.band_step = rows.band_step;
+    uint32_t v[5], d0;
+    bih::xorwow_seed(seed, v, &d0);
+    a.d_base = d0 + (uint32_t)((uint64_t)2 * spp * frame) * 362437u;
+    a.hdr = tr->t.hdr;
+    a.nodes = tr->t.nodes;
+    a.tris = tr->t.tris_s;
+    a.dup_cnt = tr->t.dup_cnt;
+    a.rng = tr->rng;
+    a.out = d_out;
+    a.ray_stats = d_ray_stats;
+    hipError_t e = hipEventRecord(tr->ev0, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    rc = bih::launch_render(a, traverse, st);
+    if (rc) return map_hip(rc);
+    e = hipEventRecord(tr->ev1, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->timed = true;
+    return BIH_OK;
+}
+
+int bih_sync(const bih_tree *tr, void *stream) {
+    if (!tr) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+    return map_hip((int)hipStreamSynchronize(st));
+}
+
+int bih_last_render_ms(const bih_tree *tr, double *ms) {
+    if (!tr || !ms || !tr->timed) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    hipError_t e = hipEventSynchronize(tr->ev1);
+    if (e != hipSuccess) return map_hip((int)e);
+    float f = 0.f;
+    e = hipEventElapsedTime(&f, tr->ev0, tr->ev1);
+    if (e != hipSuccess) return map_hip((int)e);
+    *ms = f;
+    return BIH_OK;
+}
+
+static int render_host(const bih_scene *scene, const bih_tree *ctr, const bih_camera *cam,
+                       bih_framebuffer *fb, uint32_t row0, uint32_t nrows) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !cam || !fb || !fb->rgba) return BIH_ERR_INVALID;
+    if (scene && (scene->n_tris != tr->t.n || (tr->host_v && scene->v != tr->host_v)))
+        return BIH_ERR_MISMATCH;
+    if (fb->w == 0 || fb->h == 0 || fb->spp == 0) return BIH_ERR_INVALID;
+    if ((uint64_t)row0 + nrows > fb->h) return BIH_ERR_INVALID;
+    if (nrows == 0) return BIH_OK;
+    DeviceGuard g(tr->t.device);
+    const size_t P = (size_t)nrows * fb->w;
+    {
+        std::lock_guard<std::mutex> lk(tr->mu);
+        if (P > tr->fb_cap) {
+            if (tr->fb) (void)hipFree(tr->fb);
+            tr->fb = nullptr;
+            tr->fb_cap = 0;
+            hipError_t e = hipMalloc((void **)&tr->fb, P * 4);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->fb_cap = P;
+        }
+    }
+    bih_rows rows{row0, nrows, nrows, 1};
+    int rc = bih_render_device(tr, cam, fb->w, fb->h, fb->spp, fb->frame, fb->seed, &rows,
+                               BIH_TRAVERSE_ANYHIT, tr->fb, nullptr, nullptr);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(fb->rgba, tr->fb, P * 4, hipMemcpyDeviceToHost, tr->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(tr->stream);
+    return map_hip((int)e);
+}
+
+int bih_render(const bih_scene *scene, const bih_tree *tr, const bih_camera *cam, bih_framebuffer *fb) {
+    if (!fb) return BIH_ERR_INVALID;
+    return render_host(scene, tr, cam, fb, 0, fb->h);
+}
+
+int bih_render_rows(const bih_scene *scene, const bih_tree *tr, const bih_camera *cam,
+                    bih_framebuffer *fb, uint32_t row0, uint32_t nrows) {
+    return render_host(scene, tr, cam, fb, row0, nrows);
+}
+
+}  // extern "C"

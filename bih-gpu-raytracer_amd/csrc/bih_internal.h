@@ -1,0 +1,101 @@
+// bih_internal.h -- shared host/device definitions of libbih_amd (gfx950).
+//
+// HBM layout of one built tree (all buffers hipMalloc'd on the tree's device):
+//
+//   tris_s   f32[9N]    triangles in Morton-sorted order, rewritten as
+//                        {v0, e1 = v1-v0, e2 = v2-v0} (36 B; MT's first two
+//                        subtractions, CUDAKernels.cu:18-19, done once at build)
+//   nodes    u32x4[U-1] render node (16 B): {clip0, clip1, z, w}
+//                        z = split | axis<<27 | leafL<<29 | leafR<<30
+//                        w = mid | cntL<<27 | cntR<<29, mid = firstIdx[split+1]
+//                        left child  = internal node `split` or leaf tris
+//                                      [mid - cntL, mid); right child = node
+//                                      `split+1` or leaf tris [mid, mid + cntR);
+//                        cnt code 0 = escape, read dup_cnt[leaf] (count > 3)
+//   canonical arrays (reference names, GPUArrayManager.h:46-55) kept for the
+//   builder and for bih_tree_export: morton/tri_idx (sorted), unique_mc,
+//   dup_cnt, first_idx, leaf_parent, clip, axis, children, is_leaf, parent.
+//   rng      u32[5][P]  XORWOW v[0..4] per pixel, plane-major (the Weyl counter
+//                        d is identical for every pixel, so it is not stored).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#define BIH_HOST_DEVICE __host__ __device__
+
+namespace bih {
+
+constexpr uint32_t kIdxBits = 27;
+constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
+constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bit codes
+
+// Device-resident header written by the builder.
+struct TreeHeader {
+    float scene_lo[3];
+    float scene_hi[3];
+    uint32_t n_tris;
+    uint32_t n_unique;
+    uint32_t nonfinite;
+    uint32_t pad0;
+    unsigned long long lo_key[3];   // argmin keys (App.cpp:133-137 tie rules)
+    unsigned long long hi_key[3];   // argmax keys
+};
+
+// Render parameters, passed by value.
+struct RenderArgs {
+    float cam[12];          // origin, lower_left, horizontal, vertical
+    uint32_t w, h, spp;
+    uint32_t row0, nrows, band_h, band_step;
+    uint32_t d_base;        // XORWOW Weyl counter at the start of this frame
+    const TreeHeader *hdr;
+    const uint4 *nodes;
+    const float *tris;
+    const uint32_t *dup_cnt;
+    uint32_t *rng;          // 5 planes of nrows*w
+    uint32_t *out;          // nrows*w pixels
+    uint32_t *ray_stats;    // optional 2 u32 per ray
+};
+
+// Device buffers of one tree.
+struct DeviceTree {
+    int device = 0;
+    uint32_t n = 0, u = 0;
+    size_t bytes = 0;
+    float *v = nullptr;            // input soup f32[9N] (device copy)
+    bool owns_v = false;
+    TreeHeader *hdr = nullptr;
+    float *tri_lo = nullptr, *tri_hi = nullptr;     // f32[3N]
+    uint32_t *keys = nullptr, *vals = nullptr;      // sorted morton / tri idx
+    uint32_t *keys2 = nullptr, *vals2 = nullptr;    // sort ping-pong
+    uint32_t *scan_tmp = nullptr;                   // scan scratch
+    uint32_t *flags = nullptr;                      // u32[N+1]
+    uint32_t *unique_mc = nullptr, *dup_cnt = nullptr;
+    int32_t *first_idx = nullptr, *leaf_parent = nullptr;
+    float *clip = nullptr;
+    int32_t *axis = nullptr, *children = nullptr, *parent = nullptr;
+    uint8_t *is_leaf = nullptr;
+    uint32_t *fit_cnt = nullptr;                    // u32[U-1] arrival counters
+    int32_t *fit_box = nullptr;                     // i32[U-1][2][6] child boxes
+    uint4 *nodes = nullptr;
+    float *tris_s = nullptr;
+    uint32_t *hist = nullptr;                       // radix histograms
+    uint32_t *partials = nullptr;
+};
+
+// builder (bih_build.hip); returns hipError_t as int
+int build_tree_device(DeviceTree &t, void *stream, float *ms_out);
+void free_tree_device(DeviceTree &t);
+
+// render (bih_render.hip)
+int upload_rng_tables(int device);
+const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 step][160][5]
+int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
+                    uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
+int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
+
+// host XORWOW helpers (xorwow_host.cpp)
+void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);
+const uint32_t *xorwow_tables_host();   // same layout as rng_tables_device
+
+}  // namespace bih

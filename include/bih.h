@@ -1,0 +1,162 @@
+/*
+ * bih.h -- C ABI of the MI355X-native BIH ray tracer (libbih_amd.so).
+ *
+ * Drop-in boundary for the reference's hot path (rehakvoj1/BIH-GPU-Raytracer,
+ * paths relative to BIH_Raytracer/BIH_Raytracer/):
+ *
+ *   bih_build   replaces Renderer::Render steps 1-7 (src/Renderer.cpp:422-503:
+ *               Morton transform, stable_sort_by_key, reduce_by_key,
+ *               unique_by_key_copy, Launch_BuildTree, Launch_FindClipPlanes)
+ *               plus the host scene prep of App::LoadModels (src/App.cpp:95-164).
+ *   bih_render  replaces Renderer::Launch_cudaRender (src/Renderer.h:27,
+ *               src/CUDAKernels.cu:425-447 -> cudaRender :391-423) including the
+ *               persistent cuRAND state of InitRandGPU (:450-463) and the
+ *               framebuffer writeback g_odata[j*W+i] = rgbToInt(col) (:420-422).
+ *   bih_camera_reference  replaces `new Camera(vec3(2,0,-2), (float)W/H)`
+ *               (src/Renderer.cpp:99, src/Camera.cu:5-9).
+ *
+ * Conventions: every call is synchronous, returns 0 or a negative BIH_ERR_*
+ * code (never exits; the reference's checkCudaErrors calls exit(99),
+ * src/Renderer.cpp:63-73), and touches exactly one device (the one the tree
+ * was built on).  The caller owns scenes and host framebuffers; the library
+ * owns device memory (scene, tree, per-pixel RNG state).  Distinct trees may
+ * be used concurrently from distinct host threads.  No HIP/torch types cross
+ * this boundary: streams are passed as void* (hipStream_t), device buffers as
+ * plain pointers.
+ */
+#ifndef BIH_H
+#define BIH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BIH_ABI_VERSION 1
+
+/* error codes */
+#define BIH_OK               0
+#define BIH_ERR_INVALID     -1   /* bad argument / shape                     */
+#define BIH_ERR_NO_DEVICE   -2   /* no HIP device, or device index invalid   */
+#define BIH_ERR_HIP         -3   /* HIP runtime error                        */
+#define BIH_ERR_OOM         -4   /* device or host allocation failed         */
+#define BIH_ERR_NONFINITE   -5   /* scene holds a NaN/Inf coordinate         */
+#define BIH_ERR_TOO_LARGE   -6   /* more than BIH_MAX_TRIS triangles         */
+#define BIH_ERR_MISMATCH    -7   /* scene does not belong to this tree       */
+
+#define BIH_MAX_TRIS (1u << 27)
+
+/* Triangle soup, file order (App.cpp:108-121 flattening): v[9*i .. 9*i+8] =
+ * v0.xyz, v1.xyz, v2.xyz of triangle i.  Host-owned. */
+typedef struct bih_scene {
+    uint32_t n_tris;
+    const float *v;
+} bih_scene;
+
+/* Opaque BIH; built by bih_build*, owned by the library, freed by bih_free. */
+typedef struct bih_tree bih_tree;
+
+/* == Camera members m_origin, m_lowerLeftCorner, m_horizontal, m_vertical
+ * (src/Camera.h:14-17).  Ray(u,v) = Ray(origin,
+ * lower_left + u*horizontal + v*vertical - origin), Camera.cu:18-20. */
+typedef struct bih_camera {
+    float origin[3], lower_left[3], horizontal[3], vertical[3];
+} bih_camera;
+
+/* Host framebuffer: w*h uint32 0x00BBGGRR, row 0 = bottom (GL convention).
+ * Frame f consumes cuRAND draws [2*spp*f, 2*spp*(f+1)) of the XORWOW
+ * subsequence `pixel = y*w + x` seeded with `seed` (reference: 1984). */
+typedef struct bih_framebuffer {
+    uint32_t w, h, spp, frame;
+    uint64_t seed;
+    uint32_t *rgba;
+} bih_framebuffer;
+
+/* Traversal flavours; both produce bit-identical RGBA.
+ * BIH_TRAVERSE_REFERENCE visits exactly the nodes/leaves/triangles of
+ * TraverseTree (CUDAKernels.cu:227-368); BIH_TRAVERSE_ANYHIT (default) runs
+ * the same walk but stops at the first triangle that sets rec.triangleIdx,
+ * which is all Color() (:370-389) consumes. */
+#define BIH_TRAVERSE_ANYHIT     0u
+#define BIH_TRAVERSE_REFERENCE  1u
+
+/* Row tiling for bih_render_device: local row r (0 <= r < nrows) is global
+ * row y = row0 + (r / band_h) * band_h * band_step + (r % band_h).
+ * {row0, nrows, band_h=nrows, band_step=1} = contiguous block;
+ * {rank*B, rows_of_rank, B, world} = interleaved bands of B rows. */
+typedef struct bih_rows {
+    uint32_t row0, nrows, band_h, band_step;
+} bih_rows;
+
+typedef struct bih_tree_info {
+    uint32_t n_tris, n_unique;            /* N, U (U-1 internal nodes)        */
+    float scene_lo[3], scene_hi[3];       /* App.cpp:133-137 scene AABB        */
+    int device;
+    uint64_t device_bytes;                /* device memory held by the tree    */
+    double build_ms;                      /* device time of the last build     */
+} bih_tree_info;
+
+/* Canonical arrays for parity checks (reference buffer names in brackets). */
+enum bih_array {
+    BIH_ARR_MORTON_SORTED = 0, /* u32[N]  [m_mortonCodes after sort]          */
+    BIH_ARR_TRI_INDEX,         /* u32[N]  [m_trisIndexes]                      */
+    BIH_ARR_UNIQUE_MC,         /* u32[U]  [m_uniqueMortonCodes]                */
+    BIH_ARR_DUP_COUNT,         /* u32[U]  [m_duplicatesCnts]                   */
+    BIH_ARR_FIRST_IDX,         /* i32[U]  [m_firstIdxs]                        */
+    BIH_ARR_LEAF_PARENT,       /* i32[U]  [m_leafParents]                      */
+    BIH_ARR_CLIP,              /* f32[2*(U-1)] [TreeInternalNode::t_clipPlanes]*/
+    BIH_ARR_AXIS,              /* i32[U-1]    [t_axis]                         */
+    BIH_ARR_CHILDREN,          /* i32[2*(U-1)] [children]                      */
+    BIH_ARR_IS_LEAF,           /* u8[2*(U-1)]  [isLeaf]                        */
+    BIH_ARR_PARENT,            /* i32[U-1]    [parent]                         */
+    BIH_ARR_TRI_LO,            /* f32[3N] [AABBs::arrLo]                       */
+    BIH_ARR_TRI_HI,            /* f32[3N] [AABBs::arrHi]                       */
+    BIH_ARR_COUNT
+};
+
+int bih_device_count(void);
+const char *bih_strerror(int code);
+int bih_abi_version(void);
+
+int bih_camera_reference(uint32_t w, uint32_t h, bih_camera *out);
+
+/* Build from a host soup (copied H2D) or a device-resident soup. */
+int bih_build(const bih_scene *scene, int device, bih_tree **out);
+int bih_build_device(const float *d_v, uint32_t n_tris, int device, void *stream,
+                     bih_tree **out);
+/* Rebuild in place (per-frame rebuild as in Renderer::Render). */
+int bih_rebuild(bih_tree *tree);
+void bih_free(bih_tree *tree);
+
+int bih_tree_get_info(const bih_tree *tree, bih_tree_info *info);
+/* Copies one canonical array to host memory; *bytes in/out. */
+int bih_tree_export(const bih_tree *tree, int which, void *host_dst, size_t *bytes);
+
+/* Full frame into a host framebuffer (reference render() entry point). */
+int bih_render(const bih_scene *scene, const bih_tree *tree, const bih_camera *camera,
+               bih_framebuffer *fb);
+/* Rows [row0, row0+nrows) into fb->rgba[(y-row0)*w + x]; RNG subsequence and
+ * jitter use the GLOBAL pixel index, so tiles reassemble the full frame. */
+int bih_render_rows(const bih_scene *scene, const bih_tree *tree, const bih_camera *camera,
+                    bih_framebuffer *fb, uint32_t row0, uint32_t nrows);
+
+/* Device-resident render (bench / multi-GPU): writes nrows*w pixels to d_out
+ * (device memory on the tree's device) in local row order, on `stream`
+ * (NULL = the tree's stream), asynchronously; bih_sync waits for it.
+ * traverse = BIH_TRAVERSE_*.  d_ray_stats (optional, device u32[2*rays]) gets
+ * per-ray {node visits, triangle tests} for parity checks against the oracle. */
+int bih_render_device(const bih_tree *tree, const bih_camera *camera, uint32_t w, uint32_t h,
+                      uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows,
+                      uint32_t traverse, uint32_t *d_out, uint32_t *d_ray_stats, void *stream);
+int bih_sync(const bih_tree *tree, void *stream);
+
+/* Device time (ms, HIP events on the render stream) of the last render
+ * kernel launched through this tree. */
+int bih_last_render_ms(const bih_tree *tree, double *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BIH_H */

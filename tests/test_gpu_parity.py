@@ -1,0 +1,165 @@
+"""GPU parity: the HIP builder and renderer (through the C ABI) against the
+strict-IEEE oracle, bit-exact (integer/index/RGBA work and exact f32)."""
+import numpy as np
+import pytest
+
+from conftest import edge_scenes
+
+pytestmark = pytest.mark.gpu
+
+TREE_KEYS = ["morton", "tri_idx", "unique_mc", "dup_cnt", "first_idx", "leaf_parent", "clip",
+             "axis", "children", "is_leaf", "parent", "lo", "hi", "scene_lo", "scene_hi"]
+
+
+def _tree_equal(gpu_arrays, ot):
+    for k in TREE_KEYS:
+        a = gpu_arrays[k]
+        b = getattr(ot, k)
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        # bitwise for floats (distinguishes -0/+0)
+        if a.dtype == np.float32:
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+        else:
+            assert np.array_equal(a, b), k
+
+
+SCENES = edge_scenes()
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_build_matches_oracle_edge(name, gpu, bihrt_mod, oracle_mod):
+    tris = SCENES[name]
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    assert g.info().n_unique == ot.U
+    _tree_equal(g.arrays(), ot)
+
+
+@pytest.mark.parametrize("n,seed", [(1000, 11), (70_000, 1), (300_000, 2)])
+def test_build_matches_oracle_soup(n, seed, gpu, bihrt_mod, oracle_mod):
+    tris = bihrt_mod.scenes.soup(n, seed=seed)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    _tree_equal(g.arrays(), ot)
+
+
+def test_build_torus(gpu, bihrt_mod, oracle_mod):
+    tris = bihrt_mod.scenes.torus()
+    _tree_equal(bihrt_mod.GPUArrayManager(tris).arrays(), oracle_mod.OracleTree(tris))
+
+
+def test_rebuild_deterministic(gpu, bihrt_mod):
+    tris = bihrt_mod.scenes.soup(50_000, seed=9)
+    g = bihrt_mod.GPUArrayManager(tris)
+    a = g.arrays()
+    g.rebuild()
+    b = g.arrays()
+    for k in TREE_KEYS:
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+
+
+@pytest.mark.parametrize("name", ["cornell", "dodeca", "clustered", "signed_zero", "one_tri",
+                                  "dup_all", "flat_z"])
+@pytest.mark.parametrize("w,h,spp", [(64, 48, 4), (37, 29, 3)])
+def test_render_matches_oracle_small(name, w, h, spp, gpu, bihrt_mod, oracle_mod):
+    tris = SCENES[name]
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    r = bihrt_mod.Renderer(g, w, h, spp=spp, seed=1984)
+    for frame in range(3):
+        img = r.render(frame)
+        ref, _ = ot.render(w, h, spp=spp, frame=frame, seed=1984)
+        assert np.array_equal(img, ref), (name, frame)
+
+
+def test_cornell_256_frames(gpu, bihrt_mod, oracle_mod):
+    tris = bihrt_mod.scenes.cornell()
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    r = bihrt_mod.Renderer(g, 256, 256)
+    # sequential frames reuse the advanced RNG state; frame 7 re-seeds with a skip-ahead
+    for frame in (0, 1, 2, 7, 8):
+        img = r.render(frame)
+        ref, _ = ot.render(256, 256, frame=frame)
+        assert np.array_equal(img, ref), frame
+
+
+def test_render_rows_tile_reassembles(gpu, bihrt_mod, oracle_mod):
+    tris = bihrt_mod.scenes.torus()
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, 192, 108)
+    full = r.render(0)
+    parts = [bihrt_mod.Renderer(g, 192, 108).render(0, rows=(y, 27)) for y in range(0, 108, 27)]
+    assert np.array_equal(np.concatenate(parts, 0), full)
+    ref, _ = oracle_mod.OracleTree(tris).render(192, 108)
+    assert np.array_equal(full, ref)
+
+
+def _device_render(bihrt, g, w, h, spp, frame, traverse, rows=None, stats=False):
+    import torch
+    nrows = rows.nrows if rows is not None else h
+    out = torch.zeros(nrows * w, dtype=torch.int32, device="cuda")
+    st = torch.zeros(3 * nrows * w * spp, dtype=torch.int32, device="cuda") if stats else None
+    r = bihrt.Renderer(g, w, h, spp=spp)
+    r.render_device(out.data_ptr(), frame, rows=rows, traverse=traverse,
+                    stats_ptr=st.data_ptr() if stats else None)
+    r.sync()
+    img = out.cpu().numpy().view(np.uint32).reshape(nrows, w)
+    if stats:
+        s = st.cpu().numpy().view(np.uint32).reshape(-1, 3)
+        return img, s
+    return img
+
+
+@pytest.mark.parametrize("scene", ["torus", "soup"])
+def test_per_ray_counters_match_oracle(scene, gpu, bihrt_mod, oracle_mod):
+    """The HIP walk visits exactly the reference's nodes and triangles
+    (TRAVERSE_REFERENCE) / the oracle's any-hit prefix of them (ANYHIT)."""
+    tris = bihrt_mod.scenes.torus() if scene == "torus" else bihrt_mod.scenes.soup(60_000, seed=4)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h, spp = 96, 54, 4
+    for traverse, mode in ((bihrt_mod.TRAVERSE_REFERENCE, oracle_mod.MODE_GPU_REF),
+                           (bihrt_mod.TRAVERSE_ANYHIT, oracle_mod.MODE_GPU_ANYHIT)):
+        img, s = _device_render(bihrt_mod, g, w, h, spp, 0, traverse, stats=True)
+        ref, _, rs = ot.render(w, h, spp=spp, mode=mode, ray_stats=True)
+        assert np.array_equal(img, ref)
+        assert np.array_equal(s[:, 0], rs[:, 0]), "node visits differ"
+        assert np.array_equal(s[:, 1], rs[:, 1]), "leaf visits differ"
+        assert np.array_equal(s[:, 2], rs[:, 2]), "triangle tests differ"
+
+
+def test_interleaved_bands(gpu, bihrt_mod, oracle_mod):
+    """Row bands as bench.py's multi-GPU tiling uses them."""
+    tris = bihrt_mod.scenes.soup(40_000, seed=6)
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h, world, B = 160, 90, 3, 8
+    full = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_ANYHIT)
+    ref, _ = oracle_mod.OracleTree(tris).render(w, h)
+    assert np.array_equal(full, ref)
+    from bihrt.tiling import band_rows, rows_of_rank
+    for rank in range(world):
+        rows = band_rows(h, B, rank, world)
+        img = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_ANYHIT, rows=rows)
+        ys = rows_of_rank(h, B, rank, world)
+        assert np.array_equal(img, full[ys])
+
+
+def test_1m_1080p_properties(gpu, bihrt_mod, oracle_mod):
+    """Full BASELINE size: both traversals agree on every pixel; sampled rows
+    equal the oracle; re-render of the same frame is identical."""
+    tris = bihrt_mod.scenes.soup(1_000_000, seed=1)
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 1920, 1080
+    a = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_ANYHIT)
+    b = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_REFERENCE)
+    assert np.array_equal(a, b)
+    ot = oracle_mod.OracleTree(tris)
+    rows = (311, 6, 97)   # 6 rows spread over the frame
+    ref, _ = ot.render(w, h, rows=rows, mode=oracle_mod.MODE_GPU_ANYHIT)
+    ys = [311 + 97 * k for k in range(6)]
+    assert np.array_equal(a[ys], ref)
+    vals = np.unique(a)
+    # k of 4 samples hit -> floor((255k + 20(4-k))/4), B = 10(4-k) (CUDAKernels.cu:384-388, :420)
+    assert set(vals.tolist()) <= {0x281414, 0x1e4e4e, 0x148989, 0x0ac4c4, 0x00ffff}, \
+        [hex(x) for x in vals]
