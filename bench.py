@@ -67,7 +67,9 @@ def main():
     from bihrt.tiling import band_rows, max_rows, rows_of_rank
 
     W, H, SPP = args.width, args.height, args.spp
-    stream = torch.cuda.current_stream()
+    # one explicit stream for build, render, events and the all-gather
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
     # scene: generated on the host (deterministic), resident in HBM before timing

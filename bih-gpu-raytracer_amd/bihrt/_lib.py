@@ -12,7 +12,7 @@ import re
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libbih_amd.so")
+LIB_PATH = os.environ.get("BIH_LIB") or os.path.join(PKG_DIR, "lib", "libbih_amd.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "bih.h")
 
 BIH_OK = 0
@@ -87,6 +87,14 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise OSError(f"{LIB_PATH} not built: run `make -C bih-gpu-raytracer_amd` "
                       "(or __graft_entry__.build())")
+    # One HIP runtime per process: the torch wheel bundles its own
+    # libamdhip64 (soname libamdhip64.so.7, NEEDED as "libamdhip64.so"), so
+    # if torch is present it is loaded first and libbih_amd.so binds to that
+    # same runtime instead of pulling in a second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
     L.bih_abi_version.restype = i32

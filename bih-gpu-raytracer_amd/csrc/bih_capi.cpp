@@ -26,6 +26,7 @@ struct bih_tree {
     mutable std::mutex mu;
     uint32_t *rng = nullptr;
     size_t rng_cap = 0;              // pixels
+    int rng_cur = 0;                 // which XORWOW buffer holds the next frame's input
     uint32_t *fb = nullptr;
     size_t fb_cap = 0;               // pixels
     bool rng_valid = false;
@@ -34,6 +35,8 @@ struct bih_tree {
     uint32_t next_frame = 0;
     bool timed = false;
     bool owns_stream = false;
+    uint32_t *work = nullptr;        // persistent-kernel tile counter
+    uint32_t *spill = nullptr;       // traversal stack spill area
 };
 
 namespace {
@@ -205,6 +208,8 @@ void bih_free(bih_tree *tr) {
     bih::free_tree_device(tr->t);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
+    if (tr->work) (void)hipFree(tr->work);
+    if (tr->spill) (void)hipFree(tr->spill);
     if (tr->ev0) (void)hipEventDestroy(tr->ev0);
     if (tr->ev1) (void)hipEventDestroy(tr->ev1);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
@@ -273,12 +278,15 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
                        const bih_rows &rows, hipStream_t st) {
     const size_t P = (size_t)rows.nrows * w;
     if (P > tr->rng_cap) {
+        // layout: [2][5][cap] XORWOW planes (in/out, swapped per frame) + [cap] pixel accumulators
         if (tr->rng) (void)hipFree(tr->rng);
         tr->rng = nullptr;
         tr->rng_cap = 0;
-        hipError_t e = hipMalloc((void **)&tr->rng, P * 5 * sizeof(uint32_t));
+        hipError_t e = hipMalloc((void **)&tr->rng, P * 11 * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(tr->rng + 10 * P, 0, P * sizeof(uint32_t), st);
         if (e != hipSuccess) return map_hip((int)e);
         tr->rng_cap = P;
+        tr->rng_cur = 0;
         tr->rng_valid = false;
     }
     bool same = tr->rng_valid && tr->key_w == w && tr->key_spp == spp && tr->key_seed == seed &&
@@ -286,7 +294,8 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
                 tr->key_bh == rows.band_h && tr->key_bs == rows.band_step && tr->next_frame == frame;
     if (!same) {
         uint64_t skip = (uint64_t)2 * spp * frame;
-        int e = bih::launch_rng_init(tr->rng, w, rows.row0, rows.nrows, rows.band_h, rows.band_step,
+        int e = bih::launch_rng_init(tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap, w, rows.row0,
+                                     rows.nrows, rows.band_h, rows.band_step,
                                      seed, skip, tr->t.device, st);
         if (e) return map_hip(e);
         tr->rng_valid = true;
@@ -319,6 +328,19 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+    if (!tr->work) {
+        hipError_t e = hipMalloc((void **)&tr->work, 64);
+        if (e == hipSuccess)
+            e = hipMalloc((void **)&tr->spill,
+                          bih::spill_words(bih::wave_grid_blocks(tr->t.device)) * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    // renders through one tree share its RNG state, tile counter and spill
+    // area: order this launch after the previous one, whatever the stream
+    if (tr->timed) {
+        hipError_t e = hipStreamWaitEvent(st, tr->ev1, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
     bih::RenderArgs a;
@@ -337,9 +359,15 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
     a.dup_cnt = tr->t.dup_cnt;
-    a.rng = tr->rng;
+    const size_t P = (size_t)rows.nrows * w;
+    a.rng_in = tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap;
+    a.rng_out = tr->rng + (size_t)(1 - tr->rng_cur) * 5 * tr->rng_cap;
+    a.pixacc = tr->rng + (size_t)10 * tr->rng_cap;
+    (void)P;
     a.out = d_out;
     a.ray_stats = d_ray_stats;
+    a.work = tr->work;
+    a.spill = tr->spill;
     hipError_t e = hipEventRecord(tr->ev0, st);
     if (e != hipSuccess) return map_hip((int)e);
     rc = bih::launch_render(a, traverse, st);
@@ -347,6 +375,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     e = hipEventRecord(tr->ev1, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->timed = true;
+    tr->rng_cur = 1 - tr->rng_cur;   // this frame's output state feeds the next frame
     return BIH_OK;
 }
 

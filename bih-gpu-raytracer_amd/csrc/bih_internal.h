@@ -29,6 +29,12 @@ namespace bih {
 constexpr uint32_t kIdxBits = 27;
 constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
 constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bit codes
+#ifndef BIH_LDS_STACK
+#define BIH_LDS_STACK 10
+#endif
+// stack entries per lane held in LDS (12 B each); deeper ones spill to HBM.
+// 1M-tri soup @1080p: 0.8 % of pushes land in slot >= 10 (12 % at >= 8).
+constexpr int kLdsStack = BIH_LDS_STACK;
 
 // Device-resident header written by the builder.
 struct TreeHeader {
@@ -52,9 +58,14 @@ struct RenderArgs {
     const uint4 *nodes;
     const float *tris;
     const uint32_t *dup_cnt;
-    uint32_t *rng;          // 5 planes of nrows*w
+    const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame
+    uint32_t *rng_out;      // state after the frame (double-buffered: a pixel's
+                            // samples may run in different waves)
+    uint32_t *pixacc;       // per-pixel {hits<<16 | samples} of the refill kernel (kept 0)
     uint32_t *out;          // nrows*w pixels
-    uint32_t *ray_stats;    // optional 2 u32 per ray
+    uint32_t *ray_stats;    // optional 3 u32 per ray {nodes, leaves, tris}
+    uint32_t *work;         // tile counter of the persistent kernel (zeroed per launch)
+    uint32_t *spill;        // per-lane stack spill area (spill_words(grid) u32)
 };
 
 // Device buffers of one tree.
@@ -93,6 +104,8 @@ const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 s
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
+uint32_t wave_grid_blocks(int device);     // persistent grid of k_render_wave
+size_t spill_words(uint32_t blocks);
 
 // host XORWOW helpers (xorwow_host.cpp)
 void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);

@@ -1,4 +1,4 @@
-// bih_render.hip -- primary-ray render kernel for gfx950 (MI355X).
+// bih_render.hip -- primary-ray render kernels for gfx950 (MI355X).
 //
 // Replaces cudaRender (reference src/CUDAKernels.cu:391-423) and its callees
 // Camera::GetRay (Camera.cu:18-20), Ray::Ray (Ray.cu:3-10), Color (:370-389),
@@ -11,8 +11,26 @@
 // the strict-IEEE oracle.  `det < 0.000001` (a double compare) is the f32
 // compare det <= 0x1.0c6f7ap-20f; `1.0 / det` rounded to f32 is the correctly
 // rounded f32 reciprocal (double rounding is innocuous for division).
+//
+// Kernels
+//   k_render_tile    persistent waves; a wave takes a tile of 64/spp pixels x
+//                    spp samples (lane = one ray), walks until all 64 rays end,
+//                    combines each pixel's samples with one ballot.
+//   k_render_refill  persistent waves; a lane that finishes its ray takes the
+//                    next ray id from a global counter (wave-aggregated
+//                    atomic), so SIMD lanes stay busy; pixels are combined
+//                    with a per-pixel atomic hit counter.
+//   k_render_pixel   any spp: one lane per pixel, samples in sequence.
+// The traversal core (Walker) is shared: it makes the reference's 4-way
+// decision per node, queues the node's tested leaves (at most two) and tests
+// their triangles before fetching the next node, so the visit order and the
+// per-ray counters equal TraverseTree's.  The stack keeps its first
+// kLdsStack entries per lane in LDS ([entry][lane], conflict-free) and spills
+// deeper ones to a per-lane HBM area.
 #include <hip/hip_runtime.h>
 #include <float.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <mutex>
 
@@ -24,9 +42,17 @@ namespace {
 constexpr int kThreads = 256;
 constexpr float kDetEps = 9.99999997475242708e-07f;   // 0x358637bd: largest f32 < 1e-6
 constexpr uint32_t kWeyl = 362437u;
+constexpr uint32_t kDone = 0xFFFFFFFFu;
+
+#ifndef BIH_MT_EARLY_OUT
+#define BIH_MT_EARLY_OUT 1      // return at the back-face test (else fully predicated MT)
+#endif
+#ifndef BIH_SPILL_NT
+#define BIH_SPILL_NT 0          // non-temporal loads/stores for the HBM stack slots
+#endif
 
 // ---------------------------------------------------------------------------
-// RNG init: v = M^skip * J^pixel * seed_state (J = M^(2^67)).
+// RNG: v = M^skip * J^pixel * seed_state (J = M^(2^67)), cuRAND XORWOW.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void gf2_apply(const uint32_t *__restrict__ m, uint32_t x[5]) {
     uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
@@ -68,161 +94,6 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
     for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
 }
 
-// ---------------------------------------------------------------------------
-// Traversal
-// ---------------------------------------------------------------------------
-struct Ray {
-    float o[3], d[3], inv[3];
-    uint32_t sgn[3];
-};
-
-__device__ __forceinline__ float pick3(const float v[3], uint32_t a) {
-    return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]);
-}
-__device__ __forceinline__ uint32_t pick3u(const uint32_t v[3], uint32_t a) {
-    return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]);
-}
-
-// RayTriangleIntersection + the t>0 && t<rec.t record test of
-// FindNearestTriangle.  Returns true when the triangle sets rec.triangleIdx.
-// With rec.t starting at FLT_MAX (Color, :380-382) "some triangle was
-// recorded" == "some tested triangle has MT true and 0 < t < FLT_MAX".
-__device__ __forceinline__ bool tri_hit(const float *__restrict__ tp, const Ray &r) {
-    float v0x = tp[0], v0y = tp[1], v0z = tp[2];
-    float e1x = tp[3], e1y = tp[4], e1z = tp[5];
-    float e2x = tp[6], e2y = tp[7], e2z = tp[8];
-    // pvec = cross(D, e2)
-    float px = r.d[1] * e2z - e2y * r.d[2];
-    float py = r.d[2] * e2x - e2z * r.d[0];
-    float pz = r.d[0] * e2y - e2x * r.d[1];
-    float det = (e1x * px + e1y * py) + e1z * pz;
-    if (det <= kDetEps) return false;      // det < 0.000001 (double), NaN passes
-    float inv = 1.0f / det;
-    float sx = r.o[0] - v0x, sy = r.o[1] - v0y, sz = r.o[2] - v0z;
-    float u = ((sx * px + sy * py) + sz * pz) * inv;
-    if (u < 0.0f || u > 1.0f) return false;
-    // qvec = cross(tvec, e1)
-    float qx = sy * e1z - e1y * sz;
-    float qy = sz * e1x - e1z * sx;
-    float qz = sx * e1y - e1x * sy;
-    float v = ((r.d[0] * qx + r.d[1] * qy) + r.d[2] * qz) * inv;
-    if (v < 0.0f || u + v > 1.0f) return false;
-    float t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
-    return t > 0.0f && t < FLT_MAX;
-}
-
-// per-ray work counters (parity evidence + algorithmic bytes, SURVEY 8d)
-struct Cnt {
-    uint32_t nodes, leaves, tris;
-};
-
-template <bool ANYHIT, bool STATS>
-__device__ __forceinline__ bool leaf_test(const float *__restrict__ tris, uint32_t begin, uint32_t count,
-                                          const Ray &r, Cnt &cnt) {
-    bool hit = false;
-    if (STATS) ++cnt.leaves;
-    for (uint32_t i = 0; i < count; ++i) {
-        if (STATS) ++cnt.tris;
-        if (tri_hit(tris + 9ull * (begin + i), r)) {
-            hit = true;
-            if (ANYHIT) break;
-        }
-    }
-    return hit;
-}
-
-template <bool ANYHIT, bool STATS>
-__device__ bool trace(const RenderArgs &a, const Ray &r, const float slo[3], const float shi[3],
-                      uint32_t U, uint32_t N, Cnt &cnt) {
-    // scene AABB slab test, CUDAKernels.cu:237-262 (tMin may be negative)
-    float tMin = ((r.sgn[0] ? shi[0] : slo[0]) - r.o[0]) * r.inv[0];
-    float tMax = ((r.sgn[0] ? slo[0] : shi[0]) - r.o[0]) * r.inv[0];
-    float tymin = ((r.sgn[1] ? shi[1] : slo[1]) - r.o[1]) * r.inv[1];
-    float tymax = ((r.sgn[1] ? slo[1] : shi[1]) - r.o[1]) * r.inv[1];
-    if ((tMin > tymax) || (tymin > tMax)) return false;
-    if (tymin > tMin) tMin = tymin;
-    if (tymax < tMax) tMax = tymax;
-    float tzmin = ((r.sgn[2] ? shi[2] : slo[2]) - r.o[2]) * r.inv[2];
-    float tzmax = ((r.sgn[2] ? slo[2] : shi[2]) - r.o[2]) * r.inv[2];
-    if ((tMin > tzmax) || (tzmin > tMax)) return false;
-    if (tzmin > tMin) tMin = tzmin;
-    if (tzmax < tMax) tMax = tzmax;
-    if (U == 0) return false;
-    if (U == 1) return leaf_test<ANYHIT, STATS>(a.tris, 0, N, r, cnt);   // reference: UB
-
-    uint32_t st_node[kStackDepth];
-    float st_min[kStackDepth], st_max[kStackDepth];
-    int sp = 0;
-    uint32_t cur = 0;
-    bool hit = false;
-    for (;;) {
-        if (STATS) ++cnt.nodes;
-        const uint4 nd = a.nodes[cur];
-        const uint32_t ax = (nd.z >> 27) & 3u;
-        const float org = pick3(r.o, ax), inv = pick3(r.inv, ax);
-        const uint32_t nr = pick3u(r.sgn, ax);
-        const float t0 = (__uint_as_float(nd.x) - org) * inv;
-        const float t1 = (__uint_as_float(nd.y) - org) * inv;
-        const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
-        const bool A = tMin < tn, B = tMax < tf;
-        const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
-        const uint32_t leafL = (nd.z >> 29) & 1u, leafR = (nd.z >> 30) & 1u;
-        const uint32_t leafN = nr ? leafR : leafL, leafF = nr ? leafL : leafR;
-        const uint32_t idxN = split + nr, idxF = split + 1u - nr;
-        // leaf ranges of the near / far child
-        auto leaf_range = [&](uint32_t right, uint32_t &beg, uint32_t &cnt) {
-            uint32_t code = right ? (nd.w >> 29) & 3u : (nd.w >> 27) & 3u;
-            cnt = code ? code : a.dup_cnt[split + right];
-            beg = right ? mid : mid - cnt;
-        };
-        bool pop = false;
-        if (!A && B) {
-            pop = true;
-        } else if (A && B) {
-            if (leafN) {
-                uint32_t b, c; leaf_range(nr, b, c);
-                hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                pop = true;
-            } else { cur = idxN; tMax = tn; }
-        } else if (!A && !B) {
-            if (leafF) {
-                uint32_t b, c; leaf_range(1u - nr, b, c);
-                hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                pop = true;
-            } else { cur = idxF; tMin = tf; }
-        } else {
-            if (leafN && leafF) {
-                uint32_t b, c; leaf_range(nr, b, c);
-                hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                if (!(ANYHIT && hit)) {
-                    leaf_range(1u - nr, b, c);
-                    hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                }
-                pop = true;
-            } else if (!leafN && leafF) {
-                uint32_t b, c; leaf_range(1u - nr, b, c);
-                hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                cur = idxN; tMax = tn;
-            } else if (leafN && !leafF) {
-                uint32_t b, c; leaf_range(nr, b, c);
-                hit |= leaf_test<ANYHIT, STATS>(a.tris, b, c, r, cnt);
-                cur = idxF; tMin = tf;
-            } else {
-                st_node[sp] = idxF; st_min[sp] = tf; st_max[sp] = tMax;
-                ++sp;
-                cur = idxN; tMax = tn;
-            }
-        }
-        if (ANYHIT && hit) break;
-        if (pop) {
-            if (sp == 0) break;
-            --sp;
-            cur = st_node[sp]; tMin = st_min[sp]; tMax = st_max[sp];
-        }
-    }
-    return hit;
-}
-
 __device__ __forceinline__ float xorwow_uniform(uint32_t v[5], uint32_t &d) {
     uint32_t t = v[0] ^ (v[0] >> 2);
     v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
@@ -239,65 +110,770 @@ __device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
     return ((uint32_t)(int)b << 16) | ((uint32_t)(int)g << 8) | (uint32_t)(int)r;
 }
 
-// One wave = one 8x8 pixel tile (coherent primary rays share node fetches);
-// one lane = one pixel, spp jittered samples in sequence (cudaRender order).
+// Pixel of k hits out of spp samples.  Color() returns (255,255,0) or
+// (20,20,40); the f32 sum of small integers is exact in any order, so the
+// reference's col /= spp; rgbToInt(col) depends only on k (:412-422).
+__device__ __forceinline__ uint32_t pixel_from_hits(uint32_t k, uint32_t spp) {
+    const float fs = (float)spp;
+    const float cr = (float)(255u * k + 20u * (spp - k));
+    const float cb = (float)(40u * (spp - k));
+    return rgb_to_int(cr / fs, cr / fs, cb / fs);
+}
+
+// ---------------------------------------------------------------------------
+// Triangle test: RayTriangleIntersection + FindNearestTriangle's record test.
+// With rec.t starting at FLT_MAX (Color, :380-382) "some triangle was
+// recorded" == "some tested triangle has MT true and 0 < t < FLT_MAX".
+// tp = {v0, e1 = v1-v0, e2 = v2-v0} (36 B, Morton order).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool tri_hit(const float *__restrict__ tp, float ox, float oy, float oz,
+                                        float dx, float dy, float dz) {
+    float v0x = tp[0], v0y = tp[1], v0z = tp[2];
+    float e1x = tp[3], e1y = tp[4], e1z = tp[5];
+    float e2x = tp[6], e2y = tp[7], e2z = tp[8];
+    // one round trip for the whole record (hipcc would otherwise sink the v0
+    // load behind the det test)
+    asm volatile("" ::"v"(v0x), "v"(v0y), "v"(v0z), "v"(e1x), "v"(e1y), "v"(e1z), "v"(e2x),
+                 "v"(e2y), "v"(e2z));
+    float px = dy * e2z - e2y * dz;                  // pvec = cross(D, e2)
+    float py = dz * e2x - e2z * dx;
+    float pz = dx * e2y - e2x * dy;
+    float det = (e1x * px + e1y * py) + e1z * pz;
+#if BIH_MT_EARLY_OUT
+    // Coherent rays see a triangle from the same side: the back-face test is
+    // usually uniform across the wave, and then skips the rest entirely.
+    if (det <= kDetEps) return false;                // det < 0.000001 (double); NaN passes
+#endif
+    float inv = 1.0f / det;
+    float sx = ox - v0x, sy = oy - v0y, sz = oz - v0z;
+    float u = ((sx * px + sy * py) + sz * pz) * inv;
+#if BIH_MT_EARLY_OUT
+    if (u < 0.0f || u > 1.0f) return false;
+#endif
+    float qx = sy * e1z - e1y * sz;                  // qvec = cross(tvec, e1)
+    float qy = sz * e1x - e1z * sx;
+    float qz = sx * e1y - e1x * sy;
+    float v = ((dx * qx + dy * qy) + dz * qz) * inv;
+#if BIH_MT_EARLY_OUT
+    if (v < 0.0f || u + v > 1.0f) return false;
+#endif
+    float t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    // det < 0.000001 (double compare) rejects; NaN det passes it
+    const bool ok_det = !(det <= kDetEps);
+    const bool ok_u = !(u < 0.0f || u > 1.0f);
+    const bool ok_v = !(v < 0.0f || u + v > 1.0f);
+    const bool ok_t = t > 0.0f && t < FLT_MAX;
+    return ok_det & ok_u & ok_v & ok_t;
+}
+
+// v[ax] for ax in {0,1,2} with integer masks: written as a ?: chain, hipcc
+// turns the three struct fields into an indexed scratch load.
+__device__ __forceinline__ float sel3(uint32_t ax, float a, float b, float c) {
+    const uint32_t m0 = 0u - (uint32_t)(ax == 0), m1 = 0u - (uint32_t)(ax == 1);
+    const uint32_t m2 = ~(m0 | m1);
+    return __uint_as_float((__float_as_uint(a) & m0) | (__float_as_uint(b) & m1) |
+                           (__float_as_uint(c) & m2));
+}
+
+// per-ray work counters (parity evidence + algorithmic bytes, SURVEY 8d)
+struct Cnt {
+    uint32_t nodes, leaves, tris;
+};
+
+// Uniform per-launch values.
+struct SceneU {
+    float ox, oy, oz;
+    float slo0, slo1, slo2, shi0, shi1, shi2;
+    uint32_t U, N;
+    const uint4 *nodes;
+    const float *tris;
+    const uint32_t *dup_cnt;
+};
+
+__device__ __forceinline__ SceneU load_scene(const RenderArgs &a) {
+    SceneU s;
+    s.ox = a.cam[0]; s.oy = a.cam[1]; s.oz = a.cam[2];
+    s.slo0 = a.hdr->scene_lo[0]; s.slo1 = a.hdr->scene_lo[1]; s.slo2 = a.hdr->scene_lo[2];
+    s.shi0 = a.hdr->scene_hi[0]; s.shi1 = a.hdr->scene_hi[1]; s.shi2 = a.hdr->scene_hi[2];
+    s.U = a.hdr->n_unique; s.N = a.hdr->n_tris;
+    s.nodes = a.nodes; s.tris = a.tris; s.dup_cnt = a.dup_cnt;
+    return s;
+}
+
+// Per-lane stack: slots [0, kLdsStack) in LDS, deeper slots in HBM.
+struct Stack {
+    uint32_t *node;      // LDS, [kLdsStack][kThreads]
+    float *tmin, *tmax;
+    uint32_t tid;
+    uint32_t *spill;     // HBM, [(kStackDepth-kLdsStack)*3][gthreads]
+    uint64_t gthreads, gtid;
+
+    // The HBM slots sit behind a wave-uniform __any() test: written as one
+    // if/else, hipcc merges both sides into FLAT loads (LDS through the
+    // vector-memory path, waiting on vmcnt) on every pop.
+    __device__ __forceinline__ void push(uint32_t sp, uint32_t n, float lo, float hi) const {
+        const bool in_lds = sp < (uint32_t)kLdsStack;
+        if (in_lds) {
+            node[sp * kThreads + tid] = n;
+            tmin[sp * kThreads + tid] = lo;
+            tmax[sp * kThreads + tid] = hi;
+        }
+        if (__builtin_expect(__any(!in_lds), 0)) {
+            if (!in_lds) {
+                uint32_t *q = spill + (uint64_t)(sp - kLdsStack) * 3 * gthreads + gtid;
+#if BIH_SPILL_NT
+                __builtin_nontemporal_store(n, q);
+                __builtin_nontemporal_store(__float_as_uint(lo), q + gthreads);
+                __builtin_nontemporal_store(__float_as_uint(hi), q + 2 * gthreads);
+#else
+                q[0] = n;
+                q[gthreads] = __float_as_uint(lo);
+                q[2 * gthreads] = __float_as_uint(hi);
+#endif
+            }
+        }
+    }
+    __device__ __forceinline__ void pop(uint32_t sp, uint32_t &n, float &lo, float &hi) const {
+        const bool in_lds = sp < (uint32_t)kLdsStack;
+        if (in_lds) {
+            n = node[sp * kThreads + tid];
+            lo = tmin[sp * kThreads + tid];
+            hi = tmax[sp * kThreads + tid];
+        }
+        if (__builtin_expect(__any(!in_lds), 0)) {
+            if (!in_lds) {
+                const uint32_t *q = spill + (uint64_t)(sp - kLdsStack) * 3 * gthreads + gtid;
+#if BIH_SPILL_NT
+                n = __builtin_nontemporal_load(q);
+                lo = __uint_as_float(__builtin_nontemporal_load(q + gthreads));
+                hi = __uint_as_float(__builtin_nontemporal_load(q + 2 * gthreads));
+#else
+                n = q[0];
+                lo = __uint_as_float(q[gthreads]);
+                hi = __uint_as_float(q[2 * gthreads]);
+#endif
+            }
+        }
+    }
+};
+
+// One ray's walk (TraverseTree, CUDAKernels.cu:227-368).
 template <bool ANYHIT, bool STATS>
-__global__ void __launch_bounds__(kThreads) k_render(const RenderArgs a) {
-    const uint32_t tiles_x = (a.w + 7) >> 3;
-    const uint32_t wv = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t x = (wv % tiles_x) * 8 + (lane & 7);
-    const uint32_t lr = (wv / tiles_x) * 8 + (lane >> 3);
-    if (x >= a.w || lr >= a.nrows) return;
-    const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+struct Walker {
+    float dx, dy, dz, ix, iy, iz;
+    uint32_t sg;                       // sign bits of invDir (Ray::sign)
+    float tMin, tMax;
+    uint32_t cur, sp;
+    uint32_t b0, e0, b1, e1;           // leaf queue: [b0,e0) then [b1,e1)
+    bool alive, hit;
+    Cnt cnt;
+
+    // Ray::Ray + the scene-AABB slab test (:237-262); tMin may be negative.
+    __device__ __forceinline__ void start(const SceneU &s, bool valid, float dx_, float dy_, float dz_) {
+        dx = dx_; dy = dy_; dz = dz_;
+        ix = 1.0f / dx; iy = 1.0f / dy; iz = 1.0f / dz;
+        sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        tMin = (((sg & 1) ? s.shi0 : s.slo0) - s.ox) * ix;
+        tMax = (((sg & 1) ? s.slo0 : s.shi0) - s.ox) * ix;
+        const float tymin = (((sg & 2) ? s.shi1 : s.slo1) - s.oy) * iy;
+        const float tymax = (((sg & 2) ? s.slo1 : s.shi1) - s.oy) * iy;
+        bool in = valid && !((tMin > tymax) || (tymin > tMax));
+        if (tymin > tMin) tMin = tymin;
+        if (tymax < tMax) tMax = tymax;
+        const float tzmin = (((sg & 4) ? s.shi2 : s.slo2) - s.oz) * iz;
+        const float tzmax = (((sg & 4) ? s.slo2 : s.shi2) - s.oz) * iz;
+        in = in && !((tMin > tzmax) || (tzmin > tMax));
+        if (tzmin > tMin) tMin = tzmin;
+        if (tzmax < tMax) tMax = tzmax;
+        cnt.nodes = cnt.leaves = cnt.tris = 0;
+        hit = false;
+        cur = 0; sp = 0;
+        b0 = e0 = b1 = e1 = 0;
+        alive = in && s.U > 0;
+        if (alive && s.U == 1) {           // single leaf; reference: UB
+            cur = kDone;
+            e0 = s.N;
+            if (STATS) cnt.leaves = 1;
+        }
+    }
+
+    // One unit of work: a queued triangle, else one node.
+    __device__ __forceinline__ void step(const SceneU &s, const Stack &st) {
+        if (b0 < e0) {
+            if (STATS) ++cnt.tris;
+            const bool h = tri_hit(s.tris + 9ull * b0, s.ox, s.oy, s.oz, dx, dy, dz);
+            hit |= h;
+            ++b0;
+            if (ANYHIT && h) {
+                if (STATS && e1 > b1) --cnt.leaves;   // queued far leaf never visited
+                alive = false;
+                return;
+            }
+            if (b0 == e0) { b0 = b1; e0 = e1; b1 = e1 = 0; }
+            if (b0 >= e0 && cur == kDone) alive = false;
+            return;
+        }
+        if (STATS) ++cnt.nodes;
+        const uint4 nd = s.nodes[cur];
+        const uint32_t ax = (nd.z >> 27) & 3u;
+        const float org = sel3(ax, s.ox, s.oy, s.oz);
+        const float inv = sel3(ax, ix, iy, iz);
+        const uint32_t nr = (sg >> ax) & 1u;
+        const float t0 = (__uint_as_float(nd.x) - org) * inv;
+        const float t1 = (__uint_as_float(nd.y) - org) * inv;
+        const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
+        const bool A = tMin < tn, B = tMax < tf;
+        const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
+        const bool leafL = (nd.z >> 29) & 1u, leafR = (nd.z >> 30) & 1u;
+        const bool leafN = nr ? leafR : leafL, leafF = nr ? leafL : leafR;
+        // the reference's four cases, flattened
+        const bool testN = A && leafN;                       // near leaf searched
+        const bool testF = !B && leafF;                      // far leaf searched
+        const bool goN = A && !leafN;                        // descend near
+        const bool goF = !B && !leafF && (!A || leafN);      // descend far
+        const bool push = goN && !B && !leafF;               // both internal: stack far
+        // leaf ranges, computed unconditionally: left [mid-cL, mid), right [mid, mid+cR)
+        uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
+        const bool escL = testN | testF ? (leafL && cL == 0) : false;   // count > 3
+        const bool escR = testN | testF ? (leafR && cR == 0) : false;
+        if (__builtin_expect(__any(escL | escR), 0)) {
+            if (escL) cL = s.dup_cnt[split];
+            if (escR) cR = s.dup_cnt[split + 1];
+        }
+        const uint32_t nb = nr ? mid : mid - cL, ne = nr ? mid + cR : mid;
+        const uint32_t fb = nr ? mid - cL : mid, fe = nr ? mid : mid + cR;
+        const bool two = testN && testF;
+        b0 = testN ? nb : (testF ? fb : b0);
+        e0 = testN ? ne : (testF ? fe : e0);
+        b1 = two ? fb : b1;
+        e1 = two ? fe : e1;
+        if (STATS) cnt.leaves += (testN ? 1u : 0u) + (testF ? 1u : 0u);
+        // stack: push the far child, or pop when no child is descended
+        const bool pop = !goN && !goF && sp != 0;
+        const uint32_t far = split + 1u - nr;
+        uint32_t pn = kDone;
+        float pmin = tMin, pmax = tMax;
+        if (push) st.push(sp, far, tf, tMax);
+        if (pop) st.pop(sp - 1u, pn, pmin, pmax);
+        sp = sp + (push ? 1u : 0u) - (pop ? 1u : 0u);
+        cur = goN ? split + nr : (goF ? far : pn);
+        tMax = goN ? tn : pmax;
+        tMin = goF ? tf : pmin;
+        if (cur == kDone && b0 >= e0) alive = false;
+    }
+};
+
+// Camera::GetRay(u, v) direction, Camera.cu:18-20 (glm order, no contraction).
+__device__ __forceinline__ void camera_dir(const RenderArgs &a, float u, float v, float &dx, float &dy,
+                                           float &dz) {
+    dx = ((a.cam[3] + u * a.cam[6]) + v * a.cam[9]) - a.cam[0];
+    dy = ((a.cam[4] + u * a.cam[7]) + v * a.cam[10]) - a.cam[1];
+    dz = ((a.cam[5] + u * a.cam[8]) + v * a.cam[11]) - a.cam[2];
+}
+
+template <int L>
+struct TileShape {   // TW x TH pixels, TW*TH = 64 >> log2(spp)
+    static constexpr uint32_t LP = 6 - L;
+    static constexpr uint32_t TW = 1u << ((LP + 1) / 2);
+    static constexpr uint32_t TH = 1u << (LP / 2);
+};
+
+// Ray id -> (local pixel, sample).  Ids run tile-major: 64 consecutive ids
+// are one TW x TH pixel tile, pixel-major within the tile.
+template <int LOG2SPP>
+__device__ __forceinline__ void ray_coords(uint64_t rid, uint32_t tiles_x, uint32_t &x, uint32_t &lr,
+                                           uint32_t &s) {
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    const uint32_t tile = (uint32_t)(rid >> 6);
+    const uint32_t pix = ((uint32_t)rid & 63u) >> LOG2SPP;
+    s = (uint32_t)rid & ((1u << LOG2SPP) - 1u);
+    x = (tile % tiles_x) * TW + (pix % TW);
+    lr = (tile / tiles_x) * TH + (pix / TW);
+}
+
+// RNG for sample s of pixel lp: draws 2s, 2s+1 of this frame (the pixel's
+// state advanced 2s+2 steps).  The lane of the last sample stores the state
+// the reference's cudaRender leaves behind (:419) into rng_out.
+template <uint32_t SPP>
+__device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uint32_t s, float &ru,
+                                           float &rv) {
     const uint64_t P = (uint64_t)a.nrows * a.w;
-    const uint64_t lp = (uint64_t)lr * a.w + x;
-
-    const float slo[3] = {a.hdr->scene_lo[0], a.hdr->scene_lo[1], a.hdr->scene_lo[2]};
-    const float shi[3] = {a.hdr->scene_hi[0], a.hdr->scene_hi[1], a.hdr->scene_hi[2]};
-    const uint32_t U = a.hdr->n_unique, N = a.hdr->n_tris;
-
     uint32_t v[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) v[i] = a.rng[(uint64_t)i * P + lp];
+    for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
     uint32_t d = a.d_base;
-
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    for (uint32_t s = 0; s < a.spp; ++s) {
-        const float ru = xorwow_uniform(v, d);
-        const float rv = xorwow_uniform(v, d);
-        const float u = ((float)x + ru) / (float)a.w;
-        const float vv = ((float)y + rv) / (float)a.h;
-        Ray r;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            r.o[c] = a.cam[c];
-            float hu = u * a.cam[6 + c];
-            float vq = vv * a.cam[9 + c];
-            r.d[c] = ((a.cam[3 + c] + hu) + vq) - a.cam[c];
-            r.inv[c] = 1.0f / r.d[c];
-            r.sgn[c] = r.inv[c] < 0.0f;
-        }
-        Cnt cnt = {0, 0, 0};
-        const bool hit = trace<ANYHIT, STATS>(a, r, slo, shi, U, N, cnt);
-        if (STATS) {
-            uint64_t rid = lp * a.spp + s;
-            a.ray_stats[3 * rid] = cnt.nodes;
-            a.ray_stats[3 * rid + 1] = cnt.leaves;
-            a.ray_stats[3 * rid + 2] = cnt.tris;
-        }
-        cr += hit ? 255.0f : 20.0f;
-        cg += hit ? 255.0f : 20.0f;
-        cb += hit ? 0.0f : 40.0f;
+    for (uint32_t k = 0; k <= s; ++k) {
+        ru = xorwow_uniform(v, d);
+        rv = xorwow_uniform(v, d);
     }
+    if (s == SPP - 1) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) a.rng[(uint64_t)i * P + lp] = v[i];
-    const float fs = (float)a.spp;
-    a.out[lp] = rgb_to_int(cr / fs, cg / fs, cb / fs);
+        for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_render_tile
+// ---------------------------------------------------------------------------
+template <bool ANYHIT, bool STATS, int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_tile(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    __shared__ uint32_t s_node[kLdsStack * kThreads];
+    __shared__ float s_min[kLdsStack * kThreads];
+    __shared__ float s_max[kLdsStack * kThreads];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
+                      (uint64_t)blockIdx.x * kThreads + tid};
+    const SceneU sc = load_scene(a);
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+
+    for (;;) {
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(a.work, 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles) break;
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        float dx = 0.f, dy = 0.f, dz = 1.f;
+        if (valid) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            const float u = ((float)x + ru) / fw;     // :414-415
+            const float v = ((float)y + rv) / fh;
+            camera_dir(a, u, v, dx, dy, dz);
+        }
+        Walker<ANYHIT, STATS> w;
+        w.start(sc, valid, dx, dy, dz);
+        while (w.alive) w.step(sc, st);
+        if (STATS && valid) {
+            const uint64_t rid = lp * SPP + s;
+            a.ray_stats[3 * rid] = w.cnt.nodes;
+            a.ray_stats[3 * rid + 1] = w.cnt.leaves;
+            a.ray_stats[3 * rid + 2] = w.cnt.tris;
+        }
+        const unsigned long long hb = __ballot(w.hit);
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hb >> (pix * SPP)) & m), SPP);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_render_refill
+// ---------------------------------------------------------------------------
+template <bool ANYHIT, bool STATS, int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_refill(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    constexpr int kRefillMin = 16;   // refill once this many lanes are idle
+    __shared__ uint32_t s_node[kLdsStack * kThreads];
+    __shared__ float s_min[kLdsStack * kThreads];
+    __shared__ float s_max[kLdsStack * kThreads];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
+                      (uint64_t)blockIdx.x * kThreads + tid};
+    const SceneU sc = load_scene(a);
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const uint64_t nrays = (uint64_t)tiles_x * ((a.nrows + TH - 1) / TH) * 64;
+    const float fw = (float)a.w, fh = (float)a.h;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+
+    Walker<ANYHIT, STATS> w;
+    w.alive = false;
+    w.hit = false;
+    uint64_t lp = 0;
+    uint32_t s = 0;
+    bool exhausted = false;
+    bool own = false;                  // lane holds a valid ray to finalise
+
+    auto finish = [&]() {
+        if (STATS) {
+            const uint64_t rid = lp * SPP + s;
+            a.ray_stats[3 * rid] = w.cnt.nodes;
+            a.ray_stats[3 * rid + 1] = w.cnt.leaves;
+            a.ray_stats[3 * rid + 2] = w.cnt.tris;
+        }
+        if (SPP == 1) {
+            a.out[lp] = pixel_from_hits(w.hit ? 1u : 0u, 1u);
+        } else {
+            const uint32_t old = atomicAdd(a.pixacc + lp, w.hit ? 0x10001u : 1u);
+            if ((old & 0xFFFFu) + 1u == SPP) {       // last sample of the pixel
+                a.out[lp] = pixel_from_hits((old >> 16) + (w.hit ? 1u : 0u), SPP);
+                a.pixacc[lp] = 0u;                   // ready for the next frame
+            }
+        }
+        own = false;
+    };
+
+    for (;;) {
+        // ---- refill idle lanes (wave-aggregated atomic on the ray counter)
+        while (!exhausted) {
+            const unsigned long long need = __ballot(!w.alive);
+            if (need == 0ull) break;
+            const uint32_t cnt = (uint32_t)__popcll(need);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(a.work, cnt);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if ((uint64_t)base + cnt >= nrays) exhausted = true;
+            if (!w.alive) {
+                const uint64_t rid = (uint64_t)base + __popcll(need & lt);
+                bool valid = false;
+                float dx = 0.f, dy = 0.f, dz = 1.f;
+                if (rid < nrays) {
+                    uint32_t x, lr;
+                    ray_coords<LOG2SPP>(rid, tiles_x, x, lr, s);
+                    valid = x < a.w && lr < a.nrows;
+                    if (valid) {
+                        lp = (uint64_t)lr * a.w + x;
+                        float ru = 0.f, rv = 0.f;
+                        ray_jitter<SPP>(a, lp, s, ru, rv);
+                        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+                        const float u = ((float)x + ru) / fw;
+                        const float v = ((float)y + rv) / fh;
+                        camera_dir(a, u, v, dx, dy, dz);
+                    }
+                }
+                w.start(sc, valid, dx, dy, dz);
+                own = valid;
+                if (own && !w.alive) finish();          // slab miss: done at once
+            }
+            if (__ballot(!w.alive) == 0ull) break;
+        }
+        if (__ballot(w.alive) == 0ull) break;           // queue empty, all lanes idle
+        // ---- walk until enough lanes are idle to make a refill worthwhile
+        for (;;) {
+            if (w.alive) {
+                w.step(sc, st);
+                if (!w.alive) finish();
+            }
+            const unsigned long long idle = __ballot(!w.alive);
+            if (idle == ~0ull) break;
+            if (!exhausted && __popcll(idle) >= kRefillMin) break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_render_pixel: any spp; one lane per pixel, spp samples in sequence
+// (cudaRender's own loop order).  One wave = one 8x8 pixel tile.
+// ---------------------------------------------------------------------------
+template <bool ANYHIT, bool STATS>
+__global__ void __launch_bounds__(kThreads) k_render_pixel(const RenderArgs a) {
+    __shared__ uint32_t s_node[kLdsStack * kThreads];
+    __shared__ float s_min[kLdsStack * kThreads];
+    __shared__ float s_max[kLdsStack * kThreads];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t tiles_x = (a.w + 7) >> 3;
+    const uint32_t ntiles = tiles_x * ((a.nrows + 7) >> 3);
+    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
+                      (uint64_t)blockIdx.x * kThreads + tid};
+    const SceneU sc = load_scene(a);
+    const uint64_t P = (uint64_t)a.nrows * a.w;
+    // grid-stride over 8x8 tiles (the grid is capped at the spill area's size)
+    for (uint32_t wv = blockIdx.x * (kThreads / 64) + (tid >> 6); wv < ntiles;
+         wv += gridDim.x * (kThreads / 64)) {
+        const uint32_t x = (wv % tiles_x) * 8 + (lane & 7);
+        const uint32_t lr = (wv / tiles_x) * 8 + (lane >> 3);
+        if (x >= a.w || lr >= a.nrows) continue;
+        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
+        uint32_t d = a.d_base;
+        uint32_t k = 0;
+        for (uint32_t s = 0; s < a.spp; ++s) {
+            const float ru = xorwow_uniform(v, d);
+            const float rv = xorwow_uniform(v, d);
+            float dx, dy, dz;
+            camera_dir(a, ((float)x + ru) / (float)a.w, ((float)y + rv) / (float)a.h, dx, dy, dz);
+            Walker<ANYHIT, STATS> w;
+            w.start(sc, true, dx, dy, dz);
+            while (w.alive) w.step(sc, st);
+            if (STATS) {
+                const uint64_t rid = lp * a.spp + s;
+                a.ray_stats[3 * rid] = w.cnt.nodes;
+                a.ray_stats[3 * rid + 1] = w.cnt.leaves;
+                a.ray_stats[3 * rid + 2] = w.cnt.tris;
+            }
+            k += w.hit ? 1u : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = v[i];
+        a.out[lp] = pixel_from_hits(k, a.spp);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_render_packet: the wave walks the BIH as one packet of 64 rays.
+//
+// Every lane keeps its own interval [tMin, tMax] and makes the reference's
+// own decision at each node: it visits the near child iff tMin < t[near]
+// (interval [tMin, t[near]]) and the far child iff !(tMax < t[far])
+// (interval [t[far], tMax]) -- the four cases of TraverseTree
+// (CUDAKernels.cu:295-365) reduce to exactly that.  A lane's visited set and
+// its intervals depend only on the path from the root, not on the order in
+// which subtrees are walked, so the wave may walk the UNION of its lanes'
+// sets in one order, with a 64-bit mask of the lanes that visit each node:
+// every lane still tests exactly the leaves TraverseTree tests (reference
+// walk), or a prefix of them in another order (any-hit walk, whose RGBA only
+// needs "some tested triangle hit").
+// Node index, masks and the triangle records are wave-uniform (scalar loads
+// through the scalar cache); the per-lane intervals of the stack live in
+// VGPRs indexed by the uniform stack pointer (s_set_gpr_idx), entries past
+// kPacketRegs in a per-wave HBM area.
+// ---------------------------------------------------------------------------
+#ifndef BIH_PACKET_REGS
+#define BIH_PACKET_REGS 16
+#endif
+constexpr int kPacketRegs = BIH_PACKET_REGS;
+
+__device__ __forceinline__ unsigned long long lane_bit(uint32_t lane) { return 1ull << lane; }
+
+template <bool ANYHIT, bool STATS, int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    constexpr int D = kPacketRegs;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned long long me = lane_bit(lane);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + wv;
+    uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - D) * 3 * 64;
+    const SceneU sc = load_scene(a);
+    const uint4 *__restrict__ nodes = sc.nodes;
+    const float *__restrict__ tris = sc.tris;
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+
+    for (;;) {
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(a.work, 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles) break;
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        float dx = 0.f, dy = 0.f, dz = 1.f;
+        if (valid) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
+        }
+        // Ray::Ray + slab test (reuse the per-lane Walker's start)
+        Walker<ANYHIT, STATS> w;
+        w.start(sc, valid, dx, dy, dz);
+        const float ix = w.ix, iy = w.iy, iz = w.iz;
+        float tMin = w.tMin, tMax = w.tMax;
+        bool hit = false;
+        uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
+        unsigned long long live = __ballot(w.alive);      // lanes whose ray is still searching
+
+        // test the triangles [b, b+n) for the lanes in m
+        auto test_leaf = [&](uint32_t b, uint32_t n, unsigned long long m) {
+            if (STATS && (m & me)) ++c_leaves;
+            for (uint32_t i = 0; i < n; ++i) {
+                if (ANYHIT) {
+                    m &= live;
+                    if (!m) break;
+                }
+                const float *tp = tris + 9ull * (b + i);
+                if (m & me) {
+                    if (STATS) ++c_tris;
+                    const bool h = tri_hit(tp, sc.ox, sc.oy, sc.oz, dx, dy, dz);
+                    hit |= h;
+                }
+                if (ANYHIT) live &= ~__ballot(hit);
+            }
+        };
+
+#ifdef BIH_PACKET_DEBUG
+        c_nodes = (uint32_t)((live >> lane) & 1ull) + (w.alive ? 10u : 0u) + (valid ? 100u : 0u);
+        live = 0;
+#endif
+        if (live && sc.U == 1) {                          // single leaf (reference: UB)
+            test_leaf(0, sc.N, live);
+        } else if (live) {
+            float st_lo[D], st_hi[D];
+            uint32_t st_nd[D];
+            uint32_t cur = 0, sp = 0;
+            unsigned long long act = live;
+#ifdef BIH_PACKET_DEBUG2
+            const unsigned long long live0 = live;
+            uint32_t dbg_step = 0, dbg_first = 0;
+#endif
+            for (;;) {
+#ifdef BIH_PACKET_DEBUG2
+                ++dbg_step;
+                if ((act & ~live0) && !dbg_first) dbg_first = dbg_step;
+                if ((act & ~live0) & me) c_tris = 1000000 + dbg_first;
+#endif
+                if (STATS && (act & me)) ++c_nodes;
+                const uint4 nd = nodes[cur];
+                const uint32_t ax = (nd.z >> 27) & 3u;
+                const float org = sel3(ax, sc.ox, sc.oy, sc.oz);
+                const float inv = sel3(ax, ix, iy, iz);
+                const bool nr = (w.sg >> ax) & 1u;
+                const float t0 = (__uint_as_float(nd.x) - org) * inv;
+                const float t1 = (__uint_as_float(nd.y) - org) * inv;
+                const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
+                const bool A = tMin < tn;                 // near child visited
+                const bool nB = !(tMax < tf);             // far child visited
+                // child intervals: near [tMin, tn], far [tf, tMax]
+                const float lo_L = nr ? tf : tMin, hi_L = nr ? tMax : tn;
+                const float lo_R = nr ? tMin : tf, hi_R = nr ? tn : tMax;
+                const unsigned long long mN = __ballot(A) & act, mF = __ballot(nB) & act;
+                const unsigned long long mnr = __ballot(nr);
+                unsigned long long mL = (mN & ~mnr) | (mF & mnr);
+                unsigned long long mR = (mN & mnr) | (mF & ~mnr);
+                const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
+                const bool leafL = (nd.z >> 29) & 1u, leafR = (nd.z >> 30) & 1u;
+                // near first for the majority of the packet
+                const bool nearL = __popcll(act & mnr) * 2 <= (uint32_t)__popcll(act);
+                if ((leafL && mL) || (leafR && mR)) {
+                    uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
+                    if (leafL && cL == 0) cL = sc.dup_cnt[split];
+                    if (leafR && cR == 0) cR = sc.dup_cnt[split + 1];
+                    if (nearL) {
+                        if (leafL && mL) test_leaf(mid - cL, cL, mL);
+                        if (leafR && mR) test_leaf(mid, cR, mR);
+                    } else {
+                        if (leafR && mR) test_leaf(mid, cR, mR);
+                        if (leafL && mL) test_leaf(mid - cL, cL, mL);
+                    }
+                }
+                if (ANYHIT) {
+                    mL &= live;
+                    mR &= live;
+                }
+                const unsigned long long gL = leafL ? 0ull : mL, gR = leafR ? 0ull : mR;
+                if (gL && gR) {
+                    // descend near, stack far (node, mask, per-lane interval)
+                    const uint32_t fnode = nearL ? split + 1 : split;
+                    const unsigned long long fmask = nearL ? gR : gL;
+                    const float flo = nearL ? lo_R : lo_L, fhi = nearL ? hi_R : hi_L;
+                    // entry word: node index | this lane's mask bit << 31
+                    const uint32_t word = fnode | (((fmask & me) != 0ull) ? 0x80000000u : 0u);
+                    if (sp < (uint32_t)D) {
+                        st_lo[sp] = flo;
+                        st_hi[sp] = fhi;
+                        st_nd[sp] = word;
+                    } else {
+                        uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
+                        q[0] = __float_as_uint(flo);
+                        q[64] = __float_as_uint(fhi);
+                        q[128] = word;
+                    }
+                    sp = __builtin_amdgcn_readfirstlane(sp + 1);
+                    cur = nearL ? split : split + 1;
+                    act = nearL ? gL : gR;
+                    tMin = nearL ? lo_L : lo_R;
+                    tMax = nearL ? hi_L : hi_R;
+                } else if (gL) {
+                    cur = split; act = gL; tMin = lo_L; tMax = hi_L;
+                } else if (gR) {
+                    cur = split + 1; act = gR; tMin = lo_R; tMax = hi_R;
+                } else {
+                    // pop until an entry still has a live lane
+                    bool found = false;
+                    while (sp > 0) {
+                        sp = __builtin_amdgcn_readfirstlane(sp - 1);
+                        uint32_t word;
+                        float lo, hi;
+                        if (sp < (uint32_t)D) {
+                            lo = st_lo[sp];
+                            hi = st_hi[sp];
+                            word = st_nd[sp];
+                        } else {
+                            const uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
+                            lo = __uint_as_float(q[0]);
+                            hi = __uint_as_float(q[64]);
+                            word = q[128];
+                        }
+                        unsigned long long m = __ballot(word >> 31);
+                        if (ANYHIT) m &= live;
+                        if (!m) continue;
+                        cur = __builtin_amdgcn_readfirstlane(word & 0x7fffffffu);
+                        act = m;
+                        tMin = lo;
+                        tMax = hi;
+                        found = true;
+                        break;
+                    }
+                    if (!found) break;
+                }
+            }
+        }
+
+        if (STATS && valid) {
+            const uint64_t rid = lp * SPP + s;
+            a.ray_stats[3 * rid] = c_nodes;
+            a.ray_stats[3 * rid + 1] = c_leaves;
+            a.ray_stats[3 * rid + 2] = c_tris;
+        }
+        const unsigned long long hb = __ballot(hit);
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hb >> (pix * SPP)) & m), SPP);
+        }
+    }
 }
 
 std::mutex g_tab_mu;
 uint32_t *g_tab_dev[64] = {nullptr};
+
+enum class Variant { Tile, Refill, Packet };
+
+Variant variant_from_env() {
+    const char *e = getenv("BIH_RENDER_KERNEL");
+    if (e && strcmp(e, "tile") == 0) return Variant::Tile;
+    if (e && strcmp(e, "refill") == 0) return Variant::Refill;
+    return Variant::Packet;
+}
+
+template <int L>
+hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse, hipStream_t st,
+                             uint32_t blocks) {
+    const bool stats = a.ray_stats != nullptr;
+    const dim3 g(blocks), b(kThreads);
+    if (var == Variant::Tile) {
+        if (traverse == 0) {
+            if (stats) hipLaunchKernelGGL((k_render_tile<true, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_tile<true, false, L>), g, b, 0, st, a);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_render_tile<false, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_tile<false, false, L>), g, b, 0, st, a);
+        }
+    } else if (var == Variant::Refill) {
+        if (traverse == 0) {
+            if (stats) hipLaunchKernelGGL((k_render_refill<true, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_refill<true, false, L>), g, b, 0, st, a);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_render_refill<false, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_refill<false, false, L>), g, b, 0, st, a);
+        }
+    } else {
+        if (traverse == 0) {
+            if (stats) hipLaunchKernelGGL((k_render_packet<true, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet<true, false, L>), g, b, 0, st, a);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_render_packet<false, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet<false, false, L>), g, b, 0, st, a);
+        }
+    }
+    return hipGetLastError();
+}
 
 }  // namespace
 
@@ -335,18 +911,71 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
+// Resident blocks of the persistent kernels on `device` (grid size).
+uint32_t wave_grid_blocks(int device) {
+    static std::mutex mu;
+    static uint32_t cache[64] = {0};
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0 || device >= 64) return 0;
+    if (!cache[device]) {
+        int cus = 0, per = 0, per2 = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void *>(k_render_refill<true, false, 2>), kThreads, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per2, reinterpret_cast<const void *>(k_render_tile<true, false, 2>), kThreads, 0);
+        if (per2 > per) per = per2;
+        if (cus <= 0) cus = 256;
+        if (per <= 0) per = 1;
+        cache[device] = (uint32_t)(cus * per);
+    }
+    return cache[device];
+}
+
+size_t spill_words(uint32_t blocks) {
+    return (size_t)blocks * kThreads * (kStackDepth - kLdsStack) * 3;
+}
+
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t spp = a.spp;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint32_t grid = wave_grid_blocks(dev);
+    if (spp <= 64 && (spp & (spp - 1)) == 0) {
+        static const Variant var = variant_from_env();
+        const int L = __builtin_ctz(spp);
+        const uint32_t pix = 64u >> L;
+        const uint32_t tw = 1u << ((6 - L + 1) / 2), th = pix / tw;
+        const uint64_t tiles = (uint64_t)((a.w + tw - 1) / tw) * ((a.nrows + th - 1) / th);
+        if (tiles == 0) return 0;
+        uint32_t blocks = (uint32_t)((tiles + 3) / 4);
+        if (blocks > grid) blocks = grid;
+        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+        switch (L) {
+        case 0: e = launch_persistent<0>(var, a, traverse, st, blocks); break;
+        case 1: e = launch_persistent<1>(var, a, traverse, st, blocks); break;
+        case 2: e = launch_persistent<2>(var, a, traverse, st, blocks); break;
+        case 3: e = launch_persistent<3>(var, a, traverse, st, blocks); break;
+        case 4: e = launch_persistent<4>(var, a, traverse, st, blocks); break;
+        case 5: e = launch_persistent<5>(var, a, traverse, st, blocks); break;
+        default: e = launch_persistent<6>(var, a, traverse, st, blocks); break;
+        }
+        return (int)e;
+    }
+    // any other spp: one lane per pixel, grid-stride, grid capped at the spill area
     const uint32_t tiles = ((a.w + 7) >> 3) * ((a.nrows + 7) >> 3);
     if (tiles == 0) return 0;
-    const uint32_t blocks = (tiles + 3) / 4;
-    hipStream_t st = (hipStream_t)stream;
+    uint32_t blocks = (tiles + 3) / 4;
+    if (blocks > grid) blocks = grid;
     const bool stats = a.ray_stats != nullptr;
     if (traverse == 0) {
-        if (stats) hipLaunchKernelGGL((k_render<true, true>), dim3(blocks), dim3(kThreads), 0, st, a);
-        else hipLaunchKernelGGL((k_render<true, false>), dim3(blocks), dim3(kThreads), 0, st, a);
+        if (stats) hipLaunchKernelGGL((k_render_pixel<true, true>), dim3(blocks), dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((k_render_pixel<true, false>), dim3(blocks), dim3(kThreads), 0, st, a);
     } else {
-        if (stats) hipLaunchKernelGGL((k_render<false, true>), dim3(blocks), dim3(kThreads), 0, st, a);
-        else hipLaunchKernelGGL((k_render<false, false>), dim3(blocks), dim3(kThreads), 0, st, a);
+        if (stats) hipLaunchKernelGGL((k_render_pixel<false, true>), dim3(blocks), dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((k_render_pixel<false, false>), dim3(blocks), dim3(kThreads), 0, st, a);
     }
     return (int)hipGetLastError();
 }

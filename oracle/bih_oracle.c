@@ -394,7 +394,7 @@ int ob_mt(const float tri[9], const float o[3], const float d[3], float *t_out) 
 /* ------------------------------------------------------------------ */
 /* Traversal                                                            */
 /* ------------------------------------------------------------------ */
-typedef struct { uint64_t nodes, leaves, tris; int max_stack; } cnt_t;
+typedef struct { uint64_t nodes, leaves, tris; int max_stack; uint64_t push_at[33]; } cnt_t;
 typedef struct { double t; int idx; } hit_t;   /* HitRecord, Tree.cuh:9-14 */
 
 /* FindNearestTriangle, CUDAKernels.cu:206-224.  Returns 1 when anyhit and
@@ -489,6 +489,7 @@ static int traverse_gpu_ref(const ob_tree *T, const ray_t *r, cnt_t *c, int anyh
                 stack[sp].node = ch[fr]; stack[sp].tmin = t[fr]; stack[sp].tmax = tMax;
                 sp++;
                 if (sp - 1 > c->max_stack) c->max_stack = sp - 1;
+                c->push_at[sp - 1 < 32 ? sp - 1 : 32]++;   /* stack slot written */
                 cur = ch[nr]; tMax = t[nr];
             }
         }
@@ -610,6 +611,8 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
     }
     uint64_t g_nodes = 0, g_leaves = 0, g_tris = 0, g_hit = 0, g_miss = 0;
     int g_max = 0, used = 1;
+    uint64_t g_push[33];
+    memset(g_push, 0, sizeof g_push);
     double t0 = now_s();
 #pragma omp parallel reduction(+ : g_nodes, g_leaves, g_tris, g_hit, g_miss) reduction(max : g_max)
     {
@@ -620,7 +623,8 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
 #pragma omp for schedule(dynamic, 1)
         for (int64_t k = 0; k < (int64_t)nrows; ++k) {
             uint32_t j = row0 + (uint32_t)k * row_step;
-            cnt_t c = {0, 0, 0, 0};
+            cnt_t c;
+            memset(&c, 0, sizeof c);
             for (uint32_t i = 0; i < w; ++i) {
                 uint32_t *s = rv + ((size_t)k * w + i) * 6;
                 float col[3] = {0.0f, 0.0f, 0.0f};
@@ -655,6 +659,8 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
             }
             g_nodes += c.nodes; g_leaves += c.leaves; g_tris += c.tris;
             if (c.max_stack > g_max) g_max = c.max_stack;
+#pragma omp critical(ob_push_hist)
+            for (int q = 0; q < 33; ++q) g_push[q] += c.push_at[q];
         }
     }
     double t1 = now_s();
@@ -669,6 +675,7 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
         stats->max_stack = g_max;
         stats->threads = used;
         stats->render_seconds = t1 - t0;
+        for (int q = 0; q < 33; ++q) stats->push_at[q] = g_push[q];
     }
     return 0;
 }
@@ -678,7 +685,8 @@ int ob_trace_rays(const ob_tree *T, const float *orig, const float *dir, int32_t
     if (!T || (n > 0 && (!orig || !dir || !hit))) return -1;
     for (int32_t i = 0; i < n; ++i) {
         ray_t r; make_ray(orig + 3 * (size_t)i, dir + 3 * (size_t)i, &r);
-        cnt_t c = {0, 0, 0, 0};
+        cnt_t c;
+        memset(&c, 0, sizeof c);
         int h = trace_one(T, &r, mode, &c);
         hit[i] = (uint8_t)(h > 0);
         if (nodes) nodes[i] = (uint32_t)c.nodes;

@@ -57,6 +57,7 @@ typedef struct ob_stats {
     int32_t max_stack;           /* deepest stack (excluding sentinel) */
     int32_t threads;
     double render_seconds;       /* wall time of the traversal loop only */
+    uint64_t push_at[33];        /* stack pushes by slot index (32 = deeper)  */
 } ob_stats;
 
 int  ob_build(const float *v, int32_t n, ob_tree **out);

@@ -37,10 +37,13 @@ class Stats(C.Structure):
         ("rays", C.c_uint64), ("rays_hit", C.c_uint64), ("node_visits", C.c_uint64),
         ("leaf_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("slab_miss", C.c_uint64),
         ("max_stack", C.c_int32), ("threads", C.c_int32), ("render_seconds", C.c_double),
+        ("push_at", C.c_uint64 * 33),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["push_at"] = list(self.push_at)
+        return d
 
 
 _lib = None

@@ -1,0 +1,9 @@
+set -u
+timeout -k 10 600 python -m pytest tests -m gpu -q --timeout=300 > gpurun_out/t6.log 2>&1; echo tests_rc=$?; tail -3 gpurun_out/t6.log
+BIH_RENDER_KERNEL=tile timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q --timeout=300 -k "render or counters or bands or 1m" > gpurun_out/t6b.log 2>&1; echo tests_tile_rc=$?; tail -2 gpurun_out/t6b.log
+for K in variants/libbih_amd_K4.so variants/libbih_amd_K6.so variants/libbih_amd_K8.so libbih_amd.so variants/libbih_amd_K12.so; do
+  for V in tile refill; do
+    BIH_LIB=bih-gpu-raytracer_amd/lib/$K BIH_RENDER_KERNEL=$V timeout -k 10 120 python tools/time_render.py --tag ab2 >> gpurun_out/ab2.jsonl 2>/dev/null || echo "fail $K $V"
+  done
+done
+cat gpurun_out/ab2.jsonl

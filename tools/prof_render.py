@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Kernel-only driver for rocprofv3: builds the bench scene once and renders
+`--frames` frames of the bench workload (default 1M soup, 1920x1080x4)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bih-gpu-raytracer_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=4)
+    ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
+    a = ap.parse_args()
+    import torch
+    import bihrt
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    tris = bihrt.scenes.soup(a.tris, seed=1)
+    d = torch.from_numpy(tris).cuda()
+    g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=s.cuda_stream)
+    r = bihrt.Renderer(g, a.width, a.height, spp=a.spp)
+    out = torch.zeros(a.width * a.height, dtype=torch.int32, device="cuda")
+    trav = bihrt.TRAVERSE_ANYHIT if a.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
+    for f in range(a.frames):
+        r.render_device(out.data_ptr(), f, traverse=trav, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    print("frames", a.frames, "done")
+
+
+if __name__ == "__main__":
+    main()
