@@ -37,6 +37,9 @@ struct bih_tree {
     bool owns_stream = false;
     uint32_t *work = nullptr;        // persistent-kernel tile counter
     uint32_t *spill = nullptr;       // traversal stack spill area
+    float *prim = nullptr;           // primary-ray triangle records (16 f32 / tri)
+    bool prim_valid = false;
+    uint32_t prim_origin[3] = {0, 0, 0};   // bit patterns of the origin they were built for
 };
 
 namespace {
@@ -72,6 +75,7 @@ int finish_build(bih_tree *tr) {
     int e = bih::build_tree_device(tr->t, tr->stream, &ms);
     tr->build_ms = ms;
     tr->rng_valid = false;   // tree changed; RNG is independent but keep it simple
+    tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
     return map_hip(e);
 }
 
@@ -210,6 +214,7 @@ void bih_free(bih_tree *tr) {
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
     if (tr->spill) (void)hipFree(tr->spill);
+    if (tr->prim) (void)hipFree(tr->prim);
     if (tr->ev0) (void)hipEventDestroy(tr->ev0);
     if (tr->ev1) (void)hipEventDestroy(tr->ev1);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
@@ -343,6 +348,22 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     }
     int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
+    // primary-ray triangle records follow the camera origin
+    if (bih::render_uses_prim(spp) && tr->t.n > 0) {
+        uint32_t ob[3];
+        memcpy(ob, cam->origin, sizeof ob);
+        if (!tr->prim) {
+            hipError_t e = hipMalloc((void **)&tr->prim, (size_t)tr->t.n * 64);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->prim_valid = false;
+        }
+        if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
+            int e = bih::launch_tri_prim(tr->t.tris_s, tr->t.n, cam->origin, tr->prim, st);
+            if (e) return map_hip(e);
+            memcpy(tr->prim_origin, ob, sizeof ob);
+            tr->prim_valid = true;
+        }
+    }
     bih::RenderArgs a;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
@@ -358,6 +379,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.hdr = tr->t.hdr;
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
+    a.tri_prim = tr->prim;
     a.dup_cnt = tr->t.dup_cnt;
     const size_t P = (size_t)rows.nrows * w;
     a.rng_in = tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap;

@@ -57,6 +57,7 @@ struct RenderArgs {
     const TreeHeader *hdr;
     const uint4 *nodes;
     const float *tris;
+    const float *tri_prim;  // 16 f32 per triangle: primary-ray records for origin cam[0..2]
     const uint32_t *dup_cnt;
     const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame
     uint32_t *rng_out;      // state after the frame (double-buffered: a pixel's
@@ -104,8 +105,11 @@ const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 s
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
-uint32_t wave_grid_blocks(int device);     // persistent grid of k_render_wave
+uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);
+// primary-ray triangle records (k_tri_prim) for camera origin `origin`
+int launch_tri_prim(const float *tris, uint32_t n, const float origin[3], float *prim, void *stream);
+bool render_uses_prim(uint32_t spp);
 
 // host XORWOW helpers (xorwow_host.cpp)
 void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);

@@ -638,6 +638,38 @@ constexpr int kPacketRegs = BIH_PACKET_REGS;
 
 __device__ __forceinline__ unsigned long long lane_bit(uint32_t lane) { return 1ull << lane; }
 
+// Scalar (SMEM) views of read-only tree data: a load through address space 4
+// at a wave-uniform address is emitted as s_load_* (scalar cache) instead of
+// a per-lane global_load.
+typedef unsigned int su32x4 __attribute__((ext_vector_type(4)));
+typedef float sf32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(4))) const su32x4 cnode_t;
+typedef __attribute__((address_space(4))) const sf32x16 cprim_t;
+typedef __attribute__((address_space(4))) const uint32_t cu32_t;
+
+// MT for one primary-ray triangle record against this lane's ray.  The
+// record holds the ray-independent parts for the camera origin O:
+// {e1, e2, s = O - v0, q = cross(s, e1), tnum = dot(e2, q)} (k_tri_prim), so
+// per lane only p = cross(D, e2), det, u, v and t = tnum * inv remain -- each
+// the same f32 expression, in the same order, as RayTriangleIntersection
+// (:18-47).  An early-out is taken only when no lane of the wave passes it
+// (uniform branch); otherwise every lane evaluates the full predicate.
+__device__ __forceinline__ bool prim_hit(const sf32x16 r, float dx, float dy, float dz) {
+    const float px = dy * r[5] - r[4] * dz;          // pvec = cross(D, e2)
+    const float py = dz * r[3] - r[5] * dx;
+    const float pz = dx * r[4] - r[3] * dy;
+    const float det = (r[0] * px + r[1] * py) + r[2] * pz;
+    const bool ok_det = !(det <= kDetEps);           // det < 0.000001 (double); NaN passes
+    if (!__any(ok_det)) return false;
+    const float inv = 1.0f / det;
+    const float u = ((r[6] * px + r[7] * py) + r[8] * pz) * inv;
+    const bool ok_u = ok_det && !(u < 0.0f || u > 1.0f);
+    if (!__any(ok_u)) return false;
+    const float v = ((dx * r[9] + dy * r[10]) + dz * r[11]) * inv;
+    const float t = r[12] * inv;
+    return ok_u && !(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX;
+}
+
 template <bool ANYHIT, bool STATS, int LOG2SPP>
 __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) {
     constexpr uint32_t SPP = 1u << LOG2SPP;
@@ -648,8 +680,9 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
     const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + wv;
     uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - D) * 3 * 64;
     const SceneU sc = load_scene(a);
-    const uint4 *__restrict__ nodes = sc.nodes;
-    const float *__restrict__ tris = sc.tris;
+    const cnode_t *nodes = (const cnode_t *)(const void *)a.nodes;
+    const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
+    const cu32_t *dupc = (const cu32_t *)(const void *)a.dup_cnt;
     const uint32_t tiles_x = (a.w + TW - 1) / TW;
     const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
     const float fw = (float)a.w, fh = (float)a.h;
@@ -671,16 +704,28 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
             const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
             camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
         }
-        // Ray::Ray + slab test (reuse the per-lane Walker's start)
-        Walker<ANYHIT, STATS> w;
-        w.start(sc, valid, dx, dy, dz);
-        const float ix = w.ix, iy = w.iy, iz = w.iz;
-        float tMin = w.tMin, tMax = w.tMax;
+        // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
+        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+        float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+        const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+        const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+        bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
+        if (tymin > tMin) tMin = tymin;
+        if (tymax < tMax) tMax = tymax;
+        const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+        const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+        in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+        if (tzmin > tMin) tMin = tzmin;
+        if (tzmax < tMax) tMax = tzmax;
         bool hit = false;
         uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
-        unsigned long long live = __ballot(w.alive);      // lanes whose ray is still searching
+        // lanes whose ray is still searching
+        unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
 
-        // test the triangles [b, b+n) for the lanes in m
+        // test the triangles [b, b+n) for the lanes in m (every lane computes,
+        // only the lanes of m record: no per-lane branch)
         auto test_leaf = [&](uint32_t b, uint32_t n, unsigned long long m) {
             if (STATS && (m & me)) ++c_leaves;
             for (uint32_t i = 0; i < n; ++i) {
@@ -688,43 +733,27 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
                     m &= live;
                     if (!m) break;
                 }
-                const float *tp = tris + 9ull * (b + i);
-                if (m & me) {
-                    if (STATS) ++c_tris;
-                    const bool h = tri_hit(tp, sc.ox, sc.oy, sc.oz, dx, dy, dz);
-                    hit |= h;
-                }
+                const sf32x16 rec = prims[b + i];
+                const bool in = (m & me) != 0ull;
+                if (STATS) c_tris += in ? 1u : 0u;
+                hit |= in && prim_hit(rec, dx, dy, dz);
                 if (ANYHIT) live &= ~__ballot(hit);
             }
         };
 
-#ifdef BIH_PACKET_DEBUG
-        c_nodes = (uint32_t)((live >> lane) & 1ull) + (w.alive ? 10u : 0u) + (valid ? 100u : 0u);
-        live = 0;
-#endif
         if (live && sc.U == 1) {                          // single leaf (reference: UB)
             test_leaf(0, sc.N, live);
         } else if (live) {
-            float st_lo[D], st_hi[D];
-            uint32_t st_nd[D];
+            float st[3 * D];   // per-lane entries {lo, hi, word} indexed by the uniform sp
             uint32_t cur = 0, sp = 0;
             unsigned long long act = live;
-#ifdef BIH_PACKET_DEBUG2
-            const unsigned long long live0 = live;
-            uint32_t dbg_step = 0, dbg_first = 0;
-#endif
             for (;;) {
-#ifdef BIH_PACKET_DEBUG2
-                ++dbg_step;
-                if ((act & ~live0) && !dbg_first) dbg_first = dbg_step;
-                if ((act & ~live0) & me) c_tris = 1000000 + dbg_first;
-#endif
                 if (STATS && (act & me)) ++c_nodes;
-                const uint4 nd = nodes[cur];
+                const su32x4 nd = nodes[cur];
                 const uint32_t ax = (nd.z >> 27) & 3u;
-                const float org = sel3(ax, sc.ox, sc.oy, sc.oz);
+                const float org = ax == 0 ? sc.ox : (ax == 1 ? sc.oy : sc.oz);   // uniform
                 const float inv = sel3(ax, ix, iy, iz);
-                const bool nr = (w.sg >> ax) & 1u;
+                const bool nr = (sg >> ax) & 1u;
                 const float t0 = (__uint_as_float(nd.x) - org) * inv;
                 const float t1 = (__uint_as_float(nd.y) - org) * inv;
                 const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
@@ -743,8 +772,8 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
                 const bool nearL = __popcll(act & mnr) * 2 <= (uint32_t)__popcll(act);
                 if ((leafL && mL) || (leafR && mR)) {
                     uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
-                    if (leafL && cL == 0) cL = sc.dup_cnt[split];
-                    if (leafR && cR == 0) cR = sc.dup_cnt[split + 1];
+                    if (leafL && cL == 0) cL = dupc[split];
+                    if (leafR && cR == 0) cR = dupc[split + 1];
                     if (nearL) {
                         if (leafL && mL) test_leaf(mid - cL, cL, mL);
                         if (leafR && mR) test_leaf(mid, cR, mR);
@@ -766,9 +795,9 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
                     // entry word: node index | this lane's mask bit << 31
                     const uint32_t word = fnode | (((fmask & me) != 0ull) ? 0x80000000u : 0u);
                     if (sp < (uint32_t)D) {
-                        st_lo[sp] = flo;
-                        st_hi[sp] = fhi;
-                        st_nd[sp] = word;
+                        st[3 * sp] = flo;
+                        st[3 * sp + 1] = fhi;
+                        st[3 * sp + 2] = __uint_as_float(word);
                     } else {
                         uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
                         q[0] = __float_as_uint(flo);
@@ -792,9 +821,9 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
                         uint32_t word;
                         float lo, hi;
                         if (sp < (uint32_t)D) {
-                            lo = st_lo[sp];
-                            hi = st_hi[sp];
-                            word = st_nd[sp];
+                            lo = st[3 * sp];
+                            hi = st[3 * sp + 1];
+                            word = __float_as_uint(st[3 * sp + 2]);
                         } else {
                             const uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
                             lo = __uint_as_float(q[0]);
@@ -828,6 +857,32 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
             a.out[lp] = pixel_from_hits(__popcll((hb >> (pix * SPP)) & m), SPP);
         }
     }
+}
+
+// Primary-ray triangle records for the camera origin O (every primary ray of
+// a frame starts at O, Camera.cu:18-20): per Morton-ordered triangle
+// {e1, e2, s = O - v0, q = cross(s, e1), tnum = dot(e2, q), 0, 0, 0}, the
+// ray-independent half of RayTriangleIntersection (:18-19, :33, :40, :47),
+// computed once per origin instead of once per ray.
+__global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__ tris, uint32_t n,
+                                                       float ox, float oy, float oz,
+                                                       float *__restrict__ prim) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float *t = tris + 9ull * i;
+    const float v0x = t[0], v0y = t[1], v0z = t[2];
+    const float e1x = t[3], e1y = t[4], e1z = t[5];
+    const float e2x = t[6], e2y = t[7], e2z = t[8];
+    const float sx = ox - v0x, sy = oy - v0y, sz = oz - v0z;    // tvec
+    const float qx = sy * e1z - e1y * sz;                       // qvec = cross(tvec, e1)
+    const float qy = sz * e1x - e1z * sx;
+    const float qz = sx * e1y - e1x * sy;
+    const float tn = (e2x * qx + e2y * qy) + e2z * qz;          // dot(e2, qvec)
+    float4 *o = reinterpret_cast<float4 *>(prim + 16ull * i);
+    o[0] = make_float4(e1x, e1y, e1z, e2x);
+    o[1] = make_float4(e2y, e2z, sx, sy);
+    o[2] = make_float4(sz, qx, qy, qz);
+    o[3] = make_float4(tn, 0.f, 0.f, 0.f);
 }
 
 std::mutex g_tab_mu;
@@ -911,6 +966,18 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
+int launch_tri_prim(const float *tris, uint32_t n, const float origin[3], float *prim, void *stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       (hipStream_t)stream, tris, n, origin[0], origin[1], origin[2], prim);
+    return (int)hipGetLastError();
+}
+
+bool render_uses_prim(uint32_t spp) {
+    static const Variant var = variant_from_env();
+    return var == Variant::Packet && spp <= 64 && (spp & (spp - 1)) == 0;
+}
+
 // Resident blocks of the persistent kernels on `device` (grid size).
 uint32_t wave_grid_blocks(int device) {
     static std::mutex mu;
@@ -933,7 +1000,11 @@ uint32_t wave_grid_blocks(int device) {
 }
 
 size_t spill_words(uint32_t blocks) {
-    return (size_t)blocks * kThreads * (kStackDepth - kLdsStack) * 3;
+    // per block: per-lane kernels [(32-kLdsStack)*3][256 lanes]; packet kernel
+    // 4 waves x [(32-kPacketRegs)*3][64 lanes] -- size for the larger
+    const size_t lane_k = (size_t)kThreads * (kStackDepth - kLdsStack) * 3;
+    const size_t packet_k = (size_t)(kThreads / 64) * (kStackDepth - kPacketRegs) * 3 * 64;
+    return (size_t)blocks * (lane_k > packet_k ? lane_k : packet_k);
 }
 
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
