@@ -37,7 +37,8 @@ struct bih_tree {
     bool owns_stream = false;
     uint32_t *work = nullptr;        // persistent-kernel tile counter
     uint32_t *spill = nullptr;       // traversal stack spill area
-    float *prim = nullptr;           // primary-ray triangle records (16 f32 / tri)
+    float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
+    size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
     uint32_t prim_origin[3] = {0, 0, 0};   // bit patterns of the origin they were built for
 };
@@ -349,16 +350,23 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
     // primary-ray triangle records follow the camera origin
+    const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
     if (bih::render_uses_prim(spp) && tr->t.n > 0) {
         uint32_t ob[3];
         memcpy(ob, cam->origin, sizeof ob);
-        if (!tr->prim) {
-            hipError_t e = hipMalloc((void **)&tr->prim, (size_t)tr->t.n * 64);
+        const size_t need = bih::prim_bytes(tr->t.n, n_int);
+        if (tr->prim_cap < need) {
+            if (tr->prim) (void)hipFree(tr->prim);
+            tr->prim = nullptr;
+            tr->prim_cap = 0;
+            hipError_t e = hipMalloc((void **)&tr->prim, need);
             if (e != hipSuccess) return map_hip((int)e);
+            tr->prim_cap = need;
             tr->prim_valid = false;
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
-            int e = bih::launch_tri_prim(tr->t.tris_s, tr->t.n, cam->origin, tr->prim, st);
+            int e = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, n_int, cam->origin,
+                                     tr->prim, st);
             if (e) return map_hip(e);
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
@@ -380,6 +388,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
     a.tri_prim = tr->prim;
+    a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
     const size_t P = (size_t)rows.nrows * w;
     a.rng_in = tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap;

@@ -58,6 +58,7 @@ struct RenderArgs {
     const uint4 *nodes;
     const float *tris;
     const float *tri_prim;  // 16 f32 per triangle: primary-ray records for origin cam[0..2]
+    const uint4 *node_prim; // per node {clip0 - O[axis], clip1 - O[axis], z, w} for the same origin
     const uint32_t *dup_cnt;
     const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame
     uint32_t *rng_out;      // state after the frame (double-buffered: a pixel's
@@ -107,8 +108,11 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);
-// primary-ray triangle records (k_tri_prim) for camera origin `origin`
-int launch_tri_prim(const float *tris, uint32_t n, const float origin[3], float *prim, void *stream);
+// primary-ray records for camera origin `origin`: n triangle records
+// (16 f32, k_tri_prim) followed by m = U-1 node records (u32x4, k_node_prim)
+size_t prim_bytes(uint32_t n, uint32_t m);
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
+                float *prim, void *stream);
 bool render_uses_prim(uint32_t spp);
 
 // host XORWOW helpers (xorwow_host.cpp)

@@ -859,6 +859,241 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_render_packet2: the packet walk of k_render_packet, restructured so that
+// the per-node work is mostly VALU and the wave-uniform control stays short:
+//   * node records relative to the camera origin (k_node_prim): t = d * inv
+//     with d = clip - O[axis] computed once per origin (same f32 subtraction
+//     as the reference's (clip - origin[axis]), CUDAKernels.cu:300-301);
+//   * no near/far swap: with s = sign of this lane's direction on the axis,
+//       left  visited iff (t0 > (s ? tMax : tMin)) xor s,
+//       right visited iff (t1 > (s ? tMin : tMax)) xnor s,
+//     which is exactly tMin < t[near] (near) and !(tMax < t[far]) (far),
+//     NaNs included (a NaN compare is false on both sides);
+//   * hits kept as one wave-uniform mask; triangle early-outs on the lanes
+//     that actually test the leaf;
+//   * child order chosen once per packet and axis (majority direction).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long prim_hits(const sf32x16 r, float dx, float dy, float dz,
+                                                       unsigned long long m) {
+    const float px = dy * r[5] - r[4] * dz;          // pvec = cross(D, e2)
+    const float py = dz * r[3] - r[5] * dx;
+    const float pz = dx * r[4] - r[3] * dy;
+    const float det = (r[0] * px + r[1] * py) + r[2] * pz;
+    m &= __ballot(!(det <= kDetEps));                // det < 0.000001 (double); NaN passes
+    if (!m) return 0ull;
+    const float inv = 1.0f / det;
+    const float u = ((r[6] * px + r[7] * py) + r[8] * pz) * inv;
+    m &= __ballot(!(u < 0.0f || u > 1.0f));
+    if (!m) return 0ull;
+    const float v = ((dx * r[9] + dy * r[10]) + dz * r[11]) * inv;
+    const float t = r[12] * inv;
+    return m & __ballot(!(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX);
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool ANYHIT, bool STATS, int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    constexpr int D = kPacketRegs;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned long long me = lane_bit(lane);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + wv;
+    uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - D) * 3 * 64;
+    const SceneU sc = load_scene(a);
+    const cnode_t *nodes = (const cnode_t *)(const void *)a.node_prim;
+    const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
+    const cu32_t *dupc = (const cu32_t *)(const void *)a.dup_cnt;
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+
+    for (;;) {
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(a.work, 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles) break;
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        float dx = 0.f, dy = 0.f, dz = 1.f;
+        if (valid) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
+        }
+        // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
+        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+        float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+        const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+        const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+        bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
+        if (tymin > tMin) tMin = tymin;
+        if (tymax < tMax) tMax = tymax;
+        const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+        const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+        in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+        if (tzmin > tMin) tMin = tzmin;
+        if (tzmax < tMax) tMax = tzmax;
+        uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
+        const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+        unsigned long long hits = 0ull;   // lanes whose ray hit some tested triangle
+        const f32x4 invv = {ix, iy, iz, 0.0f};
+        // left child first on an axis when most of the packet runs +axis there
+        uint32_t nearbits = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k) {
+            const unsigned long long neg = __ballot((sg >> k) & 1u) & live;
+            if (__popcll(neg) * 2 <= __popcll(live)) nearbits |= 1u << k;
+        }
+
+        // test triangles [b, b+n) for the lanes of m
+        auto test_leaf = [&](uint32_t b, uint32_t n, unsigned long long m) {
+            if (STATS && (m & me)) ++c_leaves;
+            for (uint32_t i = 0; i < n; ++i) {
+                if (ANYHIT) {
+                    m &= ~hits;
+                    if (!m) break;
+                }
+                if (STATS && (m & me)) ++c_tris;
+                hits |= prim_hits(prims[b + i], dx, dy, dz, m);
+            }
+        };
+
+        if (live && sc.U == 1) {                          // single leaf (reference: UB)
+            test_leaf(0, sc.N, live);
+        } else if (live) {
+            // per-lane entries {lo, hi, node | this lane's mask bit << 31}, one
+            // interleaved array (private memory: one dwordx3 access per push/pop)
+            float st[3 * D];
+            uint32_t cur = 0, sp = 0;
+            unsigned long long act = live;
+            for (;;) {
+                if (STATS && (act & me)) ++c_nodes;
+                const su32x4 nd = nodes[cur];
+                const uint32_t ax = (nd.z >> 27) & 3u;
+                const float inv = invv[ax];
+                const bool neg = (sg >> ax) & 1u;
+                const float t0 = __uint_as_float(nd.x) * inv;
+                const float t1 = __uint_as_float(nd.y) * inv;
+                const unsigned long long mneg = __ballot(neg);
+                unsigned long long gL = (__ballot(t0 > (neg ? tMax : tMin)) ^ mneg) & act;
+                unsigned long long gR = ~(__ballot(t1 > (neg ? tMin : tMax)) ^ mneg) & act;
+                const float lo_L = neg ? t0 : tMin, hi_L = neg ? tMax : t0;
+                const float lo_R = neg ? tMin : t1, hi_R = neg ? t1 : tMax;
+                const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
+                const uint32_t leaf = nd.z >> 29;         // bit 0: left is a leaf, bit 1: right
+                const uint32_t nearL = (nearbits >> ax) & 1u;
+                if (leaf) {
+                    const unsigned long long tL = (leaf & 1u) ? gL : 0ull;
+                    const unsigned long long tR = (leaf & 2u) ? gR : 0ull;
+                    if (tL | tR) {
+                        uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
+                        if (tL && cL == 0) cL = dupc[split];
+                        if (tR && cR == 0) cR = dupc[split + 1];
+                        if (nearL) {
+                            if (tL) test_leaf(mid - cL, cL, tL);
+                            if (tR) test_leaf(mid, cR, tR);
+                        } else {
+                            if (tR) test_leaf(mid, cR, tR);
+                            if (tL) test_leaf(mid - cL, cL, tL);
+                        }
+                    }
+                    if (leaf & 1u) gL = 0ull;
+                    if (leaf & 2u) gR = 0ull;
+                    if (ANYHIT) {
+                        gL &= ~hits;
+                        gR &= ~hits;
+                    }
+                }
+                if (gL | gR) {
+                    const uint32_t takeL = (gL && gR) ? nearL : (gL ? 1u : 0u);
+                    if (gL && gR) {
+                        // descend one child, stack the other (node, mask bit, interval)
+                        const unsigned long long om = takeL ? gR : gL;
+                        const float olo = takeL ? lo_R : lo_L, ohi = takeL ? hi_R : hi_L;
+                        const uint32_t word = (split + takeL) | ((uint32_t)((om >> lane) & 1ull) << 31);
+                        if (sp < (uint32_t)D) {
+                            st[3 * sp] = olo;
+                            st[3 * sp + 1] = ohi;
+                            st[3 * sp + 2] = __uint_as_float(word);
+                        } else {
+                            uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
+                            q[0] = __float_as_uint(olo);
+                            q[64] = __float_as_uint(ohi);
+                            q[128] = word;
+                        }
+                        ++sp;
+                    }
+                    cur = split + (takeL ^ 1u);
+                    act = takeL ? gL : gR;
+                    tMin = takeL ? lo_L : lo_R;
+                    tMax = takeL ? hi_L : hi_R;
+                    continue;
+                }
+                // pop until an entry still has a searching lane
+                bool found = false;
+                while (sp > 0) {
+                    --sp;
+                    uint32_t word;
+                    float lo, hi;
+                    if (sp < (uint32_t)D) {
+                        lo = st[3 * sp];
+                        hi = st[3 * sp + 1];
+                        word = __float_as_uint(st[3 * sp + 2]);
+                    } else {
+                        const uint32_t *q = wspill + ((sp - D) * 3) * 64 + lane;
+                        lo = __uint_as_float(q[0]);
+                        hi = __uint_as_float(q[64]);
+                        word = q[128];
+                    }
+                    unsigned long long m = __ballot(word >> 31);
+                    if (ANYHIT) m &= ~hits;
+                    if (!m) continue;
+                    cur = __builtin_amdgcn_readfirstlane(word & 0x7fffffffu);
+                    act = m;
+                    tMin = lo;
+                    tMax = hi;
+                    found = true;
+                    break;
+                }
+                if (!found) break;
+            }
+        }
+
+        if (STATS && valid) {
+            const uint64_t rid = lp * SPP + s;
+            a.ray_stats[3 * rid] = c_nodes;
+            a.ray_stats[3 * rid + 1] = c_leaves;
+            a.ray_stats[3 * rid + 2] = c_tris;
+        }
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+        }
+    }
+}
+
+// Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}.
+__global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict__ nodes, uint32_t m,
+                                                        float ox, float oy, float oz,
+                                                        uint4 *__restrict__ out) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= m) return;
+    const uint4 nd = nodes[i];
+    const uint32_t ax = (nd.z >> 27) & 3u;
+    const float org = sel3(ax, ox, oy, oz);
+    out[i] = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
+                        __float_as_uint(__uint_as_float(nd.y) - org), nd.z, nd.w);
+}
+
 // Primary-ray triangle records for the camera origin O (every primary ray of
 // a frame starts at O, Camera.cu:18-20): per Morton-ordered triangle
 // {e1, e2, s = O - v0, q = cross(s, e1), tnum = dot(e2, q), 0, 0, 0}, the
@@ -888,12 +1123,13 @@ __global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__
 std::mutex g_tab_mu;
 uint32_t *g_tab_dev[64] = {nullptr};
 
-enum class Variant { Tile, Refill, Packet };
+enum class Variant { Tile, Refill, Packet1, Packet };
 
 Variant variant_from_env() {
     const char *e = getenv("BIH_RENDER_KERNEL");
     if (e && strcmp(e, "tile") == 0) return Variant::Tile;
     if (e && strcmp(e, "refill") == 0) return Variant::Refill;
+    if (e && strcmp(e, "packet1") == 0) return Variant::Packet1;
     return Variant::Packet;
 }
 
@@ -918,13 +1154,21 @@ hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse
             if (stats) hipLaunchKernelGGL((k_render_refill<false, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_refill<false, false, L>), g, b, 0, st, a);
         }
-    } else {
+    } else if (var == Variant::Packet1) {
         if (traverse == 0) {
             if (stats) hipLaunchKernelGGL((k_render_packet<true, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet<true, false, L>), g, b, 0, st, a);
         } else {
             if (stats) hipLaunchKernelGGL((k_render_packet<false, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet<false, false, L>), g, b, 0, st, a);
+        }
+    } else {
+        if (traverse == 0) {
+            if (stats) hipLaunchKernelGGL((k_render_packet2<true, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet2<true, false, L>), g, b, 0, st, a);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_render_packet2<false, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet2<false, false, L>), g, b, 0, st, a);
         }
     }
     return hipGetLastError();
@@ -966,16 +1210,23 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
-int launch_tri_prim(const float *tris, uint32_t n, const float origin[3], float *prim, void *stream) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       (hipStream_t)stream, tris, n, origin[0], origin[1], origin[2], prim);
+size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + (size_t)m * 16; }
+
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
+                float *prim, void *stream) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                           (hipStream_t)stream, tris, n, origin[0], origin[1], origin[2], prim);
+    if (m > 0)
+        hipLaunchKernelGGL(k_node_prim, dim3((m + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                           (hipStream_t)stream, nodes, m, origin[0], origin[1], origin[2],
+                           reinterpret_cast<uint4 *>(prim + 16ull * n));
     return (int)hipGetLastError();
 }
 
 bool render_uses_prim(uint32_t spp) {
     static const Variant var = variant_from_env();
-    return var == Variant::Packet && spp <= 64 && (spp & (spp - 1)) == 0;
+    return (var == Variant::Packet || var == Variant::Packet1) && spp <= 64 && (spp & (spp - 1)) == 0;
 }
 
 // Resident blocks of the persistent kernels on `device` (grid size).
@@ -985,13 +1236,21 @@ uint32_t wave_grid_blocks(int device) {
     std::lock_guard<std::mutex> lk(mu);
     if (device < 0 || device >= 64) return 0;
     if (!cache[device]) {
-        int cus = 0, per = 0, per2 = 0;
+        // resident blocks per CU: the largest over the persistent kernels
+        // (the LDS-stack kernels fit fewer than the register-stack packet ones)
+        const void *kernels[] = {
+            reinterpret_cast<const void *>(k_render_refill<true, false, 2>),
+            reinterpret_cast<const void *>(k_render_tile<true, false, 2>),
+            reinterpret_cast<const void *>(k_render_packet<true, false, 2>),
+            reinterpret_cast<const void *>(k_render_packet2<true, false, 2>),
+        };
+        int cus = 0, per = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, reinterpret_cast<const void *>(k_render_refill<true, false, 2>), kThreads, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per2, reinterpret_cast<const void *>(k_render_tile<true, false, 2>), kThreads, 0);
-        if (per2 > per) per = per2;
+        for (const void *k : kernels) {
+            int p = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, k, kThreads, 0);
+            if (p > per) per = p;
+        }
         if (cus <= 0) cus = 256;
         if (per <= 0) per = 1;
         cache[device] = (uint32_t)(cus * per);
