@@ -6,6 +6,7 @@
 // both, per device, and errors are returned instead of exit(99)
 // (src/Renderer.cpp:63-73).
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -335,7 +336,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     if (!tr->work) {
-        hipError_t e = hipMalloc((void **)&tr->work, 64);
+        hipError_t e = hipMalloc((void **)&tr->work, bih::kWorkWords * sizeof(uint32_t));
         if (e == hipSuccess)
             e = hipMalloc((void **)&tr->spill,
                           bih::spill_words(bih::wave_grid_blocks(tr->t.device)) * sizeof(uint32_t));
@@ -414,6 +415,18 @@ int bih_sync(const bih_tree *tr, void *stream) {
     if (!tr) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+#if BIH_PACKET_COUNTERS
+    if (tr->work) {
+        uint32_t c[bih::kWorkWords];
+        if (hipMemcpyAsync(c, tr->work, sizeof c, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            fprintf(stderr, "packet-counters packets %u nodes %u leaves %u tris %u pushes %u pops %u maxsp %u depth",
+                    c[16], c[17], c[18], c[19], c[20], c[21], c[22]);
+            for (int k = 0; k < 32; ++k) fprintf(stderr, " %u", c[24 + k]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
     return map_hip((int)hipStreamSynchronize(st));
 }
 

@@ -891,7 +891,45 @@ __device__ __forceinline__ unsigned long long prim_hits(const sf32x16 r, float d
     return m & __ballot(!(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX);
 }
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+
+// The descend decision of one packet node step, wave-uniform: pickL = take
+// the left child (nearL ? gL != 0 : gR == 0); the taken child gets mask gT,
+// node cT and its lanes' intervals, the other (gO, cO, olo/ohi) is stacked
+// when gO != 0.  Written as one SALU/VALU sequence (hipcc's own lowering of
+// the same selects spends about twice the scalar instructions).
+__device__ __forceinline__ void descend_pick(unsigned long long gL, unsigned long long gR,
+                                             uint32_t nearL, uint32_t split, float loL, float hiL,
+                                             float loR, float hiR, unsigned long long &gT,
+                                             unsigned long long &gO, uint32_t &cT, uint32_t &cO,
+                                             float &tlo, float &thi, float &olo, float &ohi) {
+    uint32_t p, q;
+    unsigned long long mk;
+    asm volatile(
+        "s_cmp_lg_u64 %[gL], 0\n\t"
+        "s_cselect_b32 %[p], 1, 0\n\t"
+        "s_cmp_eq_u64 %[gR], 0\n\t"
+        "s_cselect_b32 %[q], 1, 0\n\t"
+        "s_cmp_lg_u32 %[nearL], 0\n\t"
+        "s_cselect_b32 %[p], %[p], %[q]\n\t"
+        "s_cmp_lg_u32 %[p], 0\n\t"
+        "s_cselect_b64 %[gT], %[gL], %[gR]\n\t"
+        "s_cselect_b64 %[gO], %[gR], %[gL]\n\t"
+        "s_cselect_b64 %[mk], -1, 0\n\t"
+        "s_add_u32 %[cO], %[split], %[p]\n\t"
+        "s_xor_b32 %[q], %[p], 1\n\t"
+        "s_add_u32 %[cT], %[split], %[q]\n\t"
+        "v_cndmask_b32_e64 %[tlo], %[loR], %[loL], %[mk]\n\t"
+        "v_cndmask_b32_e64 %[thi], %[hiR], %[hiL], %[mk]\n\t"
+        "v_cndmask_b32_e64 %[olo], %[loL], %[loR], %[mk]\n\t"
+        "v_cndmask_b32_e64 %[ohi], %[hiL], %[hiR], %[mk]"
+        : [p] "=&s"(p), [q] "=&s"(q), [mk] "=&s"(mk), [gT] "=&s"(gT), [gO] "=&s"(gO),
+          [cT] "=&s"(cT), [cO] "=&s"(cO), [tlo] "=&v"(tlo), [thi] "=&v"(thi), [olo] "=&v"(olo),
+          [ohi] "=&v"(ohi)
+        : [gL] "s"(gL), [gR] "s"(gR), [nearL] "s"(nearL), [split] "s"(split), [loL] "v"(loL),
+          [hiL] "v"(hiL), [loR] "v"(loR), [hiR] "v"(hiR)
+        : "scc");
+}
 
 template <bool ANYHIT, bool STATS, int LOG2SPP>
 __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a) {
@@ -943,9 +981,11 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
         if (tzmin > tMin) tMin = tzmin;
         if (tzmax < tMax) tMax = tzmax;
         uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
+#if BIH_PACKET_COUNTERS
+        uint32_t pk[8] = {1, 0, 0, 0, 0, 0, 0, 0};   // packet-level walk counters (debug builds)
+#endif
         const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
         unsigned long long hits = 0ull;   // lanes whose ray hit some tested triangle
-        const f32x4 invv = {ix, iy, iz, 0.0f};
         // left child first on an axis when most of the packet runs +axis there
         uint32_t nearbits = 0;
 #pragma unroll
@@ -957,13 +997,19 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
         // test triangles [b, b+n) for the lanes of m
         auto test_leaf = [&](uint32_t b, uint32_t n, unsigned long long m) {
             if (STATS && (m & me)) ++c_leaves;
-            for (uint32_t i = 0; i < n; ++i) {
+#if BIH_PACKET_COUNTERS
+            ++pk[2];
+#endif
+            for (const uint32_t e = b + n; b < e; ++b) {
                 if (ANYHIT) {
                     m &= ~hits;
                     if (!m) break;
                 }
+#if BIH_PACKET_COUNTERS
+                ++pk[3];
+#endif
                 if (STATS && (m & me)) ++c_tris;
-                hits |= prim_hits(prims[b + i], dx, dy, dz, m);
+                hits |= prim_hits(prims[b], dx, dy, dz, m);
             }
         };
 
@@ -977,9 +1023,13 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
             unsigned long long act = live;
             for (;;) {
                 if (STATS && (act & me)) ++c_nodes;
+#if BIH_PACKET_COUNTERS
+                ++pk[1];
+#endif
                 const su32x4 nd = nodes[cur];
                 const uint32_t ax = (nd.z >> 27) & 3u;
-                const float inv = invv[ax];
+                // axis 0/1/2 from bits 27 and 28 of z (uniform bit tests)
+                const float inv = (nd.z & (1u << 28)) ? iz : ((nd.z & (1u << 27)) ? iy : ix);
                 const bool neg = (sg >> ax) & 1u;
                 const float t0 = __uint_as_float(nd.x) * inv;
                 const float t1 = __uint_as_float(nd.y) * inv;
@@ -1014,13 +1064,16 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                     }
                 }
                 if (gL | gR) {
-                    const uint32_t takeL = (gL && gR) ? nearL : (gL ? 1u : 0u);
-                    if (gL && gR) {
-                        // descend one child, stack the other (node, mask bit, interval)
-                        const unsigned long long om = takeL ? gR : gL;
-                        const float olo = takeL ? lo_R : lo_L, ohi = takeL ? hi_R : hi_L;
-                        const uint32_t word = (split + takeL) | ((uint32_t)((om >> lane) & 1ull) << 31);
-                        if (sp < (uint32_t)D) {
+                    // take the near child (majority order) when both are
+                    // visited, else the only one; stack the other if visited
+                    unsigned long long gT, gO;
+                    uint32_t cT, cO;
+                    float tlo, thi, olo, ohi;
+                    descend_pick(gL, gR, nearL, split, lo_L, hi_L, lo_R, hi_R, gT, gO, cT, cO, tlo,
+                                 thi, olo, ohi);
+                    if (gO) {
+                        const uint32_t word = cO | ((uint32_t)((gO >> lane) & 1ull) << 31);
+                        if (__builtin_expect(sp < (uint32_t)D, 1)) {
                             st[3 * sp] = olo;
                             st[3 * sp + 1] = ohi;
                             st[3 * sp + 2] = __uint_as_float(word);
@@ -1030,18 +1083,26 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                             q[64] = __float_as_uint(ohi);
                             q[128] = word;
                         }
+#if BIH_PACKET_COUNTERS
+                        ++pk[4];
+                        if (lane == 0) atomicAdd(a.work + 24 + (sp < 32 ? sp : 31), 1u);
+                        pk[6] = sp + 1 > pk[6] ? sp + 1 : pk[6];
+#endif
                         ++sp;
                     }
-                    cur = split + (takeL ^ 1u);
-                    act = takeL ? gL : gR;
-                    tMin = takeL ? lo_L : lo_R;
-                    tMax = takeL ? hi_L : hi_R;
+                    cur = cT;
+                    act = gT;
+                    tMin = tlo;
+                    tMax = thi;
                     continue;
                 }
                 // pop until an entry still has a searching lane
                 bool found = false;
                 while (sp > 0) {
                     --sp;
+#if BIH_PACKET_COUNTERS
+                    ++pk[5];
+#endif
                     uint32_t word;
                     float lo, hi;
                     if (sp < (uint32_t)D) {
@@ -1068,6 +1129,12 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
             }
         }
 
+#if BIH_PACKET_COUNTERS
+        if (lane == 0) {
+            for (int k = 0; k < 6; ++k) atomicAdd(a.work + 16 + k, pk[k]);
+            atomicMax(a.work + 22, pk[6]);
+        }
+#endif
         if (STATS && valid) {
             const uint64_t rid = lp * SPP + s;
             a.ray_stats[3 * rid] = c_nodes;
@@ -1281,7 +1348,11 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         if (tiles == 0) return 0;
         uint32_t blocks = (uint32_t)((tiles + 3) / 4);
         if (blocks > grid) blocks = grid;
+#if BIH_PACKET_COUNTERS
+        hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
+#else
         hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), st);
+#endif
         if (e != hipSuccess) return (int)e;
         switch (L) {
         case 0: e = launch_persistent<0>(var, a, traverse, st, blocks); break;
