@@ -386,6 +386,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     bih::xorwow_seed(seed, v, &d0);
     a.d_base = d0 + (uint32_t)((uint64_t)2 * spp * frame) * 362437u;
     a.hdr = tr->t.hdr;
+    a.hdr_n_tris = tr->t.n;
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
     a.tri_prim = tr->prim;

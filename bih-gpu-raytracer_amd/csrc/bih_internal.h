@@ -59,6 +59,7 @@ struct RenderArgs {
     uint32_t w, h, spp;
     uint32_t row0, nrows, band_h, band_step;
     uint32_t d_base;        // XORWOW Weyl counter at the start of this frame
+    uint32_t hdr_n_tris;    // host copy of hdr->n_tris (kernel choice)
     const TreeHeader *hdr;
     const uint4 *nodes;
     const float *tris;

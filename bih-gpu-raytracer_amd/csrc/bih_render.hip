@@ -35,6 +35,7 @@
 #include <mutex>
 
 #include "bih_internal.h"
+#include "bih_packet_asm.h"
 
 namespace bih {
 namespace {
@@ -1148,6 +1149,145 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
+// loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
+// offsets are 32-bit in the loop: used for scenes of < 2^26 triangles.
+// ---------------------------------------------------------------------------
+template <bool ANYHIT, bool STATS, int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_packet_asm(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + wv;
+    const uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - kPacketRegs) * 3 * 64;
+    const SceneU sc = load_scene(a);
+    const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
+    const void *nodes = (const void *)a.node_prim;
+    const void *dupc = (const void *)a.dup_cnt;
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+    const uint32_t lane4 = lane * 4u;
+    const uint32_t snan = 0x7f800001u;
+    const uint32_t eps = __float_as_uint(kDetEps), fmax = __float_as_uint(FLT_MAX);
+
+    for (;;) {
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(a.work, 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles) break;
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        float dx = 0.f, dy = 0.f, dz = 1.f;
+        if (valid) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
+        }
+        // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
+        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+        float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+        const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+        const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+        bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
+        if (tymin > tMin) tMin = tymin;
+        if (tymax < tMax) tMax = tymax;
+        const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+        const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+        in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+        if (tzmin > tMin) tMin = tzmin;
+        if (tzmax < tMax) tMax = tzmax;
+        uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
+        const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+        unsigned long long hits = 0ull;
+        uint32_t nearbits = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k) {
+            const unsigned long long neg = __ballot((sg >> k) & 1u) & live;
+            if (__popcll(neg) * 2 <= __popcll(live)) nearbits |= 1u << k;
+        }
+        nearbits = __builtin_amdgcn_readfirstlane(nearbits);
+        if (live && sc.U == 1) {                          // single leaf (reference: UB)
+            unsigned long long m = live;
+            if (STATS && (m & lane_bit(lane))) ++c_leaves;
+            for (uint32_t b = 0; b < sc.N; ++b) {
+                if (ANYHIT) {
+                    m &= ~hits;
+                    if (!m) break;
+                }
+                if (STATS && (m & lane_bit(lane))) ++c_tris;
+                hits |= prim_hits(prims[b], dx, dy, dz, m);
+            }
+        } else if (live) {
+            if constexpr (ANYHIT && !STATS) {
+                asm volatile(BIH_PACKET_WALK(BIH_ANY_ON, BIH_CLR_ON,
+                                             BIH_POP_ANY,
+                                             "", "", "", "", "")
+                             : [hits] "=&s"(hits), [tmin] "+v"(tMin), [tmax] "+v"(tMax)
+                             : [nodes] "s"(nodes), [prims] "s"(prims), [dupc] "s"(dupc),
+                               [spill] "s"(wspill), [live] "s"(live), [near] "s"(nearbits),
+                               [eps] "s"(eps), [fmax] "s"(fmax), [snan] "v"(snan),
+                               [lane4] "v"(lane4), [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz),
+                               [ix] "v"(ix), [iy] "v"(iy), [iz] "v"(iz), [sgn] "v"(sg)
+                             : BIH_PACKET_CLOBBERS);
+            } else if constexpr (ANYHIT && STATS) {
+                asm volatile(BIH_PACKET_WALK(BIH_ANY_ON, BIH_CLR_ON,
+                                             BIH_POP_ANY,
+                                             BIH_CNT_NODE, BIH_CNT_LEAF_L, BIH_CNT_LEAF_R,
+                                             BIH_CNT_TRI_L, BIH_CNT_TRI_R)
+                             : [hits] "=&s"(hits), [tmin] "+v"(tMin), [tmax] "+v"(tMax),
+                               [cn] "+v"(c_nodes), [cl] "+v"(c_leaves), [ct] "+v"(c_tris)
+                             : [nodes] "s"(nodes), [prims] "s"(prims), [dupc] "s"(dupc),
+                               [spill] "s"(wspill), [live] "s"(live), [near] "s"(nearbits),
+                               [eps] "s"(eps), [fmax] "s"(fmax), [snan] "v"(snan),
+                               [lane4] "v"(lane4), [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz),
+                               [ix] "v"(ix), [iy] "v"(iy), [iz] "v"(iz), [sgn] "v"(sg)
+                             : BIH_PACKET_CLOBBERS);
+            } else if constexpr (!ANYHIT && !STATS) {
+                asm volatile(BIH_PACKET_WALK(BIH_ANY_OFF, BIH_CLR_OFF, "", "", "", "", "", "")
+                             : [hits] "=&s"(hits), [tmin] "+v"(tMin), [tmax] "+v"(tMax)
+                             : [nodes] "s"(nodes), [prims] "s"(prims), [dupc] "s"(dupc),
+                               [spill] "s"(wspill), [live] "s"(live), [near] "s"(nearbits),
+                               [eps] "s"(eps), [fmax] "s"(fmax), [snan] "v"(snan),
+                               [lane4] "v"(lane4), [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz),
+                               [ix] "v"(ix), [iy] "v"(iy), [iz] "v"(iz), [sgn] "v"(sg)
+                             : BIH_PACKET_CLOBBERS);
+            } else {
+                asm volatile(BIH_PACKET_WALK(BIH_ANY_OFF, BIH_CLR_OFF, "",
+                                             BIH_CNT_NODE, BIH_CNT_LEAF_L, BIH_CNT_LEAF_R,
+                                             BIH_CNT_TRI_L, BIH_CNT_TRI_R)
+                             : [hits] "=&s"(hits), [tmin] "+v"(tMin), [tmax] "+v"(tMax),
+                               [cn] "+v"(c_nodes), [cl] "+v"(c_leaves), [ct] "+v"(c_tris)
+                             : [nodes] "s"(nodes), [prims] "s"(prims), [dupc] "s"(dupc),
+                               [spill] "s"(wspill), [live] "s"(live), [near] "s"(nearbits),
+                               [eps] "s"(eps), [fmax] "s"(fmax), [snan] "v"(snan),
+                               [lane4] "v"(lane4), [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz),
+                               [ix] "v"(ix), [iy] "v"(iy), [iz] "v"(iz), [sgn] "v"(sg)
+                             : BIH_PACKET_CLOBBERS);
+            }
+        }
+
+        if (STATS && valid) {
+            const uint64_t rid = lp * SPP + s;
+            a.ray_stats[3 * rid] = c_nodes;
+            a.ray_stats[3 * rid + 1] = c_leaves;
+            a.ray_stats[3 * rid + 2] = c_tris;
+        }
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+        }
+    }
+}
+
 // Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}.
 __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict__ nodes, uint32_t m,
                                                         float ox, float oy, float oz,
@@ -1190,14 +1330,15 @@ __global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__
 std::mutex g_tab_mu;
 uint32_t *g_tab_dev[64] = {nullptr};
 
-enum class Variant { Tile, Refill, Packet1, Packet };
+enum class Variant { Tile, Refill, Packet1, Packet2, PacketAsm };
 
 Variant variant_from_env() {
     const char *e = getenv("BIH_RENDER_KERNEL");
     if (e && strcmp(e, "tile") == 0) return Variant::Tile;
     if (e && strcmp(e, "refill") == 0) return Variant::Refill;
     if (e && strcmp(e, "packet1") == 0) return Variant::Packet1;
-    return Variant::Packet;
+    if (e && strcmp(e, "packet2") == 0) return Variant::Packet2;
+    return Variant::PacketAsm;
 }
 
 template <int L>
@@ -1228,6 +1369,14 @@ hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse
         } else {
             if (stats) hipLaunchKernelGGL((k_render_packet<false, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet<false, false, L>), g, b, 0, st, a);
+        }
+    } else if (var == Variant::PacketAsm && a.hdr_n_tris < (1u << 26)) {
+        if (traverse == 0) {
+            if (stats) hipLaunchKernelGGL((k_render_packet_asm<true, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet_asm<true, false, L>), g, b, 0, st, a);
+        } else {
+            if (stats) hipLaunchKernelGGL((k_render_packet_asm<false, true, L>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((k_render_packet_asm<false, false, L>), g, b, 0, st, a);
         }
     } else {
         if (traverse == 0) {
@@ -1293,7 +1442,7 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, c
 
 bool render_uses_prim(uint32_t spp) {
     static const Variant var = variant_from_env();
-    return (var == Variant::Packet || var == Variant::Packet1) && spp <= 64 && (spp & (spp - 1)) == 0;
+    return var != Variant::Tile && var != Variant::Refill && spp <= 64 && (spp & (spp - 1)) == 0;
 }
 
 // Resident blocks of the persistent kernels on `device` (grid size).
@@ -1310,6 +1459,7 @@ uint32_t wave_grid_blocks(int device) {
             reinterpret_cast<const void *>(k_render_tile<true, false, 2>),
             reinterpret_cast<const void *>(k_render_packet<true, false, 2>),
             reinterpret_cast<const void *>(k_render_packet2<true, false, 2>),
+            reinterpret_cast<const void *>(k_render_packet_asm<true, false, 2>),
         };
         int cus = 0, per = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
