@@ -16,6 +16,7 @@
 //   s[68:69]  left-leaf lanes  s[70:71] right-leaf lanes  s[72:73] tmp
 //   s74 cur  s75 sp  s76 axis  s77 split  s78-s80 tmp  s81 b  s82 e
 //   s83 saved m0  s84 mid  s85 near bit
+//   s[88:95]  prefetched records of the current node's children (split, split+1)
 //   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of left/right
 //   v33-v38 temps (MT: v35-v37 p, v38 det then 1/det)  v39 stacked node ids
 //   (lane k = slot k)  v40-v51 stacked lo (slot = gpr index)  v52-v63 stacked hi
@@ -161,11 +162,22 @@
     "s_mov_b64 s[56:57], %[live]\n\t"                                                 \
     "s_mov_b64 %[hits], 0\n\t"                                                        \
     /* ---- node step: cur's record, per-lane child decisions ---- */                 \
-    ".LBIH_N_%=:\n\t"                                                                   \
+    ".LBIH_N_%=:\n\t"                       /* cur's record from memory (root, pops) */ \
     CNT_NODE                                                                          \
     "s_lshl_b32 s78, s74, 4\n\t"                                                      \
     "s_load_dwordx4 s[36:39], %[nodes], s78\n\t"                                      \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
+    "s_branch .LBIH_NB_%=\n\t"                                                        \
+    ".LBIH_NC_%=:\n\t"                      /* cur is a child of the last node: its */ \
+    CNT_NODE                                 /* record was prefetched with its sibling */ \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
+    "s_cmp_eq_u32 s74, s77\n\t"                                                       \
+    "s_cselect_b64 s[36:37], s[88:89], s[92:93]\n\t"                                  \
+    "s_cselect_b64 s[38:39], s[90:91], s[94:95]\n\t"                                  \
+    ".LBIH_NB_%=:\n\t"                                                                \
+    "s_and_b32 s77, s38, 0x7ffffff\n\t"    /* split; prefetch nodes split, split+1 */ \
+    "s_lshl_b32 s78, s77, 4\n\t"                                                      \
+    "s_load_dwordx8 s[88:95], %[nodes], s78\n\t"                                      \
     "s_bitcmp1_b32 s38, 27\n\t"              /* inv = {ix, iy, iz}[axis] */           \
     "s_cselect_b64 s[64:65], -1, 0\n\t"                                               \
     "v_cndmask_b32_e64 v24, %[ix], %[iy], s[64:65]\n\t"                               \
@@ -189,7 +201,6 @@
     "s_and_b64 s[58:59], s[58:59], s[56:57]\n\t"                                      \
     "s_xnor_b64 s[60:61], s[60:61], s[62:63]\n\t"         /* gR = !((t1 > sR) ^ neg) */ \
     "s_and_b64 s[60:61], s[60:61], s[56:57]\n\t"                                      \
-    "s_and_b32 s77, s38, 0x7ffffff\n\t"                                               \
     "s_lshr_b32 s78, s38, 29\n\t"            /* leaf bits */                          \
     "s_cbranch_scc1 .LBIH_L_%=\n\t"                                                     \
     /* ---- descend: take near (majority order) or the only child, stack other ---- */ \
@@ -214,7 +225,7 @@
     "v_cndmask_b32_e64 %[tmin], v31, v29, s[66:67]\n\t"                               \
     "v_cndmask_b32_e64 %[tmax], v32, v30, s[66:67]\n\t"                               \
     "s_cmp_eq_u64 s[64:65], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_N_%=\n\t"                                                     \
+    "s_cbranch_scc1 .LBIH_NC_%=\n\t"                                                    \
     "v_cndmask_b32_e64 v33, v29, v31, s[66:67]\n\t"                                   \
     "v_cndmask_b32_e64 v34, v30, v32, s[66:67]\n\t"                                   \
     "v_cndmask_b32_e64 v33, %[snan], v33, s[64:65]\n\t"                               \
@@ -229,7 +240,7 @@
     "s_nop 0\n\t"                                                                     \
     "v_writelane_b32 v39, s80, m0\n\t"                                               \
     "s_add_u32 s75, s75, 1\n\t"                                                       \
-    "s_branch .LBIH_N_%=\n\t"                                                           \
+    "s_branch .LBIH_NC_%=\n\t"                                                          \
     ".LBIH_SP_%=:\n\t"                         /* deep slot: wave spill area */         \
     "s_sub_u32 s78, s75, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                \
     "s_lshl_b32 s78, s78, 9\n\t"                                                      \
@@ -294,7 +305,7 @@
     "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", \
     "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
     "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", \
-    "s84", "s85",                                                                     \
+    "s84", "s85", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",             \
     "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
     "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", \

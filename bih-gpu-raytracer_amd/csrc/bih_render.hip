@@ -1426,7 +1426,9 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
-size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + (size_t)m * 16; }
+// + one record of padding: the packet walk prefetches the record pair
+// {split, split+1}, and split+1 may be one past the last internal node
+size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + (size_t)(m + 1) * 16; }
 
 int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
                 float *prim, void *stream) {
