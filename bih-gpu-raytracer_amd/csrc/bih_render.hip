@@ -1149,6 +1149,36 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
     }
 }
 
+// XCD-local tile queues: tiles are cut into kRegions bands of consecutive
+// tiles (row bands of the image); a wave drains its own XCD's band first, so
+// the nodes and triangles of one part of the image stay in that XCD's L2,
+// then helps the other bands.  Returns false when every band is drained.
+constexpr uint32_t kRegions = 8;
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & (kRegions - 1);
+}
+
+__device__ __forceinline__ bool next_tile(uint32_t *work, uint32_t ntiles, uint32_t lane,
+                                          uint32_t &region, uint32_t &left, uint32_t &tile) {
+    while (left) {
+        const uint32_t rb = (uint32_t)(((uint64_t)ntiles * region) / kRegions);
+        const uint32_t re = (uint32_t)(((uint64_t)ntiles * (region + 1)) / kRegions);
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(work + region, 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t < re - rb) {
+            tile = rb + t;
+            return true;
+        }
+        region = (region + 1) & (kRegions - 1);
+        --left;
+    }
+    return false;
+}
+
 // ---------------------------------------------------------------------------
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
 // loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
@@ -1174,11 +1204,8 @@ __global__ void __launch_bounds__(kThreads) k_render_packet_asm(const RenderArgs
     const uint32_t snan = 0x7f800001u;
     const uint32_t eps = __float_as_uint(kDetEps), fmax = __float_as_uint(FLT_MAX);
 
-    for (;;) {
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(a.work, 1u);
-        tile = __builtin_amdgcn_readfirstlane(tile);
-        if (tile >= ntiles) break;
+    uint32_t region = xcc_id(), left = kRegions, tile = 0;
+    while (next_tile(a.work, ntiles, lane, region, left, tile)) {
         uint32_t x, lr, s;
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
@@ -1503,7 +1530,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
 #if BIH_PACKET_COUNTERS
         hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
 #else
-        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), st);
+        hipError_t e = hipMemsetAsync(a.work, 0, kRegions * sizeof(uint32_t), st);
 #endif
         if (e != hipSuccess) return (int)e;
         switch (L) {
