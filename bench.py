@@ -64,7 +64,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import bihrt
-    from bihrt.tiling import band_rows, max_rows, rows_of_rank
+    from bihrt.tiling import band_rows, gather_order, max_rows
 
     W, H, SPP = args.width, args.height, args.spp
     # one explicit stream for build, render, events and the all-gather
@@ -85,14 +85,7 @@ def main():
     out = torch.zeros(mrows * W, dtype=torch.int32, device="cuda")
     gathered = torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") if world > 1 else None
     if world > 1:
-        perm = []
-        for rr in range(world):
-            ys = rows_of_rank(H, args.band, rr, world)
-            perm.append(torch.as_tensor(ys, dtype=torch.long))
-        order = torch.empty(H, dtype=torch.long)
-        for rr in range(world):
-            order[perm[rr]] = torch.arange(perm[rr].numel()) + rr * mrows
-        order = order.cuda()
+        order = torch.from_numpy(gather_order(H, args.band, world)).cuda()
         frame_img = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 

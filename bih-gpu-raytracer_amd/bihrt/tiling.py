@@ -36,3 +36,14 @@ def assemble(parts, h: int, band: int, world: int) -> np.ndarray:
         ys = rows_of_rank(h, band, r, world)
         out[ys] = parts[r][: ys.size]
     return out
+
+
+def gather_order(h: int, band: int, world: int) -> np.ndarray:
+    """Row index into the all-gathered [world * max_rows, W] buffer (rank r's
+    rows at r * max_rows) for every frame row y: frame = gathered[order]."""
+    mrows = max_rows(h, band, world)
+    order = np.empty(h, np.int64)
+    for r in range(world):
+        ys = rows_of_rank(h, band, r, world)
+        order[ys] = np.arange(ys.size) + r * mrows
+    return order

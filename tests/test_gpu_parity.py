@@ -175,3 +175,17 @@ def test_1m_1080p_properties(gpu, bihrt_mod, oracle_mod):
     # k of 4 samples hit -> floor((255k + 20(4-k))/4), B = 10(4-k) (CUDAKernels.cu:384-388, :420)
     assert set(vals.tolist()) <= {0x281414, 0x1e4e4e, 0x148989, 0x0ac4c4, 0x00ffff}, \
         [hex(x) for x in vals]
+
+
+@pytest.mark.parametrize("fname,scene,w,h,frame", [
+    ("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
+    ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
+    ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0)])
+def test_render_matches_golden_fixture(fname, scene, w, h, frame, gpu, bihrt_mod):
+    """The committed golden framebuffers (tests/golden/make_golden.py)."""
+    from conftest import GOLDEN
+    ref = np.load(os.path.join(GOLDEN, fname))
+    g = bihrt_mod.GPUArrayManager(SCENES[scene])
+    for trav in (bihrt_mod.TRAVERSE_ANYHIT, bihrt_mod.TRAVERSE_REFERENCE):
+        img = _device_render(bihrt_mod, g, w, h, 4, frame, trav)
+        assert np.array_equal(img, ref), (fname, trav)

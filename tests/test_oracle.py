@@ -1,0 +1,356 @@
+"""CPU tests of the oracle (test infrastructure) against known answers, the
+reference's own fixture (BIH1.txt) and public third-party data (rocRAND's
+XORWOW jump matrices).  No GPU; every case runs in seconds."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, edge_scenes
+
+F32 = np.float32
+
+
+# --- Morton (Renderer.cpp:114-145) -----------------------------------------
+
+def _expand_ref(v):
+    v = (v * 0x00010001) & 0xFF0000FF
+    v = (v * 0x00000101) & 0x0F00F00F
+    v = (v * 0x00000011) & 0xC30C30C3
+    v = (v * 0x00000005) & 0x49249249
+    return v & 0xFFFFFFFF
+
+
+def _morton_ref(x, y, z):
+    def q(c):
+        c = np.float32(c) * np.float32(1024.0)
+        c = np.float32(0.0) if not (c > 0) else c          # fmaxf(c, 0): NaN -> 0
+        return int(min(c, np.float32(1023.0)))
+    return (_expand_ref(q(x)) * 4 + _expand_ref(q(y)) * 2 + _expand_ref(q(z))) & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("p,code", [((0, 0, 0), 0), ((1, 1, 1), 0x3FFFFFFF),
+                                    ((0.5, 0, 0), 1 << 29), ((0, 0.5, 0), 1 << 28),
+                                    ((0, 0, 0.5), 1 << 27), ((2.0, -1.0, float("nan")), 0x24924924)])
+def test_morton_known_answers(oracle_mod, p, code):
+    assert oracle_mod.morton3d(*p) == code == _morton_ref(*p)
+
+
+def test_morton_random_matches_restatement(oracle_mod):
+    rng = np.random.default_rng(3)
+    for x, y, z in rng.uniform(-0.1, 1.1, size=(500, 3)).astype(F32):
+        assert oracle_mod.morton3d(x, y, z) == _morton_ref(x, y, z)
+
+
+# --- Moeller-Trumbore (CUDAKernels.cu:17-50) ---------------------------------
+
+TRI = np.array([0, 0, 0, 1, 0, 0, 0, 1, 0], F32)
+
+
+@pytest.mark.parametrize("o,d,hit,t", [
+    ((0.25, 0.25, 1.0), (0, 0, -1), True, 1.0),      # front face
+    ((0.25, 0.25, -1.0), (0, 0, 1), False, None),    # back face: det = -1 culled
+    ((0.9, 0.9, 1.0), (0, 0, -1), False, None),      # u + v > 1
+    ((0.0, 0.5, 1.0), (0, 0, -1), True, 1.0),        # u == 0 on the edge: kept
+    ((0.25, 0.25, -1.0), (0, 0, -1), True, -1.0),    # behind: MT reports t < 0, the
+                                                     # caller's t > 0 drops it (:212)
+    ((0.25, 0.25, 1.0), (1, 0, 0), False, None),     # parallel: det = 0
+])
+def test_mt_known_answers(oracle_mod, o, d, hit, t):
+    h, tt = oracle_mod.mt(TRI, o, d)
+    assert h == hit
+    if hit:
+        assert tt == t
+
+
+def test_mt_det_threshold(oracle_mod):
+    # det < 1e-6 (double compare) rejects; f32 det == largest f32 below 1e-6 rejects,
+    # the next f32 up passes (det <= 0x358637bd)
+    eps = np.frombuffer(np.uint32(0x358637bd).tobytes(), F32)[0]
+    nxt = np.nextafter(eps, F32(1))
+    assert float(eps) < 1e-6 < float(nxt)
+    for det, ok in ((eps, False), (nxt, True)):
+        tri = np.array([0, 0, 0, det, 0, 0, 0, 1, 0], F32)   # det = e1.x for D = -z
+        h, _ = oracle_mod.mt(tri, (det * F32(0.25), 0.25, 1.0), (0, 0, -1))
+        assert h == ok
+
+
+# --- Camera (Renderer.cpp:99, Camera.cu:5-9) ---------------------------------
+
+@pytest.mark.parametrize("w,h,hx", [(640, 480, 2.6666667), (1920, 1080, 3.5555556),
+                                    (256, 256, 2.0)])
+def test_camera_reference(oracle_mod, w, h, hx):
+    cam = oracle_mod.camera_reference(w, h)
+    assert cam[:3].tolist() == [2, 0, -2]
+    assert cam[3:6].tolist() == [0, -1, -1]
+    assert cam[6] == F32(hx) and cam[7] == 0 and cam[8] == 0
+    assert cam[9:12].tolist() == [0, 2, 0]
+
+
+# --- Tree structure: Karras + clip fit (CUDAKernels.cu:497-710) ---------------
+
+def _clz32(x):
+    return 32 - int(x).bit_length()
+
+
+def _check_tree(ot):
+    U, m = ot.U, ot.U - 1
+    assert m >= 1
+    # sorted codes, runs and first indices (Renderer.cpp:441-472)
+    assert np.all(np.diff(ot.morton.astype(np.int64)) >= 0)
+    assert np.all(np.diff(ot.unique_mc.astype(np.int64)) > 0)
+    assert ot.dup_cnt.sum() == ot.n
+    assert np.array_equal(ot.first_idx, np.concatenate([[0], np.cumsum(ot.dup_cnt)[:-1]]))
+    # stable sort: ties keep input order
+    for k in range(U):
+        idx = ot.tri_idx[ot.first_idx[k]:ot.first_idx[k] + ot.dup_cnt[k]]
+        assert np.all(np.diff(idx.astype(np.int64)) > 0)
+    # every internal node but the root has one parent; every leaf one parent
+    seen_int = np.zeros(m, int)
+    seen_leaf = np.zeros(U, int)
+    for i in range(m):
+        for c in range(2):
+            ch = ot.children[i, c]
+            if ot.is_leaf[i, c]:
+                seen_leaf[ch] += 1
+                assert ot.leaf_parent[ch] == i
+            else:
+                seen_int[ch] += 1
+                assert ot.parent[ch] == i
+        # children are {split, split+1}; axis from the split's codes
+        split = ot.children[i, 0]
+        assert ot.children[i, 1] == split + 1
+        x = int(ot.unique_mc[split]) ^ int(ot.unique_mc[split + 1])
+        assert ot.axis[i] == (_clz32(x) + 1) % 3
+    assert seen_int[0] == 0 and np.all(seen_int[1:] == 1)
+    assert np.all(seen_leaf == 1)
+    # in-order leaf walk = 0..U-1; clip planes = tight bounds of each side
+    def leaves_of(i, leaf):
+        if leaf:
+            return [i]
+        return leaves_of(ot.children[i, 0], ot.is_leaf[i, 0]) + \
+            leaves_of(ot.children[i, 1], ot.is_leaf[i, 1])
+    assert leaves_of(0, False) == list(range(U))
+
+    def tris_of(leaves):
+        out = []
+        for k in leaves:
+            out.extend(ot.tri_idx[ot.first_idx[k]:ot.first_idx[k] + ot.dup_cnt[k]])
+        return np.asarray(out)
+    for i in range(m):
+        ax = ot.axis[i]
+        L = tris_of(leaves_of(ot.children[i, 0], ot.is_leaf[i, 0]))
+        R = tris_of(leaves_of(ot.children[i, 1], ot.is_leaf[i, 1]))
+        assert ot.clip[i, 0] == ot.hi[L, ax].max(), i
+        assert ot.clip[i, 1] == ot.lo[R, ax].min(), i
+
+
+@pytest.mark.parametrize("name", ["cornell", "dodeca", "clustered", "two_tris", "signed_zero"])
+def test_tree_invariants(oracle_mod, name):
+    ot = oracle_mod.OracleTree(edge_scenes()[name])
+    if ot.U > 1:
+        _check_tree(ot)
+
+
+def test_tree_invariants_soup(oracle_mod, bihrt_mod):
+    _check_tree(oracle_mod.OracleTree(bihrt_mod.scenes.soup(400, seed=12)))
+
+
+def test_karras_split_on_known_codes(oracle_mod):
+    """Three triangles whose centroids normalise to codes 0, 1<<27, 1<<29:
+    the root splits between leaves 1 and 2 (highest differing bit), the
+    second node between 0 and 1."""
+    c = [(0.0, 0.0, 0.0), (0.0, 0.0, 0.5), (0.5, 0.0, 0.0), (1.0, 1.0, 1.0)]
+    tris = []
+    for x, y, z in c:
+        tris.append([x, y, z, x, y, z, x, y, z])   # degenerate: centroid == vertex
+    ot = oracle_mod.OracleTree(np.asarray(tris, F32))
+    assert ot.U == 4
+    _check_tree(ot)
+    codes = [_morton_ref(*p) for p in c]
+    assert ot.unique_mc.tolist() == sorted(codes)
+
+
+# --- The reference's fixture: BIH1.txt (tree dump of a 36-tri dodecahedron) ---
+
+def _parse_dump(path):
+    nodes = []
+    cur = None
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("NODE"):
+            cur = {"id": int(line.split()[1])}
+            nodes.append(cur)
+        elif ":" in line and cur is not None:
+            k, v = [s.strip() for s in line.split(":", 1)]
+            cur[k] = v
+    return nodes
+
+
+def test_bih1_fixture_invariants():
+    nodes = _parse_dump(os.path.join(GOLDEN, "reference_BIH1.txt"))
+    assert len(nodes) == 35 and [n["id"] for n in nodes] == list(range(35))
+    coord = {0.0, 0.356822, 0.57735, 0.934172}
+    leaves = []
+    parents = {}
+    for n in nodes:
+        for side, key in (("leftChild", "isLeftLeaf"), ("rightChild", "isRightLeaf")):
+            ch = int(n[side])
+            if n[key] == "TRUE":
+                leaves.append(ch)
+            else:
+                assert ch not in parents
+                parents[ch] = n["id"]
+                assert int(nodes[ch]["parent"]) == n["id"]
+        assert int(n["rightChild"]) == int(n["leftChild"]) + 1
+        assert int(n["axis"]) in (0, 1, 2)
+        for k in ("clipPlaneLEFT", "clipPlaneRIGHT"):
+            assert abs(float(n[k])) in coord, n
+    assert sorted(leaves) == list(range(36))
+    assert set(parents) == set(range(1, 35)) and int(nodes[0]["parent"]) == -1
+
+
+def test_dodecahedron_tree_has_fixture_shape(oracle_mod):
+    """Our dodecahedron (the mesh itself is not in the reference) builds a
+    tree of the dump's shape: 35 nodes, 36 leaves, every clip plane a
+    dodecahedron coordinate."""
+    ot = oracle_mod.OracleTree(edge_scenes()["dodeca"])
+    assert ot.U == 36 and ot.clip.shape == (35, 2)
+    vals = np.unique(np.round(np.abs(ot.clip.astype(np.float64)), 6))
+    assert set(vals.tolist()) <= {0.0, 0.356822, 0.57735, 0.934172}
+
+
+# --- XORWOW (curand_init / curand_uniform, CUDAKernels.cu:411-419,458) --------
+
+ROCRAND_PRE = "/opt/rocm/include/rocrand/rocrand_xorwow_precomputed.h"
+
+
+def _rocrand_matrix(name, idx):
+    src = open(ROCRAND_PRE).read()
+    start = src.index(f"{name}[XORWOW_JUMP_MATRICES][XORWOW_SIZE] = {{")
+    body = src[start:]
+    blocks = re.findall(r"\{([^{}]*)\}", body[body.index("{") + 1:], flags=re.S)
+    return np.array([int(x) for x in blocks[idx].replace("\n", " ").split(",") if x.strip()],
+                    np.uint64).astype(np.uint32)
+
+
+def _mat_vec(m, v):
+    # rocrand_xorwow.h mul_mat_vec_inplace: m[i*32*5 + j*5 + k] is the image of bit j of word i
+    r = np.zeros(5, np.uint32)
+    for i in range(5):
+        for j in range(32):
+            if (int(v[i]) >> j) & 1:
+                r ^= m[(i * 32 + j) * 5:(i * 32 + j) * 5 + 5]
+    return r
+
+
+def _next(v, d):
+    v = [int(x) for x in v]
+    t = v[0] ^ (v[0] >> 2)
+    v = v[1:] + [((v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1))) & 0xFFFFFFFF]
+    d = (d + 362437) & 0xFFFFFFFF
+    return np.array(v, np.uint32), d, (d + v[4]) & 0xFFFFFFFF
+
+
+@pytest.mark.skipif(not os.path.exists(ROCRAND_PRE), reason="rocRAND headers absent")
+@pytest.mark.parametrize("subseq", [1, 2, 5, 37])
+def test_xorwow_subsequence_jump_pinned_by_rocrand(oracle_mod, subseq):
+    """Subsequence k = k * 2^67 steps: the oracle's jump equals rocRAND's
+    published sequence-jump matrices (h_xorwow_sequence_jump_matrices)."""
+    v0, d0 = oracle_mod.rng_state(1984, 0)
+    vk, dk = oracle_mod.rng_state(1984, subseq)
+    v = v0.copy()
+    k, mi = subseq, 0
+    while k:
+        for _ in range(k & 3):
+            v = _mat_vec(_rocrand_matrix("h_xorwow_sequence_jump_matrices", mi), v)
+        k >>= 2
+        mi += 1
+    assert np.array_equal(v, vk)
+    assert d0[0] == dk[0]          # 2^67 steps leave the 32-bit Weyl counter unchanged
+
+
+@pytest.mark.skipif(not os.path.exists(ROCRAND_PRE), reason="rocRAND headers absent")
+def test_xorwow_skip_pinned_by_rocrand(oracle_mod):
+    """skip-ahead by 4 steps == rocRAND h_xorwow_jump_matrices[1]; next() ==
+    the published recurrence."""
+    v0, d0 = oracle_mod.rng_state(1984, 3)
+    v4, _ = oracle_mod.rng_state(1984, 3, skip=4)
+    assert np.array_equal(_mat_vec(_rocrand_matrix("h_xorwow_jump_matrices", 1), v0), v4)
+    u = oracle_mod.rng_uniforms(1984, 3, 6)
+    v, d = v0.copy(), int(d0[0])
+    for k in range(6):
+        v, d, x = _next(v, d)
+        # curand_uniform: x * 2^-32 + 2^-33 (f32)
+        assert u[k] == F32(x) * F32(2.0 ** -32) + F32(2.0 ** -33)
+
+
+def test_xorwow_seed_constants(oracle_mod):
+    """curand_init seeding as restated (cuRAND is not vendored: these
+    constants are unpinned by any fixture)."""
+    v, d = oracle_mod.rng_state(1984, 0)
+    s0 = (1984 ^ 0xaad26b49) & 0xFFFFFFFF
+    s1 = (0 ^ 0xf7dcefdd) & 0xFFFFFFFF
+    t0 = (1099087573 * s0) & 0xFFFFFFFF
+    t1 = (2591861531 * s1) & 0xFFFFFFFF
+    want = [(123456789 + t0) & 0xFFFFFFFF, 362436069 ^ t0, (521288629 + t1) & 0xFFFFFFFF,
+            88675123 ^ t1, (5783321 + t0) & 0xFFFFFFFF]
+    assert v.tolist() == want
+    assert int(d[0]) == (6615241 + t1 + t0) & 0xFFFFFFFF
+
+
+# --- Traversal -----------------------------------------------------------------
+
+def test_traversal_modes_agree_with_brute_force(oracle_mod, bihrt_mod):
+    """BIH walk (reference rules) vs brute force over all triangles
+    (TraverseTriangles, CUDAKernels.cu:157-202) on random rays; the any-hit
+    walk returns the reference walk's hit flag exactly, with no more work."""
+    tris = bihrt_mod.scenes.soup(3000, seed=21)
+    ot = oracle_mod.OracleTree(tris)
+    rng = np.random.default_rng(5)
+    n = 4000
+    orig = np.tile(np.array([2, 0, -2], F32), (n, 1))
+    # aim at triangle centroids (about half are front-facing) and at random points
+    cen = tris.reshape(-1, 3, 3).mean(1)[rng.integers(0, tris.shape[0], n // 2)]
+    tgt = np.concatenate([cen, rng.uniform([0, -1, 0], [2.667, 1, 2], size=(n - n // 2, 3))])
+    tgt = tgt.astype(F32)
+    dirs = (tgt - orig).astype(F32)
+    h_ref, n_ref, t_ref = ot.trace(orig, dirs, oracle_mod.MODE_GPU_REF)
+    h_any, n_any, t_any = ot.trace(orig, dirs, oracle_mod.MODE_GPU_ANYHIT)
+    h_bf, _, _ = ot.trace(orig, dirs, oracle_mod.MODE_BRUTE)
+    assert np.array_equal(h_ref, h_any)
+    assert np.all(n_any <= n_ref) and np.all(t_any <= t_ref)
+    assert h_ref.sum() > n // 5
+    # the BIH walk is conservative up to f32 plane rounding
+    assert np.mean(h_ref != h_bf) < 1e-3
+
+
+def test_pixels_take_the_five_binary_shades(oracle_mod):
+    """k of 4 samples hit -> R=G=floor((255k + 20(4-k))/4), B=10(4-k)
+    (Color + rgbToInt, CUDAKernels.cu:370-389,74-88)."""
+    ot = oracle_mod.OracleTree(edge_scenes()["dodeca"])
+    img, _ = ot.render(64, 48, spp=4)
+    allowed = set()
+    for k in range(5):
+        rg = (255 * k + 20 * (4 - k)) // 4
+        allowed.add((10 * (4 - k)) << 16 | rg << 8 | rg)
+    assert set(np.unique(img).tolist()) <= allowed
+    assert len(np.unique(img)) >= 2
+
+
+# --- Golden framebuffers (generated by tests/golden/make_golden.py) ------------
+
+GOLDEN_CASES = [("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
+                ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
+                ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0)]
+
+
+@pytest.mark.parametrize("fname,scene,w,h,frame", GOLDEN_CASES)
+def test_oracle_reproduces_golden(oracle_mod, fname, scene, w, h, frame):
+    ref = np.load(os.path.join(GOLDEN, fname))
+    img, _ = oracle_mod.OracleTree(edge_scenes()[scene]).render(w, h, frame=frame)
+    assert np.array_equal(img, ref)
+    img2, _ = oracle_mod.OracleTree(edge_scenes()[scene]).render(
+        w, h, frame=frame, mode=oracle_mod.MODE_GPU_ANYHIT)
+    assert np.array_equal(img2, ref)
