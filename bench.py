@@ -43,8 +43,14 @@ def parse():
     ap.add_argument("--band", type=int, default=8)
     ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on rank 0 (N=1)")
-    ap.add_argument("--cpu-row-step", type=int, default=8)
+    ap.add_argument("--cpu-row-step", type=int, default=1,
+                    help="rows of frame 0 timed on all host threads (every k-th row)")
+    ap.add_argument("--cpu-serial-row-step", type=int, default=8,
+                    help="rows timed single-threaded (the reference's serial host loop)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--traffic", type=int, default=1,
+                    help="N=1: measure HBM traffic per launch with rocprofv3 PMC passes "
+                         "(child processes, before this process touches the GPU)")
     ap.add_argument("--no-reference-leg", action="store_true")
     return ap.parse_args()
 
@@ -56,6 +62,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     import numpy as np
     import torch
+
+    # PMC traffic passes run as child processes before this one initialises
+    # the GPU (rocprofv3 must start the program itself)
+    traffic = None
+    if world == 1 and args.traffic:
+        traffic = measure_traffic(args)
 
     torch.cuda.set_device(local)
     dist = None
@@ -184,12 +196,14 @@ def main():
             "build_ms": info.build_ms,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "bytes_per_ray": b_ray,
                 "counters_per_ray": {"nodes": n_node / rays_all, "leaves": n_leaf / rays_all,
                                      "tris": n_tri / rays_all},
-                "kernel": f"k_render<{'anyhit' if trav == 0 else 'reference'}>",
+                "kernel": f"k_render_packet_asm ({'any-hit' if trav == 0 else 'reference'} walk)",
             },
+            "traffic_detail": traffic,
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
         }
@@ -201,31 +215,97 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
-    """The oracle (strict-IEEE C restatement, OpenMP) on a bounded row sample
-    of the same frame; also checks those rows of the GPU frame bit-exactly."""
+    """The oracle (strict-IEEE C restatement of the reference's render path)
+    timed on the host: (i) OpenMP over the box's CPU share on every
+    --cpu-row-step-th row of frame 0 (the reported value), (ii) one thread on
+    every --cpu-serial-row-step-th row (the reference's serial host loop,
+    Renderer.cpp:374-412).  Also checks those rows of the GPU frame
+    bit-exactly."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
         min(16, os.cpu_count() or 1)
     ot = oracle.OracleTree(tris)
+    mode = oracle.MODE_GPU_ANYHIT if trav == 0 else oracle.MODE_GPU_REF
+    walk = "any-hit" if trav == 0 else "reference"
     step = args.cpu_row_step
     nrows = math.ceil(H / step)
-    mode = oracle.MODE_GPU_ANYHIT if trav == 0 else oracle.MODE_GPU_REF
     img, st = ot.render(W, H, spp=SPP, frame=0, rows=(0, nrows, step), mode=mode, threads=threads)
+    s1 = args.cpu_serial_row_step
+    n1 = math.ceil(H / s1)
+    img1, st1 = ot.render(W, H, spp=SPP, frame=0, rows=(0, n1, s1), mode=mode, threads=1)
     # GPU frame 0, untimed, same rows
     full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     r.render_device(full.data_ptr(), 0, traverse=trav, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     g = full.cpu().numpy().view(np.uint32).reshape(H, W)
-    same = bool(np.array_equal(g[0:H:step], img))
+    same = bool(np.array_equal(g[0:H:step], img) and np.array_equal(g[0:H:s1], img1))
     res = {"value": st.rays / st.render_seconds, "unit": "rays/s", "cores": st.threads,
            "kind": "port",
            "sample": f"every {step}th row of frame 0 ({nrows} rows x {W} px x {SPP} spp = "
-                     f"{st.rays} rays), oracle/bih_oracle.c "
-                     f"{'any-hit' if trav == 0 else 'reference'} traversal, OpenMP",
-           "seconds": st.render_seconds}
+                     f"{st.rays} rays), oracle/bih_oracle.c {walk} traversal, OpenMP "
+                     f"{st.threads} threads",
+           "seconds": st.render_seconds,
+           "cpu_model": cpu_model(),
+           "serial": {"value": st1.rays / st1.render_seconds, "unit": "rays/s", "cores": 1,
+                      "sample": f"every {s1}th row of frame 0 ({st1.rays} rays), 1 thread",
+                      "seconds": st1.render_seconds}}
     return res, same
+
+
+def measure_traffic(args):
+    """FETCH_SIZE and WRITE_SIZE (KB, rocprofv3, one counter per pass) of the
+    render kernel over tools/prof_render.py on this workload; gfx950
+    correction: FETCH_SIZE x 2 (MI355X_MICROARCH.md, HBM section).  These are
+    L2-to-fabric bytes: Infinity Cache hits are included."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    res = {}
+    tmp = tempfile.mkdtemp(prefix="bih_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    traverse = args.traverse
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = os.path.join(tmp, ctr)
+        cmd = [prof, "--pmc", ctr, "-d", out, "-o", ctr, "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "tools", "prof_render.py"), "--frames", "3",
+               "--tris", str(args.tris), "--width", str(args.width), "--height", str(args.height),
+               "--spp", str(args.spp), "--traverse", traverse]
+        try:
+            p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=300)
+        except (OSError, subprocess.TimeoutExpired):
+            return None
+        if p.returncode != 0:
+            return None
+        vals = []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if "k_render" in row["Kernel_Name"]:
+                    vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None
+        res[ctr] = sum(vals) / len(vals)
+    shutil.rmtree(tmp, ignore_errors=True)
+    fetch = 2.0 * res["FETCH_SIZE"] * 1024.0
+    write = res["WRITE_SIZE"] * 1024.0
+    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024"}
 
 
 if __name__ == "__main__":

@@ -145,8 +145,9 @@ int bih_render_rows(const bih_scene *scene, const bih_tree *tree, const bih_came
 /* Device-resident render (bench / multi-GPU): writes nrows*w pixels to d_out
  * (device memory on the tree's device) in local row order, on `stream`
  * (NULL = the tree's stream), asynchronously; bih_sync waits for it.
- * traverse = BIH_TRAVERSE_*.  d_ray_stats (optional, device u32[2*rays]) gets
- * per-ray {node visits, triangle tests} for parity checks against the oracle. */
+ * traverse = BIH_TRAVERSE_*.  d_ray_stats (optional, device u32[3*rays], ray =
+ * (local pixel)*spp + sample) gets per-ray {node visits, leaf visits, triangle
+ * tests} for parity checks against the oracle. */
 int bih_render_device(const bih_tree *tree, const bih_camera *camera, uint32_t w, uint32_t h,
                       uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows,
                       uint32_t traverse, uint32_t *d_out, uint32_t *d_ray_stats, void *stream);
