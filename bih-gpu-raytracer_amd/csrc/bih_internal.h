@@ -35,9 +35,9 @@ constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bi
 // stack entries per lane held in LDS (12 B each); deeper ones spill to HBM.
 // 1M-tri soup @1080p: 0.8 % of pushes land in slot >= 10 (12 % at >= 8).
 constexpr int kLdsStack = BIH_LDS_STACK;
-// work buffer: [0..8) tile counters (one per image band / XCD); [16..56) walk
-// counters of BIH_PACKET_COUNTERS builds
-constexpr uint32_t kWorkWords = 64;
+// work buffer: [0..8) chunk counters (one per image band / XCD); [16..56) walk
+// counters of BIH_PACKET_COUNTERS builds; [64..2112) per-CU tile slots (u64)
+constexpr uint32_t kWorkWords = 64 + 2 * 1024;
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif

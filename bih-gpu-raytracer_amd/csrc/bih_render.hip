@@ -1149,11 +1149,22 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
     }
 }
 
-// XCD-local tile queues: tiles are cut into kRegions bands of consecutive
-// tiles (row bands of the image); a wave drains its own XCD's band first, so
-// the nodes and triangles of one part of the image stay in that XCD's L2,
-// then helps the other bands.  Returns false when every band is drained.
+// Tile scheduling of the persistent packet kernel, two levels:
+//  * the image is cut into chunks of kChunkW x kChunkH tiles (a compact
+//    block of pixels) and the chunks into kRegions bands of chunk rows, one
+//    per XCD: an XCD drains its own band first (its L2 keeps that part of
+//    the tree), then helps the others;
+//  * all waves on one CU share one current chunk (per-CU slot, keyed by the
+//    hardware CU id), so the ~28 packets in flight on a CU trace neighbouring
+//    pixels and share the scalar cache's node and triangle lines.
+// A slot is one 64-bit word {chunk + 1, next position}: a wave claims
+// position p of the slot's chunk with one atomicAdd; the wave that draws
+// p == chunk size (or the first one on an empty slot) refills it from the
+// band counters; waves that overdraw wait (s_sleep) for the refill.
 constexpr uint32_t kRegions = 8;
+constexpr uint32_t kChunkW = 8, kChunkH = 4, kChunk = kChunkW * kChunkH;
+constexpr uint32_t kSlotWord = 64;                     // work[64..64+2*1024): CU slots
+constexpr unsigned long long kSlotDone = 0xFFFFFFFF00000000ull;
 
 __device__ __forceinline__ uint32_t xcc_id() {
     uint32_t x;
@@ -1161,22 +1172,78 @@ __device__ __forceinline__ uint32_t xcc_id() {
     return x & (kRegions - 1);
 }
 
-__device__ __forceinline__ bool next_tile(uint32_t *work, uint32_t ntiles, uint32_t lane,
-                                          uint32_t &region, uint32_t &left, uint32_t &tile) {
-    while (left) {
-        const uint32_t rb = (uint32_t)(((uint64_t)ntiles * region) / kRegions);
-        const uint32_t re = (uint32_t)(((uint64_t)ntiles * (region + 1)) / kRegions);
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(work + region, 1u);
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (t < re - rb) {
-            tile = rb + t;
-            return true;
-        }
-        region = (region + 1) & (kRegions - 1);
-        --left;
+// (XCC, SE, SH, CU) -> 0..1023, unique per CU (tools/probe/hwid_probe.hip)
+__device__ __forceinline__ uint32_t cu_key() {
+    uint32_t h;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+    return (xcc_id() << 7) | (((h >> 13) & 3u) << 5) | (((h >> 12) & 1u) << 4) | ((h >> 8) & 15u);
+}
+
+struct TileQueue {
+    uint32_t *work;
+    unsigned long long *slot;
+    uint32_t tiles_x, tiles_y, chunks_x, nchunks;
+    uint32_t band, left;
+
+    __device__ uint32_t band_begin(uint32_t b) const {
+        const uint32_t rows = (nchunks / chunks_x);
+        return (uint32_t)(((uint64_t)rows * b) / kRegions) * chunks_x;
     }
-    return false;
+
+    // Next tile (global tile index t = ty * tiles_x + tx) for this wave.
+    __device__ bool next(uint32_t lane, uint32_t &tile) {
+        for (;;) {
+            unsigned long long v = 0;
+            if (lane == 0) v = atomicAdd(slot, 1ull);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+            if (hi == 0xFFFFFFFFu) return false;
+            if (hi != 0 && lo < kChunk) {
+                const uint32_t g = hi - 1;
+                const uint32_t tx = (g % chunks_x) * kChunkW + lo % kChunkW;
+                const uint32_t ty = (g / chunks_x) * kChunkH + lo / kChunkW;
+                if (tx < tiles_x && ty < tiles_y) {
+                    tile = ty * tiles_x + tx;
+                    return true;
+                }
+                continue;                                // edge chunk: position off the image
+            }
+            if ((hi == 0 && lo == 0) || (hi != 0 && lo == kChunk)) {
+                // this wave refills the slot with the next chunk of its band
+                while (left) {
+                    uint32_t c = 0;
+                    if (lane == 0) c = atomicAdd(work + band, 1u);
+                    c = __builtin_amdgcn_readfirstlane(c);
+                    const uint32_t b0 = band_begin(band), b1 = band_begin(band + 1);
+                    if (c < b1 - b0) {
+                        const uint32_t g = b0 + c;
+                        if (lane == 0) atomicExch(slot, ((unsigned long long)(g + 1) << 32) | 1ull);
+                        tile = (g / chunks_x) * kChunkH * tiles_x + (g % chunks_x) * kChunkW;
+                        return true;                     // position 0: always on the image
+                    }
+                    band = (band + 1) & (kRegions - 1);
+                    --left;
+                }
+                if (lane == 0) atomicExch(slot, kSlotDone);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(4);                 // another wave is refilling
+        }
+    }
+};
+
+__device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t tiles_x,
+                                                uint32_t tiles_y) {
+    TileQueue q;
+    q.work = a.work;
+    q.slot = reinterpret_cast<unsigned long long *>(a.work + kSlotWord) + cu_key();
+    q.tiles_x = tiles_x;
+    q.tiles_y = tiles_y;
+    q.chunks_x = (tiles_x + kChunkW - 1) / kChunkW;
+    q.nchunks = q.chunks_x * ((tiles_y + kChunkH - 1) / kChunkH);
+    q.band = xcc_id();
+    q.left = kRegions;
+    return q;
 }
 
 // ---------------------------------------------------------------------------
@@ -1204,8 +1271,10 @@ __global__ void __launch_bounds__(kThreads) k_render_packet_asm(const RenderArgs
     const uint32_t snan = 0x7f800001u;
     const uint32_t eps = __float_as_uint(kDetEps), fmax = __float_as_uint(FLT_MAX);
 
-    uint32_t region = xcc_id(), left = kRegions, tile = 0;
-    while (next_tile(a.work, ntiles, lane, region, left, tile)) {
+    TileQueue queue = make_queue(a, tiles_x, (a.nrows + TH - 1) / TH);
+    uint32_t tile = 0;
+    (void)ntiles;
+    while (queue.next(lane, tile)) {
         uint32_t x, lr, s;
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
@@ -1530,7 +1599,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
 #if BIH_PACKET_COUNTERS
         hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
 #else
-        hipError_t e = hipMemsetAsync(a.work, 0, kRegions * sizeof(uint32_t), st);
+        hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
 #endif
         if (e != hipSuccess) return (int)e;
         switch (L) {
