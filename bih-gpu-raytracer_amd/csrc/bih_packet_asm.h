@@ -247,14 +247,12 @@
     "s_cbranch_scc1 .LBIH_L_%=\n\t"                                                   \
     /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
     ".LBIH_D_%=:\n\t"                                                                 \
-    "s_or_b64 s[60:61], s[54:55], s[56:57]\n\t"                                       \
-    "s_cbranch_scc0 .LBIH_P_%=\n\t"                                                   \
-    "s_bitcmp1_b32 %[near], s72\n\t"                                                  \
-    "s_cbranch_scc0 .LBIH_DR_%=\n\t"                                                  \
-    "s_cmp_eq_u64 s[54:55], 0\n\t"           /* near = left */                        \
-    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
-    "s_cmp_eq_u64 s[56:57], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
+    "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
+    "s_cbranch_scc0 .LBIH_DN_%=\n\t"                                                  \
+    "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
+    "s_cbranch_scc0 .LBIH_TL_%=\n\t"         /* only the left child */                \
+    "s_bitcmp1_b32 %[near], s72\n\t"        /* both: near first, stack the other */  \
+    "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
     BIH_PUSH("r", "s[56:57]", "v31", "v32", "1")                                      \
     ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
     "s_mov_b64 s[52:53], s[54:55]\n\t"                                                \
@@ -262,11 +260,7 @@
     "v_mov_b32_e32 %[tmax], v30\n\t"                                                  \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     "s_branch .LBIH_NB0_%=\n\t"                                                       \
-    ".LBIH_DR_%=:\n\t"                       /* near = right */                       \
-    "s_cmp_eq_u64 s[56:57], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
-    "s_cmp_eq_u64 s[54:55], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
+    ".LBIH_BR_%=:\n\t"                                                                \
     BIH_PUSH("l", "s[54:55]", "v29", "v30", "0")                                      \
     ".LBIH_TR_%=:\n\t"                       /* take right: record in s[88:91] */     \
     "s_mov_b64 s[52:53], s[56:57]\n\t"                                                \
@@ -274,6 +268,9 @@
     "v_mov_b32_e32 %[tmax], v32\n\t"                                                  \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     "s_branch .LBIH_NB1_%=\n\t"                                                       \
+    ".LBIH_DN_%=:\n\t"                       /* no left: right or pop */              \
+    "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
+    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
     /* ---- pop until an entry has a searching lane ---- */                           \
     ".LBIH_P_%=:\n\t"                                                                 \
     "s_waitcnt lgkmcnt(0)\n\t"               /* the pair prefetch lands in s[84:91] */ \
@@ -304,25 +301,36 @@
     "s_branch .LBIH_PQ_%=\n\t"                                                        \
     /* ---- leaves of this node: test them (near first), then descend ---- */         \
     ".LBIH_L_%=:\n\t"                                                                 \
-    "s_bitcmp1_b32 s81, 0\n\t"                                                        \
-    "s_cselect_b64 s[64:65], s[54:55], 0\n\t"                                         \
-    "s_cselect_b64 s[54:55], 0, s[54:55]\n\t"                                         \
-    "s_bitcmp1_b32 s81, 1\n\t"                                                        \
-    "s_cselect_b64 s[66:67], s[56:57], 0\n\t"                                         \
-    "s_cselect_b64 s[56:57], 0, s[56:57]\n\t"                                         \
     "s_and_b32 s82, s80, 0x7ffffff\n\t"      /* mid */                                \
+    "s_cmp_eq_u32 s81, 1\n\t"                                                         \
+    "s_cbranch_scc1 .LBIH_L1_%=\n\t"                                                  \
+    "s_cmp_eq_u32 s81, 2\n\t"                                                         \
+    "s_cbranch_scc1 .LBIH_L2_%=\n\t"                                                  \
+    "s_mov_b64 s[64:65], s[54:55]\n\t"       /* both children are leaves */           \
+    "s_mov_b64 s[66:67], s[56:57]\n\t"                                                \
     "s_bitcmp1_b32 %[near], s72\n\t"                                                  \
     "s_cbranch_scc0 .LBIH_LR_%=\n\t"                                                  \
     BIH_LEAF_L("a", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     BIH_LEAF_R("a", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \
-    "s_branch .LBIH_LE_%=\n\t"                                                        \
+    "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_LR_%=:\n\t"                                                                \
     BIH_LEAF_R("b", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \
     BIH_LEAF_L("b", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
-    ".LBIH_LE_%=:\n\t"                                                                \
-    CLR("s[54:55]")                                                                   \
+    "s_branch .LBIH_P_%=\n\t"                                                         \
+    ".LBIH_L1_%=:\n\t"                       /* left leaf, right internal */          \
+    "s_mov_b64 s[64:65], s[54:55]\n\t"                                                \
+    BIH_LEAF_L("c", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     CLR("s[56:57]")                                                                   \
-    "s_branch .LBIH_D_%=\n\t"                                                         \
+    "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
+    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
+    "s_branch .LBIH_P_%=\n\t"                                                         \
+    ".LBIH_L2_%=:\n\t"                       /* right leaf, left internal */          \
+    "s_mov_b64 s[66:67], s[56:57]\n\t"                                                \
+    BIH_LEAF_R("d", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \
+    CLR("s[54:55]")                                                                   \
+    "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
+    "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
+    "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_X_%=:\n\t"                                                                 \
     "s_mov_b32 m0, s79"
 

@@ -1251,8 +1251,13 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
 // loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
 // offsets are 32-bit in the loop: used for scenes of < 2^26 triangles.
 // ---------------------------------------------------------------------------
+#ifndef BIH_ASM_WAVES_PER_EU
+#define BIH_ASM_WAVES_PER_EU 7
+#endif
 template <bool ANYHIT, bool STATS, int LOG2SPP>
-__global__ void __launch_bounds__(kThreads) k_render_packet_asm(const RenderArgs a) {
+__global__ void __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(BIH_ASM_WAVES_PER_EU, BIH_ASM_WAVES_PER_EU)))
+k_render_packet_asm(const RenderArgs a) {
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
