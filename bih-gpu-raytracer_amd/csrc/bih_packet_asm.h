@@ -29,13 +29,14 @@
 //   s[84:91] record pair (prefetch)
 //   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of left/right
 //   v33-v38 temps (MT: v35-v37 p, v38 det then 1/det)  v39 stacked node ids
-//   (lane k = slot k)  v40-v51 stacked lo (slot = gpr index)  v52-v63 stacked hi
+//   (lane k = slot k)  v40-v50 stacked lo (slot = gpr index)  v51-v61 stacked hi
+//   (11 slots: 64 VGPRs in all, 8 waves per SIMD)
 // Slots >= BIH_ASM_SLOTS go to the wave's HBM spill area, [slot - BIH_ASM_SLOTS]
 // x {lo[64], hi[64]} f32.  Lanes outside a stacked entry's mask hold the
 // signalling-NaN pattern 0x7f800001 in lo (no f32 operation produces it).
 #pragma once
 
-#define BIH_ASM_SLOTS 12
+#define BIH_ASM_SLOTS 11
 #define BIH_S2(x) #x
 #define BIH_S(x) BIH_S2(x)
 
@@ -190,7 +191,7 @@
     "s_cbranch_scc1 .LBIH_SP" TAG "_%=\n\t"                                           \
     "s_set_gpr_idx_on s71, gpr_idx(DST)\n\t"                                          \
     "v_mov_b32_e32 v40, v33\n\t"                                                      \
-    "v_mov_b32_e32 v52, " HI "\n\t"                                                   \
+    "v_mov_b32_e32 v51, " HI "\n\t"                                                   \
     "s_set_gpr_idx_off\n\t"                                                           \
     ".LBIH_PN" TAG "_%=:\n\t"                                                         \
     "s_add_u32 s74, s73, " NODE_OFS "\n\t"                                            \
@@ -282,7 +283,7 @@
     "s_cbranch_scc1 .LBIH_SQ_%=\n\t"                                                  \
     "s_set_gpr_idx_on s71, gpr_idx(SRC0)\n\t"                                         \
     "v_mov_b32_e32 %[tmin], v40\n\t"                                                  \
-    "v_mov_b32_e32 %[tmax], v52\n\t"                                                  \
+    "v_mov_b32_e32 %[tmax], v51\n\t"                                                  \
     "s_set_gpr_idx_off\n\t"                                                           \
     ".LBIH_PQ_%=:\n\t"                                                                \
     "s_nop 0\n\t"                                                                     \
@@ -343,4 +344,4 @@
     "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
     "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", \
-    "v60", "v61", "v62", "v63", "vcc", "scc", "memory"
+    "v60", "v61", "vcc", "scc", "memory"

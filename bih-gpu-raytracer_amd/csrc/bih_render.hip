@@ -1573,6 +1573,11 @@ uint32_t wave_grid_blocks(int device) {
         }
         if (cus <= 0) cus = 256;
         if (per <= 0) per = 1;
+        // tuning knob: resident blocks per CU (the occupancy API's answer otherwise)
+        if (const char *e = getenv("BIH_BLOCKS_PER_CU")) {
+            const int v = atoi(e);
+            if (v > 0 && v <= 32) per = v;
+        }
         cache[device] = (uint32_t)(cus * per);
     }
     return cache[device];
