@@ -27,7 +27,8 @@
 //   s[68:69] tmp      s70 cur (pop)  s71 sp  s72 axis  s73 split  s74-s76 tmp
 //   s77 b  s78 e  s79 saved m0  s80 w (mid | counts)  s81 leaf bits  s82 mid
 //   s[84:91] record pair (prefetch)
-//   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of left/right
+//   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of a stacked child
+//   (MT: v24, v27-v30 division temps; t0/t1 survive the leaf tests)
 //   v33-v38 temps (MT: v35-v37 p, v38 det then 1/det)  v39 stacked node ids
 //   (lane k = slot k)  v40-v50 stacked lo (slot = gpr index)  v51-v61 stacked hi
 //   (11 slots: 64 VGPRs in all, 8 waves per SIMD)
@@ -77,17 +78,17 @@
     "v_cmp_nle_f32_e64 s[60:61], v38, %[eps]\n\t"   /* !(det <= eps): NaN passes */   \
     "s_and_b64 s[60:61], s[60:61], " MASK "\n\t"                                      \
     "s_cbranch_scc0 " NEXT "\n\t"                                                     \
-    "v_div_scale_f32 v25, s[62:63], v38, v38, 1.0\n\t"   /* 1/det, IEEE (hipcc's */  \
-    "v_rcp_f32_e32 v26, v25\n\t"                         /* own sequence)        */  \
-    "v_div_scale_f32 v27, vcc, 1.0, v38, 1.0\n\t"                                     \
-    "v_fma_f32 v28, -v25, v26, 1.0\n\t"                                               \
-    "v_fmac_f32_e32 v26, v28, v26\n\t"                                                \
-    "v_mul_f32_e32 v28, v27, v26\n\t"                                                 \
-    "v_fma_f32 v24, -v25, v28, v27\n\t"                                               \
-    "v_fmac_f32_e32 v28, v24, v26\n\t"                                                \
-    "v_fma_f32 v25, -v25, v28, v27\n\t"                                               \
-    "v_div_fmas_f32 v25, v25, v26, v28\n\t"                                           \
-    "v_div_fixup_f32 v38, v25, v38, 1.0\n\t"                                          \
+    "v_div_scale_f32 v27, s[62:63], v38, v38, 1.0\n\t"   /* 1/det, IEEE (hipcc's */  \
+    "v_rcp_f32_e32 v28, v27\n\t"                         /* own sequence; keeps  */  \
+    "v_div_scale_f32 v29, vcc, 1.0, v38, 1.0\n\t"         /* t0/t1 in v25/v26)    */  \
+    "v_fma_f32 v30, -v27, v28, 1.0\n\t"                                               \
+    "v_fmac_f32_e32 v28, v30, v28\n\t"                                                \
+    "v_mul_f32_e32 v30, v29, v28\n\t"                                                 \
+    "v_fma_f32 v24, -v27, v30, v29\n\t"                                               \
+    "v_fmac_f32_e32 v30, v24, v28\n\t"                                                \
+    "v_fma_f32 v27, -v27, v30, v29\n\t"                                               \
+    "v_div_fmas_f32 v27, v27, v28, v30\n\t"                                           \
+    "v_div_fixup_f32 v38, v27, v38, 1.0\n\t"                                          \
     "v_mul_f32_e32 v33, s42, v35\n\t"        /* u = ((sx*px + sy*py) + sz*pz)*inv */  \
     "v_mul_f32_e32 v34, s43, v36\n\t"                                                 \
     "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
@@ -175,10 +176,9 @@
     "s_mov_b32 s80, " W "\n\t"                                                        \
     "v_cmp_eq_u32_e64 s[62:63], s72, 1\n\t"                                           \
     "v_cmp_eq_u32_e64 s[68:69], s72, 2\n\t"                                           \
-    "v_bfe_u32 v33, %[sgn], s72, 1\n\t"      /* this lane runs -axis */               \
-    "v_cmp_ne_u32_e64 s[58:59], 0, v33\n\t"                                           \
     "v_cndmask_b32_e64 v24, %[ix], %[iy], s[62:63]\n\t"   /* inv = {ix,iy,iz}[axis] */ \
     "v_cndmask_b32_e64 v24, v24, %[iz], s[68:69]\n\t"                                 \
+    "v_cmp_gt_f32_e64 s[58:59], 0, v24\n\t" /* this lane runs -axis: sign = inv < 0 */ \
     "v_mul_f32_e32 v25, " D0 ", v24\n\t"     /* t0 = (clip0 - O[axis]) * inv */       \
     "v_mul_f32_e32 v26, " D1 ", v24\n\t"     /* t1 */                                 \
     "s_lshl_b32 s74, s73, 4\n\t"                                                      \
@@ -236,10 +236,6 @@
     "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
     "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
     "v_cmp_gt_f32_e64 s[56:57], v26, v28\n\t"                                         \
-    "v_cndmask_b32_e64 v29, %[tmin], v25, s[58:59]\n\t"   /* left  [neg ? t0 : tMin, */ \
-    "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
-    "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
-    "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL = (t0 > sL) ^ neg */  \
     "s_and_b64 s[54:55], s[54:55], s[52:53]\n\t"                                      \
     "s_xnor_b64 s[56:57], s[56:57], s[58:59]\n\t"         /* gR = !((t1 > sR) ^ neg) */ \
@@ -254,19 +250,23 @@
     "s_cbranch_scc0 .LBIH_TL_%=\n\t"         /* only the left child */                \
     "s_bitcmp1_b32 %[near], s72\n\t"        /* both: near first, stack the other */  \
     "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
+    "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
+    "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
     BIH_PUSH("r", "s[56:57]", "v31", "v32", "1")                                      \
     ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
     "s_mov_b64 s[52:53], s[54:55]\n\t"                                                \
-    "v_mov_b32_e32 %[tmin], v29\n\t"                                                  \
-    "v_mov_b32_e32 %[tmax], v30\n\t"                                                  \
+    "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
+    "v_cndmask_b32_e64 %[tmax], v25, %[tmax], s[58:59]\n\t" /*  neg ? tMax : t0]    */ \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     "s_branch .LBIH_NB0_%=\n\t"                                                       \
     ".LBIH_BR_%=:\n\t"                                                                \
+    "v_cndmask_b32_e64 v29, %[tmin], v25, s[58:59]\n\t"   /* left  [neg ? t0 : tMin, */ \
+    "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
     BIH_PUSH("l", "s[54:55]", "v29", "v30", "0")                                      \
     ".LBIH_TR_%=:\n\t"                       /* take right: record in s[88:91] */     \
     "s_mov_b64 s[52:53], s[56:57]\n\t"                                                \
-    "v_mov_b32_e32 %[tmin], v31\n\t"                                                  \
-    "v_mov_b32_e32 %[tmax], v32\n\t"                                                  \
+    "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[58:59]\n\t" /* [neg ? tMin : t1,    */ \
+    "v_cndmask_b32_e64 %[tmax], %[tmax], v26, s[58:59]\n\t" /*  neg ? t1 : tMax]    */ \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     "s_branch .LBIH_NB1_%=\n\t"                                                       \
     ".LBIH_DN_%=:\n\t"                       /* no left: right or pop */              \
