@@ -46,6 +46,7 @@ def main():
     print(json.dumps({"tag": a.tag, "lib": os.environ.get("BIH_LIB", "default"),
                       "kernel": os.environ.get("BIH_RENDER_KERNEL", "default"),
                       "traverse": a.traverse, "ms_mean": sum(t) / len(t), "ms_min": min(t),
+                      "ms_median": sorted(t)[len(t) // 2], "ms_all": [round(x, 3) for x in t],
                       "mrays_s": a.width * a.height * a.spp / (sum(t) / len(t)) / 1e3,
                       "img_hash": int(img.astype(np.uint64).sum())}), flush=True)
 
