@@ -52,6 +52,8 @@ def parse():
                     help="N=1: measure HBM traffic per launch with rocprofv3 PMC passes "
                          "(child processes, before this process touches the GPU)")
     ap.add_argument("--no-reference-leg", action="store_true")
+    ap.add_argument("--no-rebuild-leg", action="store_true",
+                    help="skip the leg that rebuilds the BIH every frame (as the reference does)")
     return ap.parse_args()
 
 
@@ -147,6 +149,34 @@ def main():
                    "ms_per_step": 1e3 * el2 / args.steps,
                    "kernel_ms": sum(kms2) / len(kms2)}
 
+    # the reference rebuilds the BIH every frame (Renderer::Render,
+    # Renderer.cpp:415-503): time rebuild + render per step as well
+    rebuild_leg = None
+    if not args.no_rebuild_leg:
+        def step_rb(frame):
+            arrays.rebuild()
+            step(frame, trav)
+        for k in range(args.warmup):
+            step_rb(2000 + k)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step_rb(2000 + args.warmup + k)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el3 = time.perf_counter() - t0
+        t3 = torch.tensor([el3], dtype=torch.float64, device="cuda")
+        if dist is not None:
+            dist.all_reduce(t3, op=dist.ReduceOp.MAX)
+        el3 = float(t3.item())
+        rebuild_leg = {"value": rays_per_frame * args.steps / el3, "unit": "rays/s",
+                       "ms_per_step": 1e3 * el3 / args.steps,
+                       "build_ms": arrays.info().build_ms,
+                       "note": "step = bih_rebuild + render (+ gather for N > 1)"}
+
     # per-ray work counters of one frame (untimed): exact integers, equal to
     # the oracle's (tests/test_gpu_parity.py::test_per_ray_counters_match_oracle)
     stat_frame = args.warmup
@@ -206,6 +236,7 @@ def main():
             "traffic_detail": traffic,
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
+            "with_rebuild": rebuild_leg,
         }
         if parity_rows is not None:
             res["parity_sample_rows_equal"] = parity_rows

@@ -27,6 +27,7 @@ constexpr int kScanItems = 8;
 constexpr int kScanTile = kThreads * kScanItems;     // 2048
 constexpr int kRsItems = 16;
 constexpr int kRsTile = kThreads * kRsItems;          // 4096
+constexpr uint32_t kPrepBlocks = 1024;                // k_prep grid (partials per block)
 
 __device__ __forceinline__ int clz32(uint32_t x) { return x ? __clz((int)x) : 32; }
 
@@ -56,7 +57,8 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
                                                    float *__restrict__ lo, float *__restrict__ hi,
-                                                   TreeHeader *hdr) {
+                                                   TreeHeader *hdr,
+                                                   unsigned long long *__restrict__ part) {
     unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
     uint32_t bad = 0;
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
@@ -79,7 +81,9 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
         }
     }
-    // wave reduce then one atomic per wave
+    // wave reduce, block reduce through LDS, one partial per block (the
+    // single-block k_prep_final folds them: no contended atomics)
+    __shared__ unsigned long long s_key[6][kThreads / 64];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -89,14 +93,25 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             kmax[a] = oM > kmax[a] ? oM : kmax[a];
         }
     }
-    unsigned long long anybad = __ballot(bad);
+    const unsigned long long anybad = __ballot(bad);
+    const uint32_t wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            atomicMin(&hdr->lo_key[a], kmin[a]);
-            atomicMax(&hdr->hi_key[a], kmax[a]);
+            s_key[a][wv] = kmin[a];
+            s_key[3 + a][wv] = kmax[a];
         }
         if (anybad) atomicOr(&hdr->nonfinite, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int a = threadIdx.x;
+        unsigned long long r = s_key[a][0];
+        for (uint32_t w = 1; w < kThreads / 64; ++w) {
+            const unsigned long long o = s_key[a][w];
+            r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+        }
+        part[(size_t)a * gridDim.x + blockIdx.x] = r;
     }
 }
 
@@ -116,13 +131,41 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
     }
 }
 
-__global__ void k_prep_final(const float *__restrict__ v, const float *__restrict__ lo,
-                             const float *__restrict__ hi, TreeHeader *hdr, uint32_t n) {
-    int a = threadIdx.x;
+__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
+                                                         const float *__restrict__ lo,
+                                                         const float *__restrict__ hi,
+                                                         TreeHeader *hdr, uint32_t n,
+                                                         const unsigned long long *__restrict__ part,
+                                                         uint32_t nparts) {
+    // fold the per-block (value, index) keys: min for lo, max for hi
+    __shared__ unsigned long long s_red[6][kThreads / 64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        unsigned long long r = a < 3 ? ~0ull : 0ull;
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) {
+            const unsigned long long o = part[(size_t)a * nparts + i];
+            r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(r, off);
+            r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+        }
+        if (lane == 0) s_red[a][wv] = r;
+    }
+    __syncthreads();
+    const int a = threadIdx.x;
     if (a >= 3) return;
     if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
-    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(hdr->lo_key[a] & 0xFFFFFFFFull);
-    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(hdr->hi_key[a] & 0xFFFFFFFFull);
+    unsigned long long kmin = s_red[a][0], kmax = s_red[3 + a][0];
+    for (uint32_t w = 1; w < kThreads / 64; ++w) {
+        kmin = s_red[a][w] < kmin ? s_red[a][w] : kmin;
+        kmax = s_red[3 + a][w] > kmax ? s_red[3 + a][w] : kmax;
+    }
+    hdr->lo_key[a] = kmin;
+    hdr->hi_key[a] = kmax;
+    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
+    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
     hdr->scene_lo[a] = lo[3ull * ilo + a];
     float mx = hi[3ull * ihi + a];
     float seed = v[a];                         // first vertex (App.cpp:103-106)
@@ -544,7 +587,7 @@ void free_tree_device(DeviceTree &t) {
     void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
                     t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,
                     t.children, t.parent, t.is_leaf, t.fit_cnt, t.fit_box, t.nodes, t.tris_s,
-                    t.hist, t.partials};
+                    t.hist, t.partials, t.prep_part};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (t.owns_v && t.v) (void)hipFree(t.v);
@@ -590,6 +633,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
         BIH_TRY(dalloc(&t.hist, hist_n, b));
         BIH_TRY(dalloc(&t.partials, (uint64_t)max_parts + 1, b));
+        BIH_TRY(dalloc(&t.prep_part, 6ull * kPrepBlocks, b));
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     BIH_TRY(hipEventCreate(&e0));
@@ -600,10 +644,11 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
-        uint32_t prep_blocks = blocks_for(n) < 4096u ? blocks_for(n) : 4096u;
+        const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
-                           t.tri_hi, t.hdr);
-        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(64), 0, st, t.v, t.tri_lo, t.tri_hi, t.hdr, n);
+                           t.tri_hi, t.hdr, t.prep_part);
+        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
+                           t.hdr, n, t.prep_part, prep_blocks);
         hipLaunchKernelGGL(k_morton, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi,
                            t.hdr, n, t.keys, t.vals);
         // 4 stable passes over 30-bit keys

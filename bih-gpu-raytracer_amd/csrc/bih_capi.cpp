@@ -73,10 +73,17 @@ int check_device(int device) {
 }
 
 int finish_build(bih_tree *tr) {
+    // a render launched through this tree may still read the buffers the
+    // build rewrites (it may run on another stream): order after it
+    if (tr->timed) {
+        hipError_t e = hipStreamWaitEvent(tr->stream, tr->ev1, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     float ms = 0.f;
     int e = bih::build_tree_device(tr->t, tr->stream, &ms);
     tr->build_ms = ms;
-    tr->rng_valid = false;   // tree changed; RNG is independent but keep it simple
+    // the per-pixel RNG state does not depend on the geometry: a rebuild (the
+    // reference rebuilds every frame) keeps the frame sequence going
     tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
     return map_hip(e);
 }

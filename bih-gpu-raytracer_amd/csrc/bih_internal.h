@@ -101,6 +101,7 @@ struct DeviceTree {
     float *tris_s = nullptr;
     uint32_t *hist = nullptr;                       // radix histograms
     uint32_t *partials = nullptr;
+    unsigned long long *prep_part = nullptr;        // k_prep per-block AABB keys
 };
 
 // builder (bih_build.hip); returns hipError_t as int

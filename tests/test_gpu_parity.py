@@ -236,3 +236,19 @@ def test_kernel_variants_agree(variant, gpu, tmp_path):
     for k in a.files:
         if k.endswith("_img") or "_ref_" in k:
             assert np.array_equal(a[k], b[k]), (variant, k)
+
+
+def test_rebuild_keeps_frame_sequence(gpu, bihrt_mod, oracle_mod):
+    """Per-frame rebuild (as Renderer::Render does) between renders: the tree
+    is rebuilt bit-identically and the RNG frame sequence continues."""
+    tris = SCENES["cornell"]
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    r = bihrt_mod.Renderer(g, 96, 64)
+    for frame in range(4):
+        if frame:
+            g.rebuild()
+        img = r.render(frame)
+        ref, _ = ot.render(96, 64, frame=frame)
+        assert np.array_equal(img, ref), frame
+    _tree_equal(g.arrays(), ot)
