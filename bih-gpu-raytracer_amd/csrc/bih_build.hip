@@ -506,7 +506,11 @@ __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__
     int32_t prev = (int32_t)k;
     int32_t p = leaf_parent[k];
     while (p >= 0) {
-        int side = (children[2 * p] == prev) ? 0 : 1;
+        // node data the second arriver needs, requested before the hand-off
+        const int32_t c0 = children[2 * p];
+        const int ax = axis[p];
+        const int32_t pp = parent[p];
+        int side = (c0 == prev) ? 0 : 1;
         box_put(box + (size_t)p * 12 + side * 6, blo, bhi);
         uint32_t old = atomicAdd(arrive + p, 1u);
         if (old == 0u) return;                      // first arriver stops
@@ -514,13 +518,12 @@ __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__
         box_get(box + (size_t)p * 12 + (1 - side) * 6, slo, shi);
         const float *lhi = side ? shi : bhi;    // left child's box is the sibling's when side==1
         const float *rlo = side ? blo : slo;
-        int ax = axis[p];
         clip[2 * p] = tmax(-FLT_MAX, lhi[ax]);        // initial values GPUArrayManager.cpp:79-80
         clip[2 * p + 1] = tmin(FLT_MAX, rlo[ax]);
 #pragma unroll
         for (int a = 0; a < 3; ++a) { blo[a] = tmin(blo[a], slo[a]); bhi[a] = tmax(bhi[a], shi[a]); }
         prev = p;
-        p = parent[p];
+        p = pp;
     }
 }
 
