@@ -3,11 +3,16 @@
 
 Workload (BASELINE.json configs[2]): 1,000,000-triangle
 random soup (splitmix64 seed 1), 1920x1080, 4 jittered primary rays per
-pixel, reference camera, cuRAND-XORWOW seed 1984.  One step = one frame:
-the render kernel over this rank's interleaved 8-row bands plus, for N > 1,
-the RCCL all-gather that assembles the frame on every rank.  The BIH is
-built once before the timed region (its device time is reported as build_ms;
-the reference rebuilds it every frame, Renderer.cpp:415-503).
+pixel, reference camera, cuRAND-XORWOW seed 1984.  One step = one frame
+per GPU: frames are independent units of work, so with N GPUs rank r renders
+whole frames r, r+N, r+2N, ... of the reference's frame sequence (byte-
+identical to the frames a one-GPU run renders at those indices) with no
+collective in the step -- weak scaling, value = N x rays per frame x steps /
+max-over-ranks time.  For N > 1 a second, informational leg ("strong_tiled")
+splits every frame into interleaved 8-row bands across the ranks and
+assembles it with an RCCL all-gather.  The BIH is built once before the timed
+region (its device time is reported as build_ms; the reference rebuilds it
+every frame, Renderer.cpp:415-503 -- the "with_rebuild" leg times that).
 
 Single process:   python bench.py
 Multi-GPU:        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -41,6 +46,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
+                    help="N > 1: whole frames per rank (weak) or row bands of one frame + "
+                         "all-gather (strong) as the headline; the other runs as a side leg")
     ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on rank 0 (N=1)")
     ap.add_argument("--cpu-row-step", type=int, default=1,
@@ -71,14 +79,21 @@ def main():
     if world == 1 and args.traffic:
         traffic = measure_traffic(args)
 
+    # rehearsal of the N > 1 path on a one-GPU box: all ranks on cuda:0 over gloo
+    shared = os.environ.get("BIH_BENCH_SHARE_GPU") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import bihrt
-    from bihrt.tiling import band_rows, gather_order, max_rows
+    from bihrt.tiling import band_rows, frame_of_step, gather_order, max_rows
 
     W, H, SPP = args.width, args.height, args.spp
     # one explicit stream for build, render, events and the all-gather
@@ -94,88 +109,98 @@ def main():
     info = arrays.info()
     cam = bihrt.camera_reference(W, H)
     r = bihrt.Renderer(arrays, W, H, spp=SPP, seed=1984, camera=cam)
-    rows = band_rows(H, args.band, rank, world)
+    # weak: this rank renders whole frames; strong: its bands of every frame
     mrows = max_rows(H, args.band, world)
-    out = torch.zeros(mrows * W, dtype=torch.int32, device="cuda")
+    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     gathered = torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") if world > 1 else None
     if world > 1:
         order = torch.from_numpy(gather_order(H, args.band, world)).cuda()
         frame_img = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 
-    def step(frame, traverse, ev=None):
+    def plan(mode):
+        """(rows of this rank, frame index of step k from `base`, frames per step job-wide)"""
+        if mode == "weak" or world == 1:
+            return band_rows(H, args.band, 0, 1), (lambda base, k: frame_of_step(base, k, rank, world)), world
+        return band_rows(H, args.band, rank, world), (lambda base, k: base + k), 1
+
+    def step(mode, rows, frame, traverse, ev=None):
         if ev is not None:
             ev[0].record(stream)
         r.render_device(out.data_ptr(), frame, rows=rows, traverse=traverse, stream=sptr)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        if mode == "strong" and world > 1:
+            dist.all_gather_into_tensor(gathered, out[: mrows * W])
             torch.index_select(gathered.view(world * mrows, W), 0, order,
                                out=frame_img.view(H, W))
 
-    def timed(traverse, first_frame):
-        for k in range(args.warmup):
-            step(first_frame + k, traverse)
+    def sync_all():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+
+    def max_over_ranks(el):
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(mode, traverse, base, rebuild=False):
+        rows, frame_of, fps = plan(mode)
+        for k in range(args.warmup):
+            if rebuild:
+                arrays.rebuild()
+            step(mode, rows, frame_of(base, k), traverse)
+        sync_all()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
         t0 = time.perf_counter()
         for k in range(args.steps):
-            step(first_frame + args.warmup + k, traverse, evs[k])
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        if dist is not None:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if rebuild:
+                arrays.rebuild()
+            step(mode, rows, frame_of(base, args.warmup + k), traverse, evs[k])
+        sync_all()
+        el = max_over_ranks(time.perf_counter() - t0)
         kms = [a.elapsed_time(b) for a, b in evs]
-        return float(t.item()), kms
+        return el, sum(kms) / len(kms), fps
 
-    elapsed, kms = timed(trav, 0)
+    mode = args.mode if world > 1 else "weak"
+    rows, _, _ = plan(mode)
     rays_per_frame = W * H * SPP
-    value = rays_per_frame * args.steps / elapsed
-    kernel_ms = sum(kms) / len(kms)
+    elapsed, kernel_ms, fps = timed(mode, trav, 0)
+    value = fps * rays_per_frame * args.steps / elapsed
 
     ref_leg = None
     if not args.no_reference_leg:
         other = bihrt.TRAVERSE_REFERENCE if trav == bihrt.TRAVERSE_ANYHIT else bihrt.TRAVERSE_ANYHIT
-        el2, kms2 = timed(other, 1000)
+        el2, kms2, fps2 = timed(mode, other, 1000)
         ref_leg = {"traverse": "reference" if other == bihrt.TRAVERSE_REFERENCE else "anyhit",
-                   "value": rays_per_frame * args.steps / el2,
+                   "value": fps2 * rays_per_frame * args.steps / el2,
                    "ms_per_step": 1e3 * el2 / args.steps,
-                   "kernel_ms": sum(kms2) / len(kms2)}
+                   "kernel_ms": kms2}
+
+    # N > 1: the other decomposition, informational
+    side_leg = None
+    if world > 1:
+        other_mode = "strong" if mode == "weak" else "weak"
+        el4, kms4, fps4 = timed(other_mode, trav, 3000)
+        side_leg = {"mode": other_mode,
+                    "scaling": other_mode,
+                    "value": fps4 * rays_per_frame * args.steps / el4, "unit": "rays/s",
+                    "ms_per_step": 1e3 * el4 / args.steps, "kernel_ms": kms4,
+                    "parallelism": parallelism(other_mode, args.band, world)}
 
     # the reference rebuilds the BIH every frame (Renderer::Render,
     # Renderer.cpp:415-503): time rebuild + render per step as well
     rebuild_leg = None
     if not args.no_rebuild_leg:
-        def step_rb(frame):
-            arrays.rebuild()
-            step(frame, trav)
-        for k in range(args.warmup):
-            step_rb(2000 + k)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step_rb(2000 + args.warmup + k)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el3 = time.perf_counter() - t0
-        t3 = torch.tensor([el3], dtype=torch.float64, device="cuda")
-        if dist is not None:
-            dist.all_reduce(t3, op=dist.ReduceOp.MAX)
-        el3 = float(t3.item())
-        rebuild_leg = {"value": rays_per_frame * args.steps / el3, "unit": "rays/s",
+        el3, _, fps3 = timed(mode, trav, 2000, rebuild=True)
+        rebuild_leg = {"value": fps3 * rays_per_frame * args.steps / el3, "unit": "rays/s",
                        "ms_per_step": 1e3 * el3 / args.steps,
                        "build_ms": arrays.info().build_ms,
-                       "note": "step = bih_rebuild + render (+ gather for N > 1)"}
+                       "note": "step = bih_rebuild + render"
+                               + (" + gather" if mode == "strong" and world > 1 else "")}
 
     # per-ray work counters of one frame (untimed): exact integers, equal to
     # the oracle's (tests/test_gpu_parity.py::test_per_ray_counters_match_oracle)
@@ -186,7 +211,7 @@ def main():
                     stream=sptr)
     torch.cuda.synchronize()
     sums = st.view(-1, 3).to(torch.int64).sum(0)
-    if dist is not None:
+    if dist is not None and mode == "strong":
         dist.all_reduce(sums)
     n_node, n_leaf, n_tri = [int(x) for x in sums.tolist()]
     rays_all = rays_per_frame
@@ -209,7 +234,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": mode,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: 1M-triangle soup, splitmix64 seed 1, centroids U([0,2.667]x[-1,1]x[0,2]) "
@@ -219,8 +244,7 @@ def main():
                             "reference camera, XORWOW seed 1984",
                 "tris": args.tris, "unique_codes": info.n_unique, "width": W, "height": H,
                 "spp": SPP, "traverse": args.traverse,
-                "parallelism": f"row bands of {args.band} rows interleaved over {world} GPU(s)"
-                               + (" + RCCL all_gather" if world > 1 else ""),
+                "parallelism": parallelism(mode, args.band, world),
             },
             "kernel_ms": kernel_ms,
             "build_ms": info.build_ms,
@@ -237,6 +261,7 @@ def main():
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
             "with_rebuild": rebuild_leg,
+            "other_decomposition": side_leg,
         }
         if parity_rows is not None:
             res["parity_sample_rows_equal"] = parity_rows
@@ -244,6 +269,14 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def parallelism(mode, band, world):
+    if world == 1:
+        return "1 GPU, whole frames"
+    if mode == "weak":
+        return f"whole frames round-robin over {world} GPUs (rank r: frames r, r+{world}, ...), no collective"
+    return f"row bands of {band} rows interleaved over {world} GPUs + RCCL all_gather"
 
 
 def cpu_model():

@@ -1,5 +1,10 @@
-"""Row tiling of one frame across ranks (one process per GPU).
+"""Decompositions of the frame sequence across ranks (one process per GPU).
 
+Frames (the default, weak scaling): frames are independent units of work,
+so rank r renders whole frames r, r+N, r+2N, ... of the one-GPU sequence;
+no data crosses ranks.
+
+Row bands (strong scaling, one frame split):
 The frame is cut into bands of B rows dealt round-robin to the ranks
 ("interleaved row bands"): the scene sits in the middle of the reference
 camera's view, so contiguous row blocks would leave the outer ranks idle.
@@ -47,3 +52,9 @@ def gather_order(h: int, band: int, world: int) -> np.ndarray:
         ys = rows_of_rank(h, band, r, world)
         order[ys] = np.arange(ys.size) + r * mrows
     return order
+
+
+def frame_of_step(base: int, k: int, rank: int, world: int) -> int:
+    """Frame index rank `rank` renders at its k-th step when whole frames are
+    dealt round-robin: steps k of all ranks cover frames base + kN .. base + kN + N-1."""
+    return base + k * world + rank

@@ -303,10 +303,18 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
         tr->rng_cur = 0;
         tr->rng_valid = false;
     }
-    bool same = tr->rng_valid && tr->key_w == w && tr->key_spp == spp && tr->key_seed == seed &&
-                tr->key_row0 == rows.row0 && tr->key_nrows == rows.nrows &&
-                tr->key_bh == rows.band_h && tr->key_bs == rows.band_step && tr->next_frame == frame;
-    if (!same) {
+    const bool same_px = tr->rng_valid && tr->key_w == w && tr->key_spp == spp &&
+                         tr->key_seed == seed && tr->key_row0 == rows.row0 &&
+                         tr->key_nrows == rows.nrows && tr->key_bh == rows.band_h &&
+                         tr->key_bs == rows.band_step;
+    const bool same = same_px && tr->next_frame == frame;
+    if (same_px && frame > tr->next_frame && (uint64_t)(frame - tr->next_frame) * 2 * spp <= 4096) {
+        // a short gap in the frame sequence: run the generators forward
+        // (cheaper than re-seeding with the 2^67-subsequence jump)
+        const uint32_t steps = (frame - tr->next_frame) * 2 * spp;
+        int e = bih::launch_rng_advance(tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap, P, steps, st);
+        if (e) return map_hip(e);
+    } else if (!same) {
         uint64_t skip = (uint64_t)2 * spp * frame;
         int e = bih::launch_rng_init(tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap, w, rows.row0,
                                      rows.nrows, rows.band_h, rows.band_step,

@@ -113,6 +113,8 @@ int upload_rng_tables(int device);
 const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 step][160][5]
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
+// state of every pixel advanced by `steps` draws, in place (buffer of `pixels`)
+int launch_rng_advance(uint32_t *rng, uint64_t pixels, uint32_t steps, void *stream);
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);

@@ -95,6 +95,25 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
     for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
 }
 
+// Advances every pixel's XORWOW xorshift state by `steps` draws (a frame
+// gap in a sequence: frames f..f+k-1 skipped); the Weyl counter d is derived
+// from the frame index and is not stored.
+__global__ void __launch_bounds__(kThreads) k_rng_advance(uint32_t *__restrict__ rng, uint64_t P,
+                                                          uint32_t steps) {
+    const uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (lp >= P) return;
+    uint32_t v[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v[i] = rng[(uint64_t)i * P + lp];
+    for (uint32_t k = 0; k < steps; ++k) {
+        const uint32_t t = v[0] ^ (v[0] >> 2);
+        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
+}
+
 __device__ __forceinline__ float xorwow_uniform(uint32_t v[5], uint32_t &d) {
     uint32_t t = v[0] ^ (v[0] >> 2);
     v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
@@ -1524,6 +1543,14 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     hipLaunchKernelGGL(k_rng_init, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, rng, w, row0,
                        nrows, band_h, band_step, v[0], v[1], v[2], v[3], v[4],
                        (unsigned long long)skip, tab);
+    return (int)hipGetLastError();
+}
+
+int launch_rng_advance(uint32_t *rng, uint64_t pixels, uint32_t steps, void *stream) {
+    if (pixels == 0 || steps == 0) return 0;
+    const uint32_t blocks = (uint32_t)((pixels + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, rng,
+                       (uint64_t)pixels, steps);
     return (int)hipGetLastError();
 }
 

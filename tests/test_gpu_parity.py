@@ -252,3 +252,18 @@ def test_rebuild_keeps_frame_sequence(gpu, bihrt_mod, oracle_mod):
         ref, _ = ot.render(96, 64, frame=frame)
         assert np.array_equal(img, ref), frame
     _tree_equal(g.arrays(), ot)
+
+
+@pytest.mark.gpu
+def test_frame_gaps_match_oracle(gpu, bihrt_mod, oracle_mod):
+    """Frames rendered out of sequence (the weak-scaling schedule: rank r
+    renders r, r+N, ...): short forward gaps advance the stored generators,
+    long or backward gaps re-seed; every frame equals the oracle's."""
+    tris = SCENES["cornell"]
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    r = bihrt_mod.Renderer(g, 80, 48)
+    for frame in (0, 3, 11, 12, 600, 2, 9):
+        img = r.render(frame)
+        ref, _ = ot.render(80, 48, frame=frame)
+        assert np.array_equal(img, ref), frame
