@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="frames in flight: consecutive frames on this many streams, so the "
+                         "next frame fills the tail of the one before (1 = one frame at a time)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="N > 1: whole frames per rank (weak) or row bands of one frame + "
                          "all-gather (strong) as the headline; the other runs as a side leg")
@@ -96,8 +99,12 @@ def main():
     from bihrt.tiling import band_rows, frame_of_step, gather_order, max_rows
 
     W, H, SPP = args.width, args.height, args.spp
-    # one explicit stream for build, render, events and the all-gather
-    stream = torch.cuda.Stream()
+    # explicit streams: the build and untimed work on streams[0]; frame k of a
+    # timed leg on streams[k % in_flight] with its own output buffers, so that
+    # consecutive frames overlap (libbih_amd orders what they share)
+    F = max(1, args.in_flight)
+    streams = [torch.cuda.Stream() for _ in range(F)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
@@ -111,11 +118,12 @@ def main():
     r = bihrt.Renderer(arrays, W, H, spp=SPP, seed=1984, camera=cam)
     # weak: this rank renders whole frames; strong: its bands of every frame
     mrows = max_rows(H, args.band, world)
-    out = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    gathered = torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") if world > 1 else None
+    outs = [torch.zeros(H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
+    out = outs[0]
     if world > 1:
+        gathered = [torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") for _ in range(F)]
         order = torch.from_numpy(gather_order(H, args.band, world)).cuda()
-        frame_img = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        frame_img = [torch.zeros(H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
     trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 
     def plan(mode):
@@ -124,16 +132,22 @@ def main():
             return band_rows(H, args.band, 0, 1), (lambda base, k: frame_of_step(base, k, rank, world)), world
         return band_rows(H, args.band, rank, world), (lambda base, k: base + k), 1
 
-    def step(mode, rows, frame, traverse, ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        r.render_device(out.data_ptr(), frame, rows=rows, traverse=traverse, stream=sptr)
-        if ev is not None:
-            ev[1].record(stream)
-        if mode == "strong" and world > 1:
-            dist.all_gather_into_tensor(gathered, out[: mrows * W])
-            torch.index_select(gathered.view(world * mrows, W), 0, order,
-                               out=frame_img.view(H, W))
+    def step(mode, rows, k, frame, traverse, ev=None, rebuild=False, nf=F):
+        j = k % nf
+        s = streams[j]
+        with torch.cuda.stream(s):
+            if rebuild:
+                arrays.rebuild()
+            if ev is not None:
+                ev[0].record(s)
+            r.render_device(outs[j].data_ptr(), frame, rows=rows, traverse=traverse,
+                            stream=s.cuda_stream)
+            if ev is not None:
+                ev[1].record(s)
+            if mode == "strong" and world > 1:
+                dist.all_gather_into_tensor(gathered[j], outs[j][: mrows * W])
+                torch.index_select(gathered[j].view(world * mrows, W), 0, order,
+                                   out=frame_img[j].view(H, W))
 
     def sync_all():
         if dist is not None:
@@ -146,20 +160,17 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def timed(mode, traverse, base, rebuild=False):
+    def timed(mode, traverse, base, rebuild=False, nf=F):
         rows, frame_of, fps = plan(mode)
         for k in range(args.warmup):
-            if rebuild:
-                arrays.rebuild()
-            step(mode, rows, frame_of(base, k), traverse)
+            step(mode, rows, k, frame_of(base, k), traverse, rebuild=rebuild, nf=nf)
         sync_all()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
         t0 = time.perf_counter()
         for k in range(args.steps):
-            if rebuild:
-                arrays.rebuild()
-            step(mode, rows, frame_of(base, args.warmup + k), traverse, evs[k])
+            step(mode, rows, args.warmup + k, frame_of(base, args.warmup + k), traverse, evs[k],
+                 rebuild=rebuild, nf=nf)
         sync_all()
         el = max_over_ranks(time.perf_counter() - t0)
         kms = [a.elapsed_time(b) for a, b in evs]
@@ -179,6 +190,14 @@ def main():
                    "value": fps2 * rays_per_frame * args.steps / el2,
                    "ms_per_step": 1e3 * el2 / args.steps,
                    "kernel_ms": kms2}
+
+    # one frame at a time (frame latency): informational when frames overlap
+    serial_leg = None
+    if F > 1:
+        el5, kms5, fps5 = timed(mode, trav, 4000, nf=1)
+        serial_leg = {"value": fps5 * rays_per_frame * args.steps / el5, "unit": "rays/s",
+                      "ms_per_step": 1e3 * el5 / args.steps, "kernel_ms": kms5,
+                      "note": "in_flight 1: each frame starts after the previous one ends"}
 
     # N > 1: the other decomposition, informational
     side_leg = None
@@ -245,6 +264,7 @@ def main():
                 "tris": args.tris, "unique_codes": info.n_unique, "width": W, "height": H,
                 "spp": SPP, "traverse": args.traverse,
                 "parallelism": parallelism(mode, args.band, world),
+                "frames_in_flight": F,
             },
             "kernel_ms": kernel_ms,
             "build_ms": info.build_ms,
@@ -253,6 +273,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "bytes_per_ray": b_ray,
+                "launch_ms": kernel_ms,
+                "effective_gbs": b_ray * launch_rays / (elapsed / args.steps) / 1e9,
                 "counters_per_ray": {"nodes": n_node / rays_all, "leaves": n_leaf / rays_all,
                                      "tris": n_tri / rays_all},
                 "kernel": f"k_render_packet_asm ({'any-hit' if trav == 0 else 'reference'} walk)",
@@ -261,6 +283,7 @@ def main():
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
             "with_rebuild": rebuild_leg,
+            "one_in_flight": serial_leg,
             "other_decomposition": side_leg,
         }
         if parity_rows is not None:

@@ -17,15 +17,27 @@
 #include "../../include/bih.h"
 #include "bih_internal.h"
 
+// Two renders through one tree may be in flight together (issued on two
+// streams): each launch takes one of kSlots {tile queue, spill area, events}
+// in turn, and reads its frame's XORWOW state from a ring of three buffers
+// that k_rng_advance fills one frame ahead.
+constexpr int kSlots = 2;
+constexpr int kRngBufs = 3;
+
 struct bih_tree {
     bih::DeviceTree t;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0[kSlots] = {nullptr, nullptr}, ev1[kSlots] = {nullptr, nullptr};
+    bool used[kSlots] = {false, false};
+    int slot = 0;                    // slot of the next render
+    int last_slot = -1;              // slot of the last render
+    hipEvent_t ev_rng = nullptr;     // after the advance that produced rng buffer rng_cur
+    bool rng_pending = false;
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
     // render state cache (Renderer::d_rand_state / CreateCUDABuffers)
     mutable std::mutex mu;
-    uint32_t *rng = nullptr;
+    uint32_t *rng = nullptr;         // [kRngBufs][5][cap] XORWOW planes + [kSlots][cap] accumulators
     size_t rng_cap = 0;              // pixels
     int rng_cur = 0;                 // which XORWOW buffer holds the next frame's input
     uint32_t *fb = nullptr;
@@ -34,10 +46,10 @@ struct bih_tree {
     uint32_t key_w = 0, key_spp = 0, key_row0 = 0, key_nrows = 0, key_bh = 0, key_bs = 0;
     uint64_t key_seed = 0;
     uint32_t next_frame = 0;
-    bool timed = false;
     bool owns_stream = false;
-    uint32_t *work = nullptr;        // persistent-kernel tile counter
-    uint32_t *spill = nullptr;       // traversal stack spill area
+    uint32_t *work = nullptr;        // persistent-kernel tile counters, kWorkWords per slot
+    uint32_t *spill = nullptr;       // traversal stack spill area, spill_words per slot
+    size_t spill_per_slot = 0;       // u32
     float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
@@ -72,13 +84,21 @@ int check_device(int device) {
     return BIH_OK;
 }
 
+// Orders `st` after every render in flight through this tree.
+int wait_renders(bih_tree *tr, hipStream_t st) {
+    for (int k = 0; k < kSlots; ++k)
+        if (tr->used[k]) {
+            hipError_t e = hipStreamWaitEvent(st, tr->ev1[k], 0);
+            if (e != hipSuccess) return map_hip((int)e);
+        }
+    return BIH_OK;
+}
+
 int finish_build(bih_tree *tr) {
     // a render launched through this tree may still read the buffers the
     // build rewrites (it may run on another stream): order after it
-    if (tr->timed) {
-        hipError_t e = hipStreamWaitEvent(tr->stream, tr->ev1, 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
+    int rc = wait_renders(tr, tr->stream);
+    if (rc) return rc;
     float ms = 0.f;
     int e = bih::build_tree_device(tr->t, tr->stream, &ms);
     tr->build_ms = ms;
@@ -99,8 +119,11 @@ int create_tree(int device, void *stream, bih_tree **out) {
         e = hipStreamCreateWithFlags(&tr->stream, hipStreamNonBlocking);
         tr->owns_stream = (e == hipSuccess);
     }
-    if (e == hipSuccess) e = hipEventCreate(&tr->ev0);
-    if (e == hipSuccess) e = hipEventCreate(&tr->ev1);
+    for (int k = 0; k < kSlots && e == hipSuccess; ++k) {
+        e = hipEventCreate(&tr->ev0[k]);
+        if (e == hipSuccess) e = hipEventCreate(&tr->ev1[k]);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
     if (e == hipSuccess && bih::upload_rng_tables(device) != 0) e = hipErrorUnknown;
     if (e != hipSuccess) {
         delete tr;
@@ -218,14 +241,19 @@ void bih_free(bih_tree *tr) {
     if (!tr) return;
     DeviceGuard g(tr->t.device);
     if (tr->stream) (void)hipStreamSynchronize(tr->stream);
+    for (int k = 0; k < kSlots; ++k)
+        if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
     bih::free_tree_device(tr->t);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
     if (tr->spill) (void)hipFree(tr->spill);
     if (tr->prim) (void)hipFree(tr->prim);
-    if (tr->ev0) (void)hipEventDestroy(tr->ev0);
-    if (tr->ev1) (void)hipEventDestroy(tr->ev1);
+    for (int k = 0; k < kSlots; ++k) {
+        if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
+        if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
+    }
+    if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
     delete tr;
 }
@@ -285,19 +313,31 @@ int bih_tree_export(const bih_tree *tr, int which, void *dst, size_t *bytes) {
     return map_hip((int)e);
 }
 
+static uint32_t *rng_buf(const bih_tree *tr, int k) {
+    return tr->rng + (size_t)k * 5 * tr->rng_cap;
+}
+
 // Ensures the per-pixel RNG state for this framebuffer geometry sits at the
-// start of `frame` (InitRandGPU once, then cudaRender advances it 2*spp
-// draws per frame; a non-sequential frame re-seeds with a skip-ahead).
+// start of `frame` in buffer rng_cur (InitRandGPU once, then cudaRender's
+// 2*spp draws per frame; a short gap runs the generators forward, anything
+// else re-seeds with a skip-ahead).  Runs on `st` after the renders that
+// read rng_cur before (see bih_render_device).
 static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, uint64_t seed,
                        const bih_rows &rows, hipStream_t st) {
     const size_t P = (size_t)rows.nrows * w;
     if (P > tr->rng_cap) {
-        // layout: [2][5][cap] XORWOW planes (in/out, swapped per frame) + [cap] pixel accumulators
+        for (int k = 0; k < kSlots; ++k)
+            if (tr->used[k]) {
+                hipError_t e = hipEventSynchronize(tr->ev1[k]);   // in-flight readers
+                if (e != hipSuccess) return map_hip((int)e);
+            }
         if (tr->rng) (void)hipFree(tr->rng);
         tr->rng = nullptr;
         tr->rng_cap = 0;
-        hipError_t e = hipMalloc((void **)&tr->rng, P * 11 * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemsetAsync(tr->rng + 10 * P, 0, P * sizeof(uint32_t), st);
+        const size_t words = P * (5 * kRngBufs + kSlots);
+        hipError_t e = hipMalloc((void **)&tr->rng, words * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemsetAsync(tr->rng + 5 * kRngBufs * P, 0, kSlots * P * sizeof(uint32_t), st);
         if (e != hipSuccess) return map_hip((int)e);
         tr->rng_cap = P;
         tr->rng_cur = 0;
@@ -312,11 +352,12 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
         // a short gap in the frame sequence: run the generators forward
         // (cheaper than re-seeding with the 2^67-subsequence jump)
         const uint32_t steps = (frame - tr->next_frame) * 2 * spp;
-        int e = bih::launch_rng_advance(tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap, P, steps, st);
+        uint32_t *b = rng_buf(tr, tr->rng_cur);
+        int e = bih::launch_rng_advance(b, b, P, steps, st);
         if (e) return map_hip(e);
     } else if (!same) {
         uint64_t skip = (uint64_t)2 * spp * frame;
-        int e = bih::launch_rng_init(tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap, w, rows.row0,
+        int e = bih::launch_rng_init(rng_buf(tr, tr->rng_cur), w, rows.row0,
                                      rows.nrows, rows.band_h, rows.band_step,
                                      seed, skip, tr->t.device, st);
         if (e) return map_hip(e);
@@ -351,39 +392,65 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     if (!tr->work) {
-        hipError_t e = hipMalloc((void **)&tr->work, bih::kWorkWords * sizeof(uint32_t));
+        tr->spill_per_slot = bih::spill_words(bih::wave_grid_blocks(tr->t.device));
+        hipError_t e = hipMalloc((void **)&tr->work, kSlots * bih::kWorkWords * sizeof(uint32_t));
         if (e == hipSuccess)
-            e = hipMalloc((void **)&tr->spill,
-                          bih::spill_words(bih::wave_grid_blocks(tr->t.device)) * sizeof(uint32_t));
+            e = hipMalloc((void **)&tr->spill, kSlots * tr->spill_per_slot * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip((int)e);
     }
-    // renders through one tree share its RNG state, tile counter and spill
-    // area: order this launch after the previous one, whatever the stream
-    if (tr->timed) {
-        hipError_t e = hipStreamWaitEvent(st, tr->ev1, 0);
+    // Dependencies (f = this render, f-1 and f-2 the two before it):
+    //  - slot: the render two launches ago used this tile queue and spill
+    //    area, and read rng buffer (cur+1)%3, which the advance below rewrites;
+    //  - rng: the advance issued with render f-1 produced buffer cur (and
+    //    ran after render f-3, the last reader of buffer cur before).
+    // Render f-1 itself is not waited for: consecutive frames on two
+    // streams overlap, the second filling the first one's tail.
+    const int slot = tr->slot;
+    if (tr->used[slot]) {
+        hipError_t e = hipStreamWaitEvent(st, tr->ev1[slot], 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    if (tr->rng_pending) {
+        hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
     int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
+    const size_t P = (size_t)rows.nrows * w;
+    const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
+    // the state cudaRender leaves behind for frame+1 (CUDAKernels.cu:419)
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, st));
+    if (rc) return rc;
+    hipError_t e = hipEventRecord(tr->ev_rng, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_pending = true;
     // primary-ray triangle records follow the camera origin
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
     if (bih::render_uses_prim(spp) && tr->t.n > 0) {
         uint32_t ob[3];
         memcpy(ob, cam->origin, sizeof ob);
         const size_t need = bih::prim_bytes(tr->t.n, n_int);
-        if (tr->prim_cap < need) {
+        const bool grow = tr->prim_cap < need;
+        if (grow || !tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
+            // rewritten in place: after every render still reading the records
+            rc = wait_renders(tr, st);
+            if (rc) return rc;
+        }
+        if (grow) {
+            for (int k = 0; k < kSlots; ++k)
+                if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
             if (tr->prim) (void)hipFree(tr->prim);
             tr->prim = nullptr;
             tr->prim_cap = 0;
-            hipError_t e = hipMalloc((void **)&tr->prim, need);
+            e = hipMalloc((void **)&tr->prim, need);
             if (e != hipSuccess) return map_hip((int)e);
             tr->prim_cap = need;
             tr->prim_valid = false;
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
-            int e = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, n_int, cam->origin,
-                                     tr->prim, st);
-            if (e) return map_hip(e);
+            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, n_int, cam->origin,
+                                      tr->prim, st);
+            if (le) return map_hip(le);
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
         }
@@ -407,23 +474,22 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.tri_prim = tr->prim;
     a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
-    const size_t P = (size_t)rows.nrows * w;
-    a.rng_in = tr->rng + (size_t)tr->rng_cur * 5 * tr->rng_cap;
-    a.rng_out = tr->rng + (size_t)(1 - tr->rng_cur) * 5 * tr->rng_cap;
-    a.pixacc = tr->rng + (size_t)10 * tr->rng_cap;
-    (void)P;
+    a.rng_in = rng_buf(tr, cur);
+    a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;
     a.out = d_out;
     a.ray_stats = d_ray_stats;
-    a.work = tr->work;
-    a.spill = tr->spill;
-    hipError_t e = hipEventRecord(tr->ev0, st);
+    a.work = tr->work + (size_t)slot * bih::kWorkWords;
+    a.spill = tr->spill + (size_t)slot * tr->spill_per_slot;
+    e = hipEventRecord(tr->ev0[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     rc = bih::launch_render(a, traverse, st);
     if (rc) return map_hip(rc);
-    e = hipEventRecord(tr->ev1, st);
+    e = hipEventRecord(tr->ev1[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
-    tr->timed = true;
-    tr->rng_cur = 1 - tr->rng_cur;   // this frame's output state feeds the next frame
+    tr->used[slot] = true;
+    tr->last_slot = slot;
+    tr->slot = (slot + 1) % kSlots;
+    tr->rng_cur = nxt;                 // frame+1's state
     return BIH_OK;
 }
 
@@ -447,12 +513,13 @@ int bih_sync(const bih_tree *tr, void *stream) {
 }
 
 int bih_last_render_ms(const bih_tree *tr, double *ms) {
-    if (!tr || !ms || !tr->timed) return BIH_ERR_INVALID;
+    if (!tr || !ms || tr->last_slot < 0) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
-    hipError_t e = hipEventSynchronize(tr->ev1);
+    const int k = tr->last_slot;
+    hipError_t e = hipEventSynchronize(tr->ev1[k]);
     if (e != hipSuccess) return map_hip((int)e);
     float f = 0.f;
-    e = hipEventElapsedTime(&f, tr->ev0, tr->ev1);
+    e = hipEventElapsedTime(&f, tr->ev0[k], tr->ev1[k]);
     if (e != hipSuccess) return map_hip((int)e);
     *ms = f;
     return BIH_OK;

@@ -67,9 +67,7 @@ struct RenderArgs {
     const float *tri_prim;  // 16 f32 per triangle: primary-ray records for origin cam[0..2]
     const uint4 *node_prim; // per node {clip0 - O[axis], clip1 - O[axis], z, w} for the same origin
     const uint32_t *dup_cnt;
-    const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame
-    uint32_t *rng_out;      // state after the frame (double-buffered: a pixel's
-                            // samples may run in different waves)
+    const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame (read only)
     uint32_t *pixacc;       // per-pixel {hits<<16 | samples} of the refill kernel (kept 0)
     uint32_t *out;          // nrows*w pixels
     uint32_t *ray_stats;    // optional 3 u32 per ray {nodes, leaves, tris}
@@ -113,8 +111,9 @@ int upload_rng_tables(int device);
 const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 step][160][5]
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
-// state of every pixel advanced by `steps` draws, in place (buffer of `pixels`)
-int launch_rng_advance(uint32_t *rng, uint64_t pixels, uint32_t steps, void *stream);
+// dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
+int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
+                       void *stream);
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);

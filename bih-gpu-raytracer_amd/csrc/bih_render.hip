@@ -95,23 +95,24 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
     for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
 }
 
-// Advances every pixel's XORWOW xorshift state by `steps` draws (a frame
-// gap in a sequence: frames f..f+k-1 skipped); the Weyl counter d is derived
-// from the frame index and is not stored.
-__global__ void __launch_bounds__(kThreads) k_rng_advance(uint32_t *__restrict__ rng, uint64_t P,
-                                                          uint32_t steps) {
+// dst = every pixel's XORWOW xorshift state `steps` draws after src's (dst
+// may be src).  2*spp steps: the state the next frame starts from
+// (cudaRender's write-back, CUDAKernels.cu:419); more: a gap in the frame
+// sequence.  The Weyl counter d is derived from the frame index, not stored.
+__global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst,
+                                                          uint64_t P, uint32_t steps) {
     const uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (lp >= P) return;
     uint32_t v[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) v[i] = rng[(uint64_t)i * P + lp];
+    for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
     for (uint32_t k = 0; k < steps; ++k) {
         const uint32_t t = v[0] ^ (v[0] >> 2);
         v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
         v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
     }
 #pragma unroll
-    for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
+    for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
 }
 
 __device__ __forceinline__ float xorwow_uniform(uint32_t v[5], uint32_t &d) {
@@ -412,8 +413,9 @@ __device__ __forceinline__ void ray_coords(uint64_t rid, uint32_t tiles_x, uint3
 }
 
 // RNG for sample s of pixel lp: draws 2s, 2s+1 of this frame (the pixel's
-// state advanced 2s+2 steps).  The lane of the last sample stores the state
-// the reference's cudaRender leaves behind (:419) into rng_out.
+// state advanced 2s+2 steps).  The state the reference's cudaRender leaves
+// behind (:419) is produced by k_rng_advance, not here: the render only reads
+// its frame's state, so consecutive frames can be in flight together.
 template <uint32_t SPP>
 __device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uint32_t s, float &ru,
                                            float &rv) {
@@ -425,10 +427,6 @@ __device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uin
     for (uint32_t k = 0; k <= s; ++k) {
         ru = xorwow_uniform(v, d);
         rv = xorwow_uniform(v, d);
-    }
-    if (s == SPP - 1) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = v[i];
     }
 }
 
@@ -626,8 +624,6 @@ __global__ void __launch_bounds__(kThreads) k_render_pixel(const RenderArgs a) {
             }
             k += w.hit ? 1u : 0u;
         }
-#pragma unroll
-        for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = v[i];
         a.out[lp] = pixel_from_hits(k, a.spp);
     }
 }
@@ -1546,11 +1542,12 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
-int launch_rng_advance(uint32_t *rng, uint64_t pixels, uint32_t steps, void *stream) {
-    if (pixels == 0 || steps == 0) return 0;
+int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
+                       void *stream) {
+    if (pixels == 0 || (steps == 0 && src == dst)) return 0;
     const uint32_t blocks = (uint32_t)((pixels + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, rng,
-                       (uint64_t)pixels, steps);
+    hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, src,
+                       dst, (uint64_t)pixels, steps);
     return (int)hipGetLastError();
 }
 

@@ -267,3 +267,28 @@ def test_frame_gaps_match_oracle(gpu, bihrt_mod, oracle_mod):
         img = r.render(frame)
         ref, _ = ot.render(80, 48, frame=frame)
         assert np.array_equal(img, ref), frame
+
+
+@pytest.mark.gpu
+def test_frames_in_flight_on_two_streams(gpu, bihrt_mod, oracle_mod):
+    """Consecutive frames issued on two streams overlap on the GPU (the
+    library orders only what they share: tile queues, spill areas, the RNG
+    ring); a gap, a rebuild and a 1M-scale frame mid-sequence keep every frame
+    equal to the oracle's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(20_000, seed=9)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 160, 96
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    frames = [0, 1, 2, 3, 7, 8, 9, 30, 31, 2, 3]
+    outs = [torch.zeros(h * w, dtype=torch.int32, device="cuda") for _ in frames]
+    for k, f in enumerate(frames):
+        if k == 6:
+            g.rebuild()
+        r.render_device(outs[k].data_ptr(), f, stream=streams[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for k, f in enumerate(frames):
+        ref, _ = ot.render(w, h, frame=f)
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32).reshape(h, w), ref), (k, f)
