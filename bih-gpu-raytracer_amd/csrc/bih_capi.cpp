@@ -17,18 +17,21 @@
 #include "../../include/bih.h"
 #include "bih_internal.h"
 
-// Two renders through one tree may be in flight together (issued on two
-// streams): each launch takes one of kSlots {tile queue, spill area, events}
-// in turn, and reads its frame's XORWOW state from a ring of three buffers
-// that k_rng_advance fills one frame ahead.
-constexpr int kSlots = 2;
-constexpr int kRngBufs = 3;
+// Up to kSlots renders through one tree may be in flight together (issued
+// on as many streams): each launch takes one of kSlots {tile queue, spill
+// area, events} in turn, and reads its frame's XORWOW state from a ring of
+// kSlots + 1 buffers that k_rng_advance fills one frame ahead.
+#ifndef BIH_RENDER_SLOTS
+#define BIH_RENDER_SLOTS 2
+#endif
+constexpr int kSlots = BIH_RENDER_SLOTS;
+constexpr int kRngBufs = kSlots + 1;
 
 struct bih_tree {
     bih::DeviceTree t;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0[kSlots] = {nullptr, nullptr}, ev1[kSlots] = {nullptr, nullptr};
-    bool used[kSlots] = {false, false};
+    hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {};
+    bool used[kSlots] = {};
     int slot = 0;                    // slot of the next render
     int last_slot = -1;              // slot of the last render
     hipEvent_t ev_rng = nullptr;     // after the advance that produced rng buffer rng_cur
@@ -398,13 +401,13 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             e = hipMalloc((void **)&tr->spill, kSlots * tr->spill_per_slot * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip((int)e);
     }
-    // Dependencies (f = this render, f-1 and f-2 the two before it):
-    //  - slot: the render two launches ago used this tile queue and spill
-    //    area, and read rng buffer (cur+1)%3, which the advance below rewrites;
+    // Dependencies (f = this render, S = kSlots):
+    //  - slot: render f-S used this tile queue and spill area, and read rng
+    //    buffer (cur+1)%(S+1), which the advance below rewrites;
     //  - rng: the advance issued with render f-1 produced buffer cur (and
-    //    ran after render f-3, the last reader of buffer cur before).
-    // Render f-1 itself is not waited for: consecutive frames on two
-    // streams overlap, the second filling the first one's tail.
+    //    ran after render f-1-S, the last reader of buffer cur before).
+    // Renders f-S+1 .. f-1 are not waited for: consecutive frames on
+    // separate streams overlap, each filling the one before's tail.
     const int slot = tr->slot;
     if (tr->used[slot]) {
         hipError_t e = hipStreamWaitEvent(st, tr->ev1[slot], 0);
@@ -448,7 +451,8 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             tr->prim_valid = false;
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
-            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, n_int, cam->origin,
+            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.dup_cnt, n_int,
+                                      cam->origin,
                                       tr->prim, st);
             if (le) return map_hip(le);
             memcpy(tr->prim_origin, ob, sizeof ob);
@@ -473,6 +477,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.tris = tr->t.tris_s;
     a.tri_prim = tr->prim;
     a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
+    a.node_cull = a.node_prim ? a.node_prim + (n_int + 1) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
     a.rng_in = rng_buf(tr, cur);
     a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;
@@ -498,13 +503,15 @@ int bih_sync(const bih_tree *tr, void *stream) {
     DeviceGuard g(tr->t.device);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
 #if BIH_PACKET_COUNTERS
-    if (tr->work) {
+    if (tr->work && tr->last_slot >= 0) {
         uint32_t c[bih::kWorkWords];
-        if (hipMemcpyAsync(c, tr->work, sizeof c, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        if (hipMemcpyAsync(c, tr->work + (size_t)tr->last_slot * bih::kWorkWords, sizeof c, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess) {
             fprintf(stderr, "packet-counters packets %u nodes %u leaves %u tris %u pushes %u pops %u maxsp %u depth",
                     c[16], c[17], c[18], c[19], c[20], c[21], c[22]);
             for (int k = 0; k < 32; ++k) fprintf(stderr, " %u", c[24 + k]);
+            fprintf(stderr, " mt");
+            for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[56 + k]);
             fprintf(stderr, "\n");
         }
     }

@@ -66,6 +66,7 @@ struct RenderArgs {
     const float *tris;
     const float *tri_prim;  // 16 f32 per triangle: primary-ray records for origin cam[0..2]
     const uint4 *node_prim; // per node {clip0 - O[axis], clip1 - O[axis], z, w} for the same origin
+    const uint4 *node_cull; // node_prim with leaves no primary ray can hit cut off (k_node_prim)
     const uint32_t *dup_cnt;
     const uint32_t *rng_in; // 5 planes of nrows*w: XORWOW v at the start of the frame (read only)
     uint32_t *pixacc;       // per-pixel {hits<<16 | samples} of the refill kernel (kept 0)
@@ -118,9 +119,11 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);
 // primary-ray records for camera origin `origin`: n triangle records
-// (16 f32, k_tri_prim) followed by m = U-1 node records (u32x4, k_node_prim)
+// (16 f32, k_tri_prim), then m = U-1 node records (u32x4, k_node_prim) + 1
+// pad, then the same m + 1 records with unhittable leaves cut off
 size_t prim_bytes(uint32_t n, uint32_t m);
-int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const uint32_t *dup_cnt,
+                uint32_t m, const float origin[3],
                 float *prim, void *stream);
 bool render_uses_prim(uint32_t spp);
 

@@ -891,16 +891,55 @@ __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) 
 //   * child order chosen once per packet and axis (majority direction).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long prim_hits(const sf32x16 r, float dx, float dy, float dz,
-                                                       unsigned long long m) {
+                                                       unsigned long long m,
+                                                       uint32_t *cnt = nullptr) {
     const float px = dy * r[5] - r[4] * dz;          // pvec = cross(D, e2)
     const float py = dz * r[3] - r[5] * dx;
     const float pz = dx * r[4] - r[3] * dy;
     const float det = (r[0] * px + r[1] * py) + r[2] * pz;
+#if BIH_PACKET_COUNTERS
+    // wave-level outcome counters (debug builds): [0] tests, [1] all lanes
+    // out at det, [2] at u, [3] reach v, [4] some hit, [5]/[6] division-free
+    // filters on u / on u and v would drop every lane, [7] [6] but not [2]
+    const bool lead = (threadIdx.x & 63) == 0;
+    unsigned long long mf = 0;
+    if (cnt) {
+        if (lead) atomicAdd(cnt, 1u);
+        const unsigned long long md = m & __ballot(!(det <= kDetEps));
+        if (md) {
+            const float un = (r[6] * px + r[7] * py) + r[8] * pz;
+            const float vn = (dx * r[9] + dy * r[10]) + dz * r[11];
+            const float lo = det * 0x1p-20f, hiu = det * (1.0f + 0x1p-20f);
+            const float hiuv = det * (1.0f + 0x1p-18f);
+            const unsigned long long fu = md & __ballot(!(un < -lo || un > hiu));
+            const unsigned long long fuv = fu & __ballot(!(vn < -lo || un + vn > hiuv));
+            if (lead && !fu) atomicAdd(cnt + 5, 1u);
+            if (lead && !fuv) atomicAdd(cnt + 6, 1u);
+            mf = fuv ? 1ull : 0ull;
+        } else if (lead) {
+            atomicAdd(cnt + 1, 1u);
+        }
+    }
+#endif
     m &= __ballot(!(det <= kDetEps));                // det < 0.000001 (double); NaN passes
     if (!m) return 0ull;
     const float inv = 1.0f / det;
     const float u = ((r[6] * px + r[7] * py) + r[8] * pz) * inv;
     m &= __ballot(!(u < 0.0f || u > 1.0f));
+#if BIH_PACKET_COUNTERS
+    if (cnt && lead) {
+        if (!m) atomicAdd(cnt + 2, 1u);
+        else atomicAdd(cnt + 3, 1u);
+        if (m && !mf) atomicAdd(cnt + 7, 1u);
+    }
+    if (cnt) {
+        const float v = ((dx * r[9] + dy * r[10]) + dz * r[11]) * inv;
+        const float t = r[12] * inv;
+        const unsigned long long h = m & __ballot(!(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX);
+        if (lead && h) atomicAdd(cnt + 4, 1u);
+        if (h && !mf && lead) atomicAdd(cnt + 4, 0x10000u);   // a filter miss: must never happen
+    }
+#endif
     if (!m) return 0ull;
     const float v = ((dx * r[9] + dy * r[10]) + dz * r[11]) * inv;
     const float t = r[12] * inv;
@@ -957,7 +996,7 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
     const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + wv;
     uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - D) * 3 * 64;
     const SceneU sc = load_scene(a);
-    const cnode_t *nodes = (const cnode_t *)(const void *)a.node_prim;
+    const cnode_t *nodes = (const cnode_t *)(const void *)(STATS ? a.node_prim : a.node_cull);
     const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
     const cu32_t *dupc = (const cu32_t *)(const void *)a.dup_cnt;
     const uint32_t tiles_x = (a.w + TW - 1) / TW;
@@ -1025,7 +1064,11 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 ++pk[3];
 #endif
                 if (STATS && (m & me)) ++c_tris;
+#if BIH_PACKET_COUNTERS
+                hits |= prim_hits(prims[b], dx, dy, dz, m, a.work + 56);
+#else
                 hits |= prim_hits(prims[b], dx, dy, dz, m);
+#endif
             }
         };
 
@@ -1281,7 +1324,7 @@ k_render_packet_asm(const RenderArgs a) {
     const uint32_t *wspill = a.spill + gwave * (uint64_t)(kStackDepth - kPacketRegs) * 3 * 64;
     const SceneU sc = load_scene(a);
     const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
-    const void *nodes = (const void *)a.node_prim;
+    const void *nodes = (const void *)(STATS ? a.node_prim : a.node_cull);
     const void *dupc = (const void *)a.dup_cnt;
     const uint32_t tiles_x = (a.w + TW - 1) / TW;
     const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
@@ -1404,17 +1447,55 @@ k_render_packet_asm(const RenderArgs a) {
     }
 }
 
-// Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}.
+// A primary ray from O can hit triangle k only if its tnum = dot(e2, q) (the
+// ray-independent numerator of t, k_tri_prim) is a positive finite f32:
+// t = tnum * (1/det) with 1/det > 0 finite for every lane that passes the
+// det test (CUDAKernels.cu:33-47), so tnum <= 0, +inf or NaN gives t <= 0,
+// inf or NaN, and the t > 0 && t < FLT_MAX test fails for every ray.
+__device__ __forceinline__ bool tri_alive(const float *prim, uint32_t k) {
+    const uint32_t b = __float_as_uint(prim[16ull * k + 12]);
+    return b - 1u < 0x7f7fffffu;                 // 0 < b < 0x7f800000
+}
+
+__device__ __forceinline__ bool leaf_dead(const float *prim, uint32_t b, uint32_t e) {
+    if (e - b > 64u) return false;               // long duplicate runs: not worth a scan
+    for (uint32_t k = b; k < e; ++k)
+        if (tri_alive(prim, k)) return false;
+    return true;
+}
+
+// Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}, and
+// the same records with every leaf child whose triangles no primary ray from
+// O can hit (tri_alive) cut off: clip0 - O = -inf (left) / clip1 - O = +inf
+// (right) make t0 = -inf*inv / t1 = +inf*inv fail the child's visit test
+// (tMin < t[near], !(tMax < t[far])) for either ray direction, so the walk
+// never enters the leaf.  Only which dead leaves are visited changes, so the
+// hit set -- and the image -- is the same; the per-ray counters are not, and
+// STATS launches use the exact records.
 __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict__ nodes, uint32_t m,
                                                         float ox, float oy, float oz,
-                                                        uint4 *__restrict__ out) {
+                                                        const float *__restrict__ prim,
+                                                        const uint32_t *__restrict__ dup_cnt,
+                                                        uint4 *__restrict__ out,
+                                                        uint4 *__restrict__ out_cull) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= m) return;
     const uint4 nd = nodes[i];
     const uint32_t ax = (nd.z >> 27) & 3u;
     const float org = sel3(ax, ox, oy, oz);
-    out[i] = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
-                        __float_as_uint(__uint_as_float(nd.y) - org), nd.z, nd.w);
+    uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
+                         __float_as_uint(__uint_as_float(nd.y) - org), nd.z, nd.w);
+    out[i] = r;
+    const uint32_t split = nd.z & 0x7ffffffu, mid = nd.w & 0x7ffffffu;
+    if ((nd.z >> 29) & 1u) {
+        const uint32_t c = ((nd.w >> 27) & 3u) ? ((nd.w >> 27) & 3u) : dup_cnt[split];
+        if (leaf_dead(prim, mid - c, mid)) r.x = 0xff800000u;   // -inf
+    }
+    if ((nd.z >> 30) & 1u) {
+        const uint32_t c = ((nd.w >> 29) & 3u) ? ((nd.w >> 29) & 3u) : dup_cnt[split + 1];
+        if (leaf_dead(prim, mid, mid + c)) r.y = 0x7f800000u;   // +inf
+    }
+    out_cull[i] = r;
 }
 
 // Primary-ray triangle records for the camera origin O (every primary ray of
@@ -1551,19 +1632,21 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
     return (int)hipGetLastError();
 }
 
-// + one record of padding: the packet walk prefetches the record pair
+// triangle records, then the exact and the culled node records, each with
+// one record of padding: the packet walk prefetches the record pair
 // {split, split+1}, and split+1 may be one past the last internal node
-size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + (size_t)(m + 1) * 16; }
+size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16; }
 
-int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
-                float *prim, void *stream) {
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const uint32_t *dup_cnt,
+                uint32_t m, const float origin[3], float *prim, void *stream) {
     if (n > 0)
         hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
                            (hipStream_t)stream, tris, n, origin[0], origin[1], origin[2], prim);
     if (m > 0)
         hipLaunchKernelGGL(k_node_prim, dim3((m + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                           (hipStream_t)stream, nodes, m, origin[0], origin[1], origin[2],
-                           reinterpret_cast<uint4 *>(prim + 16ull * n));
+                           (hipStream_t)stream, nodes, m, origin[0], origin[1], origin[2], prim,
+                           dup_cnt, reinterpret_cast<uint4 *>(prim + 16ull * n),
+                           reinterpret_cast<uint4 *>(prim + 16ull * n) + (m + 1));
     return (int)hipGetLastError();
 }
 
