@@ -451,7 +451,8 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             tr->prim_valid = false;
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
-            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.dup_cnt, n_int,
+            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
+                                      tr->t.dup_cnt, n_int,
                                       cam->origin,
                                       tr->prim, st);
             if (le) return map_hip(le);

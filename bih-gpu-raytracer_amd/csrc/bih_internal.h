@@ -120,10 +120,11 @@ uint32_t wave_grid_blocks(int device);     // persistent grid of the render kern
 size_t spill_words(uint32_t blocks);
 // primary-ray records for camera origin `origin`: n triangle records
 // (16 f32, k_tri_prim), then m = U-1 node records (u32x4, k_node_prim) + 1
-// pad, then the same m + 1 records with unhittable leaves cut off
+// pad, then the same m + 1 records with unhittable subtrees cut off, then
+// per-leaf and per-node alive bytes
 size_t prim_bytes(uint32_t n, uint32_t m);
-int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const uint32_t *dup_cnt,
-                uint32_t m, const float origin[3],
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
+                const uint32_t *dup_cnt, uint32_t m, const float origin[3],
                 float *prim, void *stream);
 bool render_uses_prim(uint32_t spp);
 

@@ -1457,25 +1457,48 @@ __device__ __forceinline__ bool tri_alive(const float *prim, uint32_t k) {
     return b - 1u < 0x7f7fffffu;                 // 0 < b < 0x7f800000
 }
 
-__device__ __forceinline__ bool leaf_dead(const float *prim, uint32_t b, uint32_t e) {
-    if (e - b > 64u) return false;               // long duplicate runs: not worth a scan
-    for (uint32_t k = b; k < e; ++k)
-        if (tri_alive(prim, k)) return false;
-    return true;
+// Leaf k can produce a hit only if one of its triangles [first[k],
+// first[k] + cnt[k]) is alive; long duplicate runs count as alive unscanned.
+__global__ void __launch_bounds__(kThreads) k_leaf_alive(const float *__restrict__ prim,
+                                                         const int32_t *__restrict__ first,
+                                                         const uint32_t *__restrict__ cnt,
+                                                         uint32_t U, uint8_t *__restrict__ alive) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= U) return;
+    const uint32_t b = (uint32_t)first[k], c = cnt[k];
+    bool a = c > 64u;
+    for (uint32_t i = 0; !a && i < c; ++i) a = tri_alive(prim, b + i);
+    alive[k] = a ? 1 : 0;
+}
+
+// Internal node p is alive if a child is (leaf: leaf_alive; internal: this
+// array).  Starts all-alive and only ever clears entries whose children are
+// both dead, so any number of passes (run in place, in any order) leaves a
+// conservative answer; dead subtrees of height h need h passes.
+__global__ void __launch_bounds__(kThreads) k_node_alive(const uint4 *__restrict__ nodes, uint32_t m,
+                                                         const uint8_t *__restrict__ leaf_alive,
+                                                         uint8_t *__restrict__ node_alive) {
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= m || !node_alive[p]) return;
+    const uint4 nd = nodes[p];
+    const uint32_t split = nd.z & 0x7ffffffu;
+    const bool aL = ((nd.z >> 29) & 1u) ? leaf_alive[split] : node_alive[split];
+    const bool aR = ((nd.z >> 30) & 1u) ? leaf_alive[split + 1] : node_alive[split + 1];
+    if (!aL && !aR) node_alive[p] = 0;
 }
 
 // Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}, and
-// the same records with every leaf child whose triangles no primary ray from
-// O can hit (tri_alive) cut off: clip0 - O = -inf (left) / clip1 - O = +inf
-// (right) make t0 = -inf*inv / t1 = +inf*inv fail the child's visit test
-// (tMin < t[near], !(tMax < t[far])) for either ray direction, so the walk
-// never enters the leaf.  Only which dead leaves are visited changes, so the
-// hit set -- and the image -- is the same; the per-ray counters are not, and
-// STATS launches use the exact records.
+// the same records with every child subtree that no primary ray from O can
+// hit (all its triangles dead, tri_alive) cut off: clip0 - O = -inf (left) /
+// clip1 - O = +inf (right) make t0 = -inf*inv / t1 = +inf*inv fail the
+// child's visit test (tMin < t[near], !(tMax < t[far])) for either ray
+// direction, so the walk never enters it.  Only which dead subtrees are
+// visited changes, so the hit set -- and the image -- is the same; the
+// per-ray counters are not, and STATS launches use the exact records.
 __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict__ nodes, uint32_t m,
                                                         float ox, float oy, float oz,
-                                                        const float *__restrict__ prim,
-                                                        const uint32_t *__restrict__ dup_cnt,
+                                                        const uint8_t *__restrict__ leaf_alive,
+                                                        const uint8_t *__restrict__ node_alive,
                                                         uint4 *__restrict__ out,
                                                         uint4 *__restrict__ out_cull) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
@@ -1486,15 +1509,11 @@ __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict_
     uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
                          __float_as_uint(__uint_as_float(nd.y) - org), nd.z, nd.w);
     out[i] = r;
-    const uint32_t split = nd.z & 0x7ffffffu, mid = nd.w & 0x7ffffffu;
-    if ((nd.z >> 29) & 1u) {
-        const uint32_t c = ((nd.w >> 27) & 3u) ? ((nd.w >> 27) & 3u) : dup_cnt[split];
-        if (leaf_dead(prim, mid - c, mid)) r.x = 0xff800000u;   // -inf
-    }
-    if ((nd.z >> 30) & 1u) {
-        const uint32_t c = ((nd.w >> 29) & 3u) ? ((nd.w >> 29) & 3u) : dup_cnt[split + 1];
-        if (leaf_dead(prim, mid, mid + c)) r.y = 0x7f800000u;   // +inf
-    }
+    const uint32_t split = nd.z & 0x7ffffffu;
+    const bool aL = ((nd.z >> 29) & 1u) ? leaf_alive[split] : node_alive[split];
+    const bool aR = ((nd.z >> 30) & 1u) ? leaf_alive[split + 1] : node_alive[split + 1];
+    if (!aL) r.x = 0xff800000u;   // -inf
+    if (!aR) r.y = 0x7f800000u;   // +inf
     out_cull[i] = r;
 }
 
@@ -1633,20 +1652,37 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
 }
 
 // triangle records, then the exact and the culled node records, each with
-// one record of padding: the packet walk prefetches the record pair
-// {split, split+1}, and split+1 may be one past the last internal node
-size_t prim_bytes(uint32_t n, uint32_t m) { return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16; }
+// one record of padding (the packet walk prefetches the record pair {split,
+// split+1}, and split+1 may be one past the last internal node), then the
+// leaf and node alive bytes
+size_t prim_bytes(uint32_t n, uint32_t m) {
+    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + (((size_t)(m + 1) + m + 15) & ~(size_t)15);
+}
 
-int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const uint32_t *dup_cnt,
-                uint32_t m, const float origin[3], float *prim, void *stream) {
+int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
+                const uint32_t *dup_cnt, uint32_t m, const float origin[3], float *prim,
+                void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
     if (n > 0)
-        hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                           (hipStream_t)stream, tris, n, origin[0], origin[1], origin[2], prim);
-    if (m > 0)
-        hipLaunchKernelGGL(k_node_prim, dim3((m + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                           (hipStream_t)stream, nodes, m, origin[0], origin[1], origin[2], prim,
-                           dup_cnt, reinterpret_cast<uint4 *>(prim + 16ull * n),
-                           reinterpret_cast<uint4 *>(prim + 16ull * n) + (m + 1));
+        hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           tris, n, origin[0], origin[1], origin[2], prim);
+    if (m > 0) {
+        uint4 *rec = reinterpret_cast<uint4 *>(prim + 16ull * n);
+        uint8_t *leaf_alive = reinterpret_cast<uint8_t *>(rec + 2 * (size_t)(m + 1));
+        uint8_t *node_alive = leaf_alive + (m + 1);
+        const dim3 gl((m + 1 + kThreads - 1) / kThreads), gn((m + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_leaf_alive, gl, dim3(kThreads), 0, st, prim, first_idx, dup_cnt, m + 1,
+                           leaf_alive);
+        hipError_t e = hipMemsetAsync(node_alive, 1, m, st);
+        if (e != hipSuccess) return (int)e;
+        // dead subtrees of a random soup are a few levels high (1M triangles:
+        // 12 % of the nodes, every one found within 7 passes)
+        for (int pass = 0; pass < 8; ++pass)
+            hipLaunchKernelGGL(k_node_alive, gn, dim3(kThreads), 0, st, nodes, m, leaf_alive,
+                               node_alive);
+        hipLaunchKernelGGL(k_node_prim, gn, dim3(kThreads), 0, st, nodes, m, origin[0], origin[1],
+                           origin[2], leaf_alive, node_alive, rec, rec + (m + 1));
+    }
     return (int)hipGetLastError();
 }
 
