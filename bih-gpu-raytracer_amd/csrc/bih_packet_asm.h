@@ -21,12 +21,13 @@
 //
 // Register map (physical registers, listed as clobbers so hipcc keeps its own
 // values out of them; the stack lives only inside the statement):
-//   s[36:51] triangle record          s[52:53] act     s[54:55] gL
+//   s[36:51] triangle record          EXEC = the active lanes   s[54:55] gL
 //   s[56:57] gR       s[58:59] lanes running -axis     s[60:61] tmp / hit mask
 //   s[62:63] tmp      s[64:65] left-leaf lanes         s[66:67] right-leaf lanes
 //   s[68:69] tmp      s70 cur (pop)  s71 sp  s72 axis  s73 split  s74-s76 tmp
 //   s77 b  s78 e  s79 saved m0  s80 w (mid | counts)  s81 leaf bits  s82 mid
 //   s[84:91] record pair (prefetch)
+//   v62-v64 {ix, iy, iz} (inv = v[62 + axis], gpr-indexed)
 //   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of a stacked child
 //   (MT: v24, v27-v30 division temps; t0/t1 survive the leaf tests)
 //   v33-v38 temps (MT: v35-v37 p, v38 det then 1/det)  v39 stacked node ids
@@ -41,26 +42,31 @@
 #define BIH_S2(x) #x
 #define BIH_S(x) BIH_S2(x)
 
-// counters (STATS builds): v33 = this lane in MASK ? 1 : 0; counter += v33
-#define BIH_CNT(MASK, CNT) "v_cndmask_b32_e64 v33, 0, 1, " MASK "\n\tv_add_u32_e32 %[" CNT "], v33, %[" CNT "]\n\t"
-#define BIH_CNT_NODE BIH_CNT("s[52:53]", "cn")
-#define BIH_CNT_LEAF_L BIH_CNT("s[64:65]", "cl")
-#define BIH_CNT_LEAF_R BIH_CNT("s[66:67]", "cl")
-#define BIH_CNT_TRI_L BIH_CNT("s[64:65]", "ct")
-#define BIH_CNT_TRI_R BIH_CNT("s[66:67]", "ct")
+// counters (STATS builds): counter += 1 on the lanes of EXEC (the node's
+// active lanes at a node step, the lanes testing the triangle in the leaf
+// loop); a leaf counts the lanes of its mask
+#define BIH_CNT_EXEC(CNT) "v_add_u32_e32 %[" CNT "], 1, %[" CNT "]\n\t"
+#define BIH_CNT_MASK(MASK, CNT) "s_mov_b64 exec, " MASK "\n\t" BIH_CNT_EXEC(CNT)
+#define BIH_CNT_NODE BIH_CNT_EXEC("cn")
+#define BIH_CNT_LEAF_L BIH_CNT_MASK("s[64:65]", "cl")
+#define BIH_CNT_LEAF_R BIH_CNT_MASK("s[66:67]", "cl")
+#define BIH_CNT_TRI_L BIH_CNT_EXEC("ct")
+#define BIH_CNT_TRI_R BIH_CNT_EXEC("ct")
 
-// any-hit: drop lanes that already hit; leave when none is left
-#define BIH_ANY_ON(MASK, EXIT) "s_andn2_b64 " MASK ", " MASK ", %[hits]\n\ts_cbranch_scc0 " EXIT "\n\t"
-#define BIH_ANY_OFF(MASK, EXIT) ""
+// EXEC = the lanes testing the next triangle of a leaf: its mask, and with
+// any-hit without the lanes that already hit (leave when none is left)
+#define BIH_ANY_ON(MASK, EXIT) "s_andn2_b64 exec, " MASK ", %[hits]\n\ts_cbranch_scc0 " EXIT "\n\t"
+#define BIH_ANY_OFF(MASK, EXIT) "s_mov_b64 exec, " MASK "\n\t"
 #define BIH_CLR_ON(MASK) "s_andn2_b64 " MASK ", " MASK ", %[hits]\n\t"
 #define BIH_CLR_OFF(MASK) ""
-#define BIH_POP_ANY "s_andn2_b64 s[52:53], s[52:53], %[hits]\n\ts_cbranch_scc0 .LBIH_PL_%=\n\t"
+#define BIH_POP_ANY "s_andn2_b64 exec, exec, %[hits]\n\ts_cbranch_scc0 .LBIH_PL_%=\n\t"
 
-// Moeller-Trumbore of the record in s[36:51] for the lanes of MASK; the
-// passing lanes end in s[60:61]; a uniform miss jumps to NEXT.
+// Moeller-Trumbore of the record in s[36:51] for the lanes of EXEC; each
+// test narrows EXEC (v_cmpx), so the passing lanes end in EXEC; a uniform
+// miss jumps to NEXT.
 // Operand order of every f32 op follows prim_hits (bih_render.hip):
 // record = {e1 s36-38, e2 s39-41, s = O - v0 s42-44, q s45-47, tnum s48}.
-#define BIH_MT(MASK, NEXT)                                                            \
+#define BIH_MT(NEXT)                                                                  \
     "v_mul_f32_e32 v33, s41, %[dy]\n\t"      /* px = dy*e2z - e2y*dz */               \
     "v_mul_f32_e32 v34, s40, %[dz]\n\t"                                               \
     "v_sub_f32_e32 v35, v33, v34\n\t"                                                 \
@@ -75,9 +81,8 @@
     "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
     "v_mul_f32_e32 v34, s38, v37\n\t"                                                 \
     "v_add_f32_e32 v38, v33, v34\n\t"                                                 \
-    "v_cmp_nle_f32_e64 s[60:61], v38, %[eps]\n\t"   /* !(det <= eps): NaN passes */   \
-    "s_and_b64 s[60:61], s[60:61], " MASK "\n\t"                                      \
-    "s_cbranch_scc0 " NEXT "\n\t"                                                     \
+    "v_cmpx_nge_f32_e32 vcc, %[eps], v38\n\t"   /* !(det <= eps): NaN passes */        \
+    "s_cbranch_execz " NEXT "\n\t"                                                    \
     "v_div_scale_f32 v27, s[62:63], v38, v38, 1.0\n\t"   /* 1/det, IEEE (hipcc's */  \
     "v_rcp_f32_e32 v28, v27\n\t"                         /* own sequence; keeps  */  \
     "v_div_scale_f32 v29, vcc, 1.0, v38, 1.0\n\t"         /* t0/t1 in v25/v26)    */  \
@@ -95,11 +100,9 @@
     "v_mul_f32_e32 v34, s44, v37\n\t"                                                 \
     "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
     "v_mul_f32_e32 v35, v33, v38\n\t"                                                 \
-    "v_cmp_nlt_f32_e64 s[62:63], v35, 0\n\t"        /* !(u < 0 || u > 1) */           \
-    "v_cmp_ngt_f32_e64 s[68:69], v35, 1.0\n\t"                                        \
-    "s_and_b64 s[60:61], s[60:61], s[62:63]\n\t"                                      \
-    "s_and_b64 s[60:61], s[60:61], s[68:69]\n\t"                                      \
-    "s_cbranch_scc0 " NEXT "\n\t"                                                     \
+    "v_cmpx_ngt_f32_e32 vcc, 0, v35\n\t"           /* !(u < 0 || u > 1) */            \
+    "v_cmpx_nlt_f32_e32 vcc, 1.0, v35\n\t"                                            \
+    "s_cbranch_execz " NEXT "\n\t"                                                    \
     "v_mul_f32_e32 v33, s45, %[dx]\n\t"      /* v = ((dx*qx + dy*qy) + dz*qz)*inv */  \
     "v_mul_f32_e32 v34, s46, %[dy]\n\t"                                               \
     "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
@@ -108,16 +111,12 @@
     "v_mul_f32_e32 v36, v33, v38\n\t"                                                 \
     "v_mul_f32_e32 v37, s48, v38\n\t"        /* t = tnum*inv */                       \
     "v_add_f32_e32 v33, v35, v36\n\t"        /* u + v */                              \
-    "v_cmp_nlt_f32_e64 s[62:63], v36, 0\n\t"        /* !(v < 0 || u+v > 1) */         \
-    "v_cmp_ngt_f32_e64 s[68:69], v33, 1.0\n\t"                                        \
-    "s_and_b64 s[60:61], s[60:61], s[62:63]\n\t"                                      \
-    "s_and_b64 s[60:61], s[60:61], s[68:69]\n\t"                                      \
-    "v_cmp_lt_f32_e64 s[62:63], 0, v37\n\t"         /* t > 0 && t < FLT_MAX */        \
-    "v_cmp_gt_f32_e64 s[68:69], %[fmax], v37\n\t"                                     \
-    "s_and_b64 s[60:61], s[60:61], s[62:63]\n\t"                                      \
-    "s_and_b64 s[60:61], s[60:61], s[68:69]\n\t"
+    "v_cmpx_ngt_f32_e32 vcc, 0, v36\n\t"           /* !(v < 0 || u+v > 1) */          \
+    "v_cmpx_nlt_f32_e32 vcc, 1.0, v33\n\t"                                            \
+    "v_cmpx_lt_f32_e32 vcc, 0, v37\n\t"            /* t > 0 && t < FLT_MAX */         \
+    "v_cmpx_gt_f32_e32 vcc, %[fmax], v37\n\t"
 
-// Triangles [s77, s78) for the lanes of MASK.
+// Triangles [s77, s78) for the lanes of MASK (EXEC per triangle).
 #define BIH_TRIS(TAG, MASK, ANY_MASK, CNT_TRI)                                        \
     ".LBIH_T" TAG "_%=:\n\t"                                                          \
     "s_cmp_ge_u32 s77, s78\n\t"                                                       \
@@ -128,8 +127,8 @@
     "s_load_dwordx16 s[36:51], %[prims], s74\n\t"                                     \
     "s_add_u32 s77, s77, 1\n\t"                                                       \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
-    BIH_MT(MASK, ".LBIH_T" TAG "_%=")                                                 \
-    "s_or_b64 %[hits], %[hits], s[60:61]\n\t"                                         \
+    BIH_MT(".LBIH_T" TAG "_%=")                                                       \
+    "s_or_b64 %[hits], %[hits], exec\n\t"                                             \
     "s_branch .LBIH_T" TAG "_%=\n\t"                                                  \
     ".LBIH_T" TAG "E_%=:\n\t"
 
@@ -174,18 +173,19 @@
     "s_bfe_u32 s72, " Z ", 0x2001b\n\t"      /* axis */                               \
     "s_lshr_b32 s81, " Z ", 29\n\t"          /* leaf bits */                          \
     "s_mov_b32 s80, " W "\n\t"                                                        \
-    "v_cmp_eq_u32_e64 s[62:63], s72, 1\n\t"                                           \
-    "v_cmp_eq_u32_e64 s[68:69], s72, 2\n\t"                                           \
-    "v_cndmask_b32_e64 v24, %[ix], %[iy], s[62:63]\n\t"   /* inv = {ix,iy,iz}[axis] */ \
-    "v_cndmask_b32_e64 v24, v24, %[iz], s[68:69]\n\t"                                 \
+    "s_set_gpr_idx_on s72, gpr_idx(SRC0)\n\t"                                         \
+    "v_mov_b32_e32 v24, v62\n\t"            /* inv = {ix,iy,iz}[axis] (v62-v64) */    \
+    "s_set_gpr_idx_off\n\t"                                                          \
     "v_cmp_gt_f32_e64 s[58:59], 0, v24\n\t" /* this lane runs -axis: sign = inv < 0 */ \
     "v_mul_f32_e32 v25, " D0 ", v24\n\t"     /* t0 = (clip0 - O[axis]) * inv */       \
     "v_mul_f32_e32 v26, " D1 ", v24\n\t"     /* t1 */                                 \
     "s_lshl_b32 s74, s73, 4\n\t"                                                      \
     "s_load_dwordx8 s[84:91], %[nodes], s74\n\t"
 
-// Stack entry {lane lo/hi (sentinel outside MASK), node id split + NODE_OFS}.
+// Stack entry {lane lo/hi (sentinel outside MASK), node id split + NODE_OFS};
+// written on every lane (EXEC = all; the caller sets EXEC afterwards).
 #define BIH_PUSH(TAG, MASK, LO, HI, NODE_OFS)                                         \
+    "s_mov_b64 exec, -1\n\t"                                                          \
     "v_cndmask_b32_e64 v33, %[snan], " LO ", " MASK "\n\t"                            \
     "s_cmp_ge_u32 s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                  \
     "s_cbranch_scc1 .LBIH_SP" TAG "_%=\n\t"                                           \
@@ -212,9 +212,12 @@
 
 #define BIH_PACKET_WALK(ANY, CLR, ANY_TEXT, CNT_NODE, CNT_LEAF_L, CNT_LEAF_R, CNT_TRI_L, CNT_TRI_R) \
     "s_mov_b32 s79, m0\n\t"                                                           \
+    "v_mov_b32_e32 v62, %[ix]\n\t"                                                    \
+    "v_mov_b32_e32 v63, %[iy]\n\t"                                                    \
+    "v_mov_b32_e32 v64, %[iz]\n\t"                                                    \
     "s_mov_b32 s70, 0\n\t"                   /* root */                               \
     "s_mov_b32 s71, 0\n\t"                                                            \
-    "s_mov_b64 s[52:53], %[live]\n\t"                                                 \
+    "s_mov_b64 exec, %[live]\n\t"           /* EXEC = the node's active lanes */      \
     "s_mov_b64 %[hits], 0\n\t"                                                        \
     /* ---- record of node s70 from memory (root, pops) ---- */                       \
     ".LBIH_N_%=:\n\t"                                                                 \
@@ -234,12 +237,10 @@
     ".LBIH_NC_%=:\n\t"                                                                \
     "v_cndmask_b32_e64 v27, %[tmin], %[tmax], s[58:59]\n\t"   /* sL = neg ? tMax : tMin */ \
     "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
-    "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
-    "v_cmp_gt_f32_e64 s[56:57], v26, v28\n\t"                                         \
+    "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"   /* (compares give 0 off EXEC) */     \
+    "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL = (t0 > sL) ^ neg */  \
-    "s_and_b64 s[54:55], s[54:55], s[52:53]\n\t"                                      \
-    "s_xnor_b64 s[56:57], s[56:57], s[58:59]\n\t"         /* gR = !((t1 > sR) ^ neg) */ \
-    "s_and_b64 s[56:57], s[56:57], s[52:53]\n\t"                                      \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR = !(t1 > sR) ^ neg */ \
     "s_cmp_lg_u32 s81, 0\n\t"                                                         \
     "s_cbranch_scc1 .LBIH_L_%=\n\t"                                                   \
     /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
@@ -254,7 +255,7 @@
     "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
     BIH_PUSH("r", "s[56:57]", "v31", "v32", "1")                                      \
     ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
-    "s_mov_b64 s[52:53], s[54:55]\n\t"                                                \
+    "s_mov_b64 exec, s[54:55]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
     "v_cndmask_b32_e64 %[tmax], v25, %[tmax], s[58:59]\n\t" /*  neg ? tMax : t0]    */ \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
@@ -264,7 +265,7 @@
     "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
     BIH_PUSH("l", "s[54:55]", "v29", "v30", "0")                                      \
     ".LBIH_TR_%=:\n\t"                       /* take right: record in s[88:91] */     \
-    "s_mov_b64 s[52:53], s[56:57]\n\t"                                                \
+    "s_mov_b64 exec, s[56:57]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[58:59]\n\t" /* [neg ? tMin : t1,    */ \
     "v_cndmask_b32_e64 %[tmax], %[tmax], v26, s[58:59]\n\t" /*  neg ? t1 : tMax]    */ \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
@@ -279,6 +280,7 @@
     "s_cmp_eq_u32 s71, 0\n\t"                                                         \
     "s_cbranch_scc1 .LBIH_X_%=\n\t"                                                   \
     "s_sub_u32 s71, s71, 1\n\t"                                                       \
+    "s_mov_b64 exec, -1\n\t"                                                          \
     "s_cmp_ge_u32 s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                  \
     "s_cbranch_scc1 .LBIH_SQ_%=\n\t"                                                  \
     "s_set_gpr_idx_on s71, gpr_idx(SRC0)\n\t"                                         \
@@ -288,7 +290,7 @@
     ".LBIH_PQ_%=:\n\t"                                                                \
     "s_nop 0\n\t"                                                                     \
     "v_readlane_b32 s70, v39, s71\n\t"                                                \
-    "v_cmp_ne_u32_e64 s[52:53], %[snan], %[tmin]\n\t"                                 \
+    "v_cmpx_ne_u32_e32 vcc, %[snan], %[tmin]\n\t"  /* EXEC = the entry's lanes */      \
     ANY_TEXT                                                                          \
     "s_nop 1\n\t"                                                                     \
     "s_branch .LBIH_N_%=\n\t"                                                         \
@@ -333,6 +335,7 @@
     "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
     "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_X_%=:\n\t"                                                                 \
+    "s_mov_b64 exec, -1\n\t"               /* the statement runs on a full wave */    \
     "s_mov_b32 m0, s79"
 
 #define BIH_PACKET_CLOBBERS                                                           \
@@ -344,4 +347,4 @@
     "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
     "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", \
-    "v60", "v61", "vcc", "scc", "memory"
+    "v60", "v61", "v62", "v63", "v64", "vcc", "scc", "memory"
