@@ -139,7 +139,7 @@
     CNT_LEAF                                                                          \
     "s_bfe_u32 s75, s80, 0x2001b\n\t"        /* cntL, 0 = read dup_cnt */            \
     "s_cbranch_scc1 .LBIH_LC" TAG "_%=\n\t"                                           \
-    "s_lshl_b32 s76, s73, 2\n\t"                                                      \
+    "s_lshr_b32 s76, s73, 2\n\t"            /* split * 4 */                          \
     "s_load_dword s75, %[dupc], s76\n\t"                                              \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     ".LBIH_LC" TAG "_%=:\n\t"                                                         \
@@ -155,7 +155,7 @@
     CNT_LEAF                                                                          \
     "s_bfe_u32 s75, s80, 0x2001d\n\t"        /* cntR */                               \
     "s_cbranch_scc1 .LBIH_RC" TAG "_%=\n\t"                                           \
-    "s_lshl_b32 s76, s73, 2\n\t"                                                      \
+    "s_lshr_b32 s76, s73, 2\n\t"                                                      \
     "s_add_u32 s76, s76, 4\n\t"                                                       \
     "s_load_dword s75, %[dupc], s76\n\t"                                              \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
@@ -165,25 +165,38 @@
     BIH_TRIS("R" TAG, "s[66:67]", ANY("s[66:67]", ".LBIH_TR" TAG "E_%="), CNT_TRI)    \
     ".LBIH_RR" TAG "_%=:\n\t"
 
-// Consume the node record (d0 d1 z w in 4 SGPRs): split/axis/leaf bits/w,
-// the lane's inv and -axis mask (VALU), t0/t1; then request the children's
-// record pair into s[84:91] (the record's registers may be overwritten).
-#define BIH_NODE_REC(D0, D1, Z, W)                                                    \
-    "s_and_b32 s73, " Z ", 0x7ffffff\n\t"    /* split */                              \
-    "s_bfe_u32 s72, " Z ", 0x2001b\n\t"      /* axis */                               \
-    "s_lshr_b32 s81, " Z ", 29\n\t"          /* leaf bits */                          \
-    "s_mov_b32 s80, " W "\n\t"                                                        \
+// Consume the node record (d0 d1 z' w in 4 SGPRs, z' = split << 4 | leafR << 3
+// | leafL << 2 | axis): the lane's inv and -axis mask (VALU), t0/t1.
+#define BIH_NODE_REC(D0, D1, Z)                                                       \
+    "s_and_b32 s72, " Z ", 3\n\t"           /* axis */                               \
     "s_set_gpr_idx_on s72, gpr_idx(SRC0)\n\t"                                         \
     "v_mov_b32_e32 v24, v62\n\t"            /* inv = {ix,iy,iz}[axis] (v62-v64) */    \
     "s_set_gpr_idx_off\n\t"                                                          \
     "v_cmp_gt_f32_e64 s[58:59], 0, v24\n\t" /* this lane runs -axis: sign = inv < 0 */ \
     "v_mul_f32_e32 v25, " D0 ", v24\n\t"     /* t0 = (clip0 - O[axis]) * inv */       \
-    "v_mul_f32_e32 v26, " D1 ", v24\n\t"     /* t1 */                                 \
-    "s_lshl_b32 s74, s73, 4\n\t"                                                      \
-    "s_load_dwordx8 s[84:91], %[nodes], s74\n\t"
+    "v_mul_f32_e32 v26, " D1 ", v24\n\t"     /* t1 */
 
-// Stack entry {lane lo/hi (sentinel outside MASK), node id split + NODE_OFS};
-// written on every lane (EXEC = all; the caller sets EXEC afterwards).
+// Per-lane child decisions (EXEC = the node's lanes; compares give 0 off
+// EXEC), then: a leaf child -> LV<X> (w still in the record registers); two
+// internal children -> request their record pair into s[84:91] (the current
+// record's registers are free by then) and continue at D (TAIL).
+#define BIH_NODE_NC(Z, X, TAIL)                                                       \
+    "v_cndmask_b32_e64 v27, %[tmin], %[tmax], s[58:59]\n\t"   /* sL = neg ? tMax : tMin */ \
+    "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
+    "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
+    "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
+    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL = (t0 > sL) ^ neg */  \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR = !(t1 > sR) ^ neg */ \
+    "s_andn2_b32 s73, " Z ", 15\n\t"         /* byte offset of the children's pair */ \
+    "s_and_b32 s81, " Z ", 12\n\t"          /* leaf bits: 4 left, 8 right */          \
+    "s_cbranch_scc1 .LBIH_LV" X "_%=\n\t"                                              \
+    "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
+    TAIL
+
+// Stack entry {lane lo/hi (sentinel outside MASK), node = byte offset of its
+// record s73 + NODE_OFS}; written on every lane (EXEC = all; the caller sets
+// EXEC afterwards).  Deep slots go to the wave's spill area in the
+// out-of-line block BIH_PUSH_SPILL(TAG) emits.
 #define BIH_PUSH(TAG, MASK, LO, HI, NODE_OFS)                                         \
     "s_mov_b64 exec, -1\n\t"                                                          \
     "v_cndmask_b32_e64 v33, %[snan], " LO ", " MASK "\n\t"                            \
@@ -198,8 +211,9 @@
     "s_mov_b32 m0, s71\n\t"                                                           \
     "s_nop 0\n\t"                                                                     \
     "v_writelane_b32 v39, s74, m0\n\t"                                                \
-    "s_add_u32 s71, s71, 1\n\t"                                                       \
-    "s_branch .LBIH_PD" TAG "_%=\n\t"                                                 \
+    "s_add_u32 s71, s71, 1\n\t"
+
+#define BIH_PUSH_SPILL(TAG, HI)                                                       \
     ".LBIH_SP" TAG "_%=:\n\t"                /* deep slot: wave spill area */         \
     "s_sub_u32 s74, s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                \
     "s_lshl_b32 s74, s74, 9\n\t"                                                      \
@@ -207,8 +221,7 @@
     "global_store_dword v35, v33, %[spill]\n\t"                                       \
     "global_store_dword v35, " HI ", %[spill] offset:256\n\t"                         \
     "s_waitcnt vmcnt(0)\n\t"                                                          \
-    "s_branch .LBIH_PN" TAG "_%=\n\t"                                                 \
-    ".LBIH_PD" TAG "_%=:\n\t"
+    "s_branch .LBIH_PN" TAG "_%=\n\t"
 
 #define BIH_PACKET_WALK(ANY, CLR, ANY_TEXT, CNT_NODE, CNT_LEAF_L, CNT_LEAF_R, CNT_TRI_L, CNT_TRI_R) \
     "s_mov_b32 s79, m0\n\t"                                                           \
@@ -220,29 +233,19 @@
     "s_mov_b64 exec, %[live]\n\t"           /* EXEC = the node's active lanes */      \
     "s_mov_b64 %[hits], 0\n\t"                                                        \
     /* ---- record of node s70 from memory (root, pops) ---- */                       \
-    ".LBIH_N_%=:\n\t"                                                                 \
-    "s_lshl_b32 s74, s70, 4\n\t"                                                      \
-    "s_load_dwordx4 s[84:87], %[nodes], s74\n\t"                                      \
+    ".LBIH_N_%=:\n\t"                        /* s70 = the record's byte offset */      \
+    "s_load_dwordx4 s[84:87], %[nodes], s70\n\t"                                      \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     /* ---- node step, record in s[84:87] (left child / loaded) ---- */               \
     ".LBIH_NB0_%=:\n\t"                                                               \
     CNT_NODE                                                                          \
-    BIH_NODE_REC("s84", "s85", "s86", "s87")                                          \
-    "s_branch .LBIH_NC_%=\n\t"                                                        \
+    BIH_NODE_REC("s84", "s85", "s86")                                                 \
+    BIH_NODE_NC("s86", "0", "s_branch .LBIH_D_%=\n\t")                                \
     /* ---- node step, record in s[88:91] (right child) ---- */                       \
     ".LBIH_NB1_%=:\n\t"                                                               \
     CNT_NODE                                                                          \
-    BIH_NODE_REC("s88", "s89", "s90", "s91")                                          \
-    /* ---- per-lane child decisions ---- */                                          \
-    ".LBIH_NC_%=:\n\t"                                                                \
-    "v_cndmask_b32_e64 v27, %[tmin], %[tmax], s[58:59]\n\t"   /* sL = neg ? tMax : tMin */ \
-    "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
-    "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"   /* (compares give 0 off EXEC) */     \
-    "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
-    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL = (t0 > sL) ^ neg */  \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR = !(t1 > sR) ^ neg */ \
-    "s_cmp_lg_u32 s81, 0\n\t"                                                         \
-    "s_cbranch_scc1 .LBIH_L_%=\n\t"                                                   \
+    BIH_NODE_REC("s88", "s89", "s90")                                                 \
+    BIH_NODE_NC("s90", "1", "")                                                       \
     /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
     ".LBIH_D_%=:\n\t"                                                                 \
     "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
@@ -253,7 +256,7 @@
     "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
     "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
     "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
-    BIH_PUSH("r", "s[56:57]", "v31", "v32", "1")                                      \
+    BIH_PUSH("r", "s[56:57]", "v31", "v32", "16")                                     \
     ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
     "s_mov_b64 exec, s[54:55]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
@@ -303,11 +306,16 @@
     "s_waitcnt vmcnt(0)\n\t"                                                          \
     "s_branch .LBIH_PQ_%=\n\t"                                                        \
     /* ---- leaves of this node: test them (near first), then descend ---- */         \
+    ".LBIH_LV0_%=:\n\t"                                                               \
+    "s_mov_b32 s80, s87\n\t"                 /* w: mid | counts */                     \
+    "s_branch .LBIH_L_%=\n\t"                                                         \
+    ".LBIH_LV1_%=:\n\t"                                                               \
+    "s_mov_b32 s80, s91\n\t"                                                          \
     ".LBIH_L_%=:\n\t"                                                                 \
     "s_and_b32 s82, s80, 0x7ffffff\n\t"      /* mid */                                \
-    "s_cmp_eq_u32 s81, 1\n\t"                                                         \
+    "s_cmp_eq_u32 s81, 4\n\t"                                                         \
     "s_cbranch_scc1 .LBIH_L1_%=\n\t"                                                  \
-    "s_cmp_eq_u32 s81, 2\n\t"                                                         \
+    "s_cmp_eq_u32 s81, 8\n\t"                                                         \
     "s_cbranch_scc1 .LBIH_L2_%=\n\t"                                                  \
     "s_mov_b64 s[64:65], s[54:55]\n\t"       /* both children are leaves */           \
     "s_mov_b64 s[66:67], s[56:57]\n\t"                                                \
@@ -321,6 +329,7 @@
     BIH_LEAF_L("b", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_L1_%=:\n\t"                       /* left leaf, right internal */          \
+    "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
     "s_mov_b64 s[64:65], s[54:55]\n\t"                                                \
     BIH_LEAF_L("c", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     CLR("s[56:57]")                                                                   \
@@ -328,12 +337,15 @@
     "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
     "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_L2_%=:\n\t"                       /* right leaf, left internal */          \
+    "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
     "s_mov_b64 s[66:67], s[56:57]\n\t"                                                \
     BIH_LEAF_R("d", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \
     CLR("s[54:55]")                                                                   \
     "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
     "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
     "s_branch .LBIH_P_%=\n\t"                                                         \
+    BIH_PUSH_SPILL("r", "v32")                                                        \
+    BIH_PUSH_SPILL("l", "v30")                                                        \
     ".LBIH_X_%=:\n\t"                                                                 \
     "s_mov_b64 exec, -1\n\t"               /* the statement runs on a full wave */    \
     "s_mov_b32 m0, s79"

@@ -1086,9 +1086,8 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 ++pk[1];
 #endif
                 const su32x4 nd = nodes[cur];
-                const uint32_t ax = (nd.z >> 27) & 3u;
-                // axis 0/1/2 from bits 27 and 28 of z (uniform bit tests)
-                const float inv = (nd.z & (1u << 28)) ? iz : ((nd.z & (1u << 27)) ? iy : ix);
+                const uint32_t ax = nd.z & 3u;          // prim record layout (k_node_prim)
+                const float inv = ax == 2u ? iz : (ax == 1u ? iy : ix);
                 const bool neg = (sg >> ax) & 1u;
                 const float t0 = __uint_as_float(nd.x) * inv;
                 const float t1 = __uint_as_float(nd.y) * inv;
@@ -1097,8 +1096,8 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 unsigned long long gR = ~(__ballot(t1 > (neg ? tMin : tMax)) ^ mneg) & act;
                 const float lo_L = neg ? t0 : tMin, hi_L = neg ? tMax : t0;
                 const float lo_R = neg ? tMin : t1, hi_R = neg ? t1 : tMax;
-                const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
-                const uint32_t leaf = nd.z >> 29;         // bit 0: left is a leaf, bit 1: right
+                const uint32_t split = nd.z >> 4, mid = nd.w & kIdxMask;
+                const uint32_t leaf = (nd.z >> 2) & 3u;  // bit 0: left is a leaf, bit 1: right
                 const uint32_t nearL = (nearbits >> ax) & 1u;
                 if (leaf) {
                     const unsigned long long tL = (leaf & 1u) ? gL : 0ull;
@@ -1487,8 +1486,10 @@ __global__ void __launch_bounds__(kThreads) k_node_alive(const uint4 *__restrict
     if (!aL && !aR) node_alive[p] = 0;
 }
 
-// Camera-relative node records: {clip0 - O[axis], clip1 - O[axis], z, w}, and
-// the same records with every child subtree that no primary ray from O can
+// Camera-relative node records {clip0 - O[axis], clip1 - O[axis], z', w} with
+// z' = split << 4 | leafR << 3 | leafL << 2 | axis (split << 4: the byte
+// offset of the children's record pair; w as in the packed nodes), and the
+// same records with every child subtree that no primary ray from O can
 // hit (all its triangles dead, tri_alive) cut off: clip0 - O = -inf (left) /
 // clip1 - O = +inf (right) make t0 = -inf*inv / t1 = +inf*inv fail the
 // child's visit test (tMin < t[near], !(tMax < t[far])) for either ray
@@ -1506,10 +1507,11 @@ __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict_
     const uint4 nd = nodes[i];
     const uint32_t ax = (nd.z >> 27) & 3u;
     const float org = sel3(ax, ox, oy, oz);
-    uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
-                         __float_as_uint(__uint_as_float(nd.y) - org), nd.z, nd.w);
-    out[i] = r;
     const uint32_t split = nd.z & 0x7ffffffu;
+    const uint32_t z = (split << 4) | (((nd.z >> 30) & 1u) << 3) | (((nd.z >> 29) & 1u) << 2) | ax;
+    uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
+                         __float_as_uint(__uint_as_float(nd.y) - org), z, nd.w);
+    out[i] = r;
     const bool aL = ((nd.z >> 29) & 1u) ? leaf_alive[split] : node_alive[split];
     const bool aR = ((nd.z >> 30) & 1u) ? leaf_alive[split + 1] : node_alive[split + 1];
     if (!aL) r.x = 0xff800000u;   // -inf
