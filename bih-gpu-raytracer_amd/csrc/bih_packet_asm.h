@@ -64,6 +64,14 @@
 // Moeller-Trumbore of the record in s[36:51] for the lanes of EXEC; each
 // test narrows EXEC (v_cmpx), so the passing lanes end in EXEC; a uniform
 // miss jumps to NEXT.
+// Before the division, lanes whose u is certain to fail are dropped on the
+// numerator un = dot(s, p) alone: with det in (eps, inf) finite, 1/det and
+// un*(1/det) are each correctly rounded (relative error <= 2^-24), so
+//   un < -det*2^-20     gives u <= (un/det)(1 - 2^-23) < -2^-21: u < 0;
+//   un > det*(1+2^-20)  (the bound itself rounded by <= 2^-24) gives
+//                       u >= (1+2^-20)(1-2^-24)^3 > 1: u > 1;
+// det*2^-20 is exact (det > eps, no underflow); det = inf or NaN and un =
+// NaN compare false and keep the lane.  The lanes kept run the exact test.
 // Operand order of every f32 op follows prim_hits (bih_render.hip):
 // record = {e1 s36-38, e2 s39-41, s = O - v0 s42-44, q s45-47, tnum s48}.
 #define BIH_MT(NEXT)                                                                  \
@@ -83,6 +91,18 @@
     "v_add_f32_e32 v38, v33, v34\n\t"                                                 \
     "v_cmpx_nge_f32_e32 vcc, %[eps], v38\n\t"   /* !(det <= eps): NaN passes */        \
     "s_cbranch_execz " NEXT "\n\t"                                                    \
+    "v_mul_f32_e32 v33, s42, v35\n\t"        /* un = (sx*px + sy*py) + sz*pz */        \
+    "v_mul_f32_e32 v34, s43, v36\n\t"                                                 \
+    "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
+    "v_mul_f32_e32 v34, s44, v37\n\t"                                                 \
+    "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
+    /* division-free pre-test (see BIH_MT's comment): drop lanes with */              \
+    /* un < -det*2^-20 (u < 0) or un > det*(1+2^-20) (u > 1) */                      \
+    "v_mul_f32_e32 v34, 0x35800000, v38\n\t"                                          \
+    "v_cmpx_nlt_f32_e64 s[62:63], v33, -v34\n\t"                                      \
+    "v_mul_f32_e32 v34, 0x3f800008, v38\n\t"                                          \
+    "v_cmpx_ngt_f32_e32 vcc, v33, v34\n\t"                                            \
+    "s_cbranch_execz " NEXT "\n\t"                                                    \
     "v_div_scale_f32 v27, s[62:63], v38, v38, 1.0\n\t"   /* 1/det, IEEE (hipcc's */  \
     "v_rcp_f32_e32 v28, v27\n\t"                         /* own sequence; keeps  */  \
     "v_div_scale_f32 v29, vcc, 1.0, v38, 1.0\n\t"         /* t0/t1 in v25/v26)    */  \
@@ -94,12 +114,7 @@
     "v_fma_f32 v27, -v27, v30, v29\n\t"                                               \
     "v_div_fmas_f32 v27, v27, v28, v30\n\t"                                           \
     "v_div_fixup_f32 v38, v27, v38, 1.0\n\t"                                          \
-    "v_mul_f32_e32 v33, s42, v35\n\t"        /* u = ((sx*px + sy*py) + sz*pz)*inv */  \
-    "v_mul_f32_e32 v34, s43, v36\n\t"                                                 \
-    "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
-    "v_mul_f32_e32 v34, s44, v37\n\t"                                                 \
-    "v_add_f32_e32 v33, v33, v34\n\t"                                                 \
-    "v_mul_f32_e32 v35, v33, v38\n\t"                                                 \
+    "v_mul_f32_e32 v35, v33, v38\n\t"        /* u = un * inv */                       \
     "v_cmpx_ngt_f32_e32 vcc, 0, v35\n\t"           /* !(u < 0 || u > 1) */            \
     "v_cmpx_nlt_f32_e32 vcc, 1.0, v35\n\t"                                            \
     "s_cbranch_execz " NEXT "\n\t"                                                    \
