@@ -131,21 +131,32 @@
     "v_cmpx_lt_f32_e32 vcc, 0, v37\n\t"            /* t > 0 && t < FLT_MAX */         \
     "v_cmpx_gt_f32_e32 vcc, %[fmax], v37\n\t"
 
-// Triangles [s77, s78) for the lanes of MASK (EXEC per triangle).
-#define BIH_TRIS(TAG, MASK, ANY_MASK, CNT_TRI)                                        \
+// Triangles [s77, s78), at least one, for the lanes of the leaf's mask
+// (ANY_MASK sets EXEC per triangle).
+#define BIH_TRIS(TAG, ANY_MASK, CNT_TRI)                                              \
     ".LBIH_T" TAG "_%=:\n\t"                                                          \
-    "s_cmp_ge_u32 s77, s78\n\t"                                                       \
-    "s_cbranch_scc1 .LBIH_T" TAG "E_%=\n\t"                                           \
     ANY_MASK                                                                          \
     CNT_TRI                                                                           \
     "s_lshl_b32 s74, s77, 6\n\t"                                                      \
     "s_load_dwordx16 s[36:51], %[prims], s74\n\t"                                     \
     "s_add_u32 s77, s77, 1\n\t"                                                       \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
-    BIH_MT(".LBIH_T" TAG "_%=")                                                       \
+    BIH_MT(".LBIH_TN" TAG "_%=")                                                      \
     "s_or_b64 %[hits], %[hits], exec\n\t"                                             \
-    "s_branch .LBIH_T" TAG "_%=\n\t"                                                  \
+    ".LBIH_TN" TAG "_%=:\n\t"                                                         \
+    "s_cmp_lt_u32 s77, s78\n\t"                                                       \
+    "s_cbranch_scc1 .LBIH_T" TAG "_%=\n\t"                                            \
     ".LBIH_T" TAG "E_%=:\n\t"
+
+// The one triangle at byte offset s74 (a leaf of count code 1, most leaves).
+#define BIH_TRI1(ANY_MASK, CNT_TRI, EXIT)                                             \
+    ANY_MASK                                                                          \
+    CNT_TRI                                                                           \
+    "s_load_dwordx16 s[36:51], %[prims], s74\n\t"                                     \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
+    BIH_MT(EXIT)                                                                      \
+    "s_or_b64 %[hits], %[hits], exec\n\t"                                             \
+    "s_branch " EXIT "\n\t"
 
 // Left leaf (triangles [mid - cL, mid), leaf index split) for s[64:65].
 #define BIH_LEAF_L(TAG, ANY, CNT_LEAF, CNT_TRI)                                       \
@@ -153,14 +164,20 @@
     "s_cbranch_scc1 .LBIH_LL" TAG "_%=\n\t"                                           \
     CNT_LEAF                                                                          \
     "s_bfe_u32 s75, s80, 0x2001b\n\t"        /* cntL, 0 = read dup_cnt */            \
-    "s_cbranch_scc1 .LBIH_LC" TAG "_%=\n\t"                                           \
+    "s_cbranch_scc0 .LBIH_LD" TAG "_%=\n\t"                                           \
+    "s_cmp_eq_u32 s75, 1\n\t"                                                         \
+    "s_cbranch_scc0 .LBIH_LC" TAG "_%=\n\t"                                           \
+    "s_lshl_b32 s74, s82, 6\n\t"            /* triangle mid - 1 */                   \
+    "s_sub_u32 s74, s74, 64\n\t"                                                      \
+    BIH_TRI1(ANY("s[64:65]", ".LBIH_LL" TAG "_%="), CNT_TRI, ".LBIH_LL" TAG "_%=")     \
+    ".LBIH_LD" TAG "_%=:\n\t"                                                         \
     "s_lshr_b32 s76, s73, 2\n\t"            /* split * 4 */                          \
     "s_load_dword s75, %[dupc], s76\n\t"                                              \
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     ".LBIH_LC" TAG "_%=:\n\t"                                                         \
     "s_sub_u32 s77, s82, s75\n\t"                                                     \
     "s_mov_b32 s78, s82\n\t"                                                          \
-    BIH_TRIS("L" TAG, "s[64:65]", ANY("s[64:65]", ".LBIH_TL" TAG "E_%="), CNT_TRI)    \
+    BIH_TRIS("L" TAG, ANY("s[64:65]", ".LBIH_TL" TAG "E_%="), CNT_TRI)                \
     ".LBIH_LL" TAG "_%=:\n\t"
 
 // Right leaf (triangles [mid, mid + cR), leaf index split + 1) for s[66:67].
@@ -169,7 +186,12 @@
     "s_cbranch_scc1 .LBIH_RR" TAG "_%=\n\t"                                           \
     CNT_LEAF                                                                          \
     "s_bfe_u32 s75, s80, 0x2001d\n\t"        /* cntR */                               \
-    "s_cbranch_scc1 .LBIH_RC" TAG "_%=\n\t"                                           \
+    "s_cbranch_scc0 .LBIH_RD" TAG "_%=\n\t"                                           \
+    "s_cmp_eq_u32 s75, 1\n\t"                                                         \
+    "s_cbranch_scc0 .LBIH_RC" TAG "_%=\n\t"                                           \
+    "s_lshl_b32 s74, s82, 6\n\t"            /* triangle mid */                       \
+    BIH_TRI1(ANY("s[66:67]", ".LBIH_RR" TAG "_%="), CNT_TRI, ".LBIH_RR" TAG "_%=")     \
+    ".LBIH_RD" TAG "_%=:\n\t"                                                         \
     "s_lshr_b32 s76, s73, 2\n\t"                                                      \
     "s_add_u32 s76, s76, 4\n\t"                                                       \
     "s_load_dword s75, %[dupc], s76\n\t"                                              \
@@ -177,7 +199,7 @@
     ".LBIH_RC" TAG "_%=:\n\t"                                                         \
     "s_mov_b32 s77, s82\n\t"                                                          \
     "s_add_u32 s78, s82, s75\n\t"                                                     \
-    BIH_TRIS("R" TAG, "s[66:67]", ANY("s[66:67]", ".LBIH_TR" TAG "E_%="), CNT_TRI)    \
+    BIH_TRIS("R" TAG, ANY("s[66:67]", ".LBIH_TR" TAG "E_%="), CNT_TRI)                \
     ".LBIH_RR" TAG "_%=:\n\t"
 
 // Consume the node record (d0 d1 z' w in 4 SGPRs, z' = split << 4 | leafR << 3
@@ -200,12 +222,12 @@
     "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
     "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
     "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
-    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL = (t0 > sL) ^ neg */  \
     "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR = !(t1 > sR) ^ neg */ \
     "s_andn2_b32 s73, " Z ", 15\n\t"         /* byte offset of the children's pair */ \
     "s_and_b32 s81, " Z ", 12\n\t"          /* leaf bits: 4 left, 8 right */          \
     "s_cbranch_scc1 .LBIH_LV" X "_%=\n\t"                                              \
     "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
+    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"  /* gL = (t0 > sL) ^ neg; SCC = gL != 0 */ \
     TAIL
 
 // Stack entry {lane lo/hi (sentinel outside MASK), node = byte offset of its
@@ -262,8 +284,7 @@
     BIH_NODE_REC("s88", "s89", "s90")                                                 \
     BIH_NODE_NC("s90", "1", "")                                                       \
     /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
-    ".LBIH_D_%=:\n\t"                                                                 \
-    "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
+    ".LBIH_D_%=:\n\t"                        /* SCC = (gL != 0) */                     \
     "s_cbranch_scc0 .LBIH_DN_%=\n\t"                                                  \
     "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
     "s_cbranch_scc0 .LBIH_TL_%=\n\t"         /* only the left child */                \
@@ -322,9 +343,11 @@
     "s_branch .LBIH_PQ_%=\n\t"                                                        \
     /* ---- leaves of this node: test them (near first), then descend ---- */         \
     ".LBIH_LV0_%=:\n\t"                                                               \
+    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL */                    \
     "s_mov_b32 s80, s87\n\t"                 /* w: mid | counts */                     \
     "s_branch .LBIH_L_%=\n\t"                                                         \
     ".LBIH_LV1_%=:\n\t"                                                               \
+    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"                                      \
     "s_mov_b32 s80, s91\n\t"                                                          \
     ".LBIH_L_%=:\n\t"                                                                 \
     "s_and_b32 s82, s80, 0x7ffffff\n\t"      /* mid */                                \
