@@ -14,6 +14,7 @@ Everything runs through libbih_amd.so (HIP, gfx950); there is no CPU path.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -151,6 +152,34 @@ class Renderer:
         return ms.value
 
 
+def load_obj(path: str) -> np.ndarray:
+    """Wavefront OBJ -> float32 (n, 9) soup in file order (bih_scene_load_obj;
+    Model::LoadModel + App::LoadModels flattening, Model.cpp:10-95,
+    App.cpp:65-121).  Raises BihError (BIH_ERR_IO / BIH_ERR_PARSE with the line)."""
+    sc = Scene()
+    line = C.c_uint32(0)
+    rc = load().bih_scene_load_obj(os.fsencode(path), C.byref(sc), C.byref(line))
+    if rc != _lib.BIH_OK:
+        raise BihError(rc, f"bih_scene_load_obj({path!r})" + (f" line {line.value}" if line.value else ""))
+    try:
+        if sc.n_tris == 0:
+            return np.zeros((0, 9), np.float32)
+        return np.ctypeslib.as_array(C.cast(sc.v, C.POINTER(C.c_float)), (sc.n_tris, 9)).copy()
+    finally:
+        load().bih_scene_free(C.byref(sc))
+
+
+class Model:
+    """Model(path) (Model.h / Model.cpp:6-8): the triangles of one OBJ file."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.triangles = load_obj(path)
+
+    def __len__(self):
+        return self.triangles.shape[0]
+
+
 def unpack_rgba(img: np.ndarray) -> np.ndarray:
     """0x00BBGGRR -> (..., 4) uint8 RGBA (alpha byte as stored, 0)."""
     return img.astype("<u4").view(np.uint8).reshape(img.shape + (4,))
@@ -165,6 +194,6 @@ def write_ppm(path: str, img: np.ndarray):
         f.write(np.ascontiguousarray(rgb).tobytes())
 
 
-__all__ = ["GPUArrayManager", "Renderer", "Camera", "Rows", "BihError", "camera_reference",
+__all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
            "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
            "TRAVERSE_REFERENCE"]

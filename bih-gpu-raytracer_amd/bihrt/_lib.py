@@ -19,6 +19,7 @@ BIH_OK = 0
 ERRORS = {
     -1: "BIH_ERR_INVALID", -2: "BIH_ERR_NO_DEVICE", -3: "BIH_ERR_HIP", -4: "BIH_ERR_OOM",
     -5: "BIH_ERR_NONFINITE", -6: "BIH_ERR_TOO_LARGE", -7: "BIH_ERR_MISMATCH",
+    -8: "BIH_ERR_IO", -9: "BIH_ERR_PARSE",
 }
 TRAVERSE_ANYHIT, TRAVERSE_REFERENCE = 0, 1
 (ARR_MORTON_SORTED, ARR_TRI_INDEX, ARR_UNIQUE_MC, ARR_DUP_COUNT, ARR_FIRST_IDX, ARR_LEAF_PARENT,
@@ -102,6 +103,9 @@ def load():
     L.bih_strerror.argtypes = [i32]
     L.bih_strerror.restype = C.c_char_p
     L.bih_camera_reference.argtypes = [u32, u32, C.POINTER(Camera)]
+    L.bih_scene_load_obj.argtypes = [C.c_char_p, C.POINTER(Scene), C.POINTER(u32)]
+    L.bih_scene_free.argtypes = [C.POINTER(Scene)]
+    L.bih_scene_free.restype = None
     L.bih_build.argtypes = [C.POINTER(Scene), i32, C.POINTER(vp)]
     L.bih_build_device.argtypes = [vp, u32, i32, vp, C.POINTER(vp)]
     L.bih_rebuild.argtypes = [vp]
@@ -116,7 +120,7 @@ def load():
                                     C.POINTER(Rows), u32, vp, vp, vp]
     L.bih_sync.argtypes = [vp, vp]
     L.bih_last_render_ms.argtypes = [vp, C.POINTER(C.c_double)]
-    for name in ("bih_camera_reference", "bih_build", "bih_build_device", "bih_rebuild",
+    for name in ("bih_camera_reference", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
                  "bih_render_device", "bih_sync", "bih_last_render_ms"):
         getattr(L, name).restype = i32

@@ -175,3 +175,24 @@ def _dodeca_faces(V):
                 out.append([int(x) for x in on[np.argsort(ang)]])
     assert len(out) == 12, len(out)
     return out
+
+
+def write_obj(path: str, tris: np.ndarray, shared: bool = False):
+    """Writes a soup as Wavefront OBJ (numpy's shortest round-trip float32
+    repr per coordinate).  shared=False: three `v` lines + one `f` per triangle;
+    shared=True: identical vertices are written once and referenced by index."""
+    tris = np.asarray(tris, np.float32).reshape(-1, 3, 3)
+    with open(path, "w") as f:
+        f.write(f"# {tris.shape[0]} triangles\no soup\n")
+        if not shared:
+            for t in tris:
+                for p in t:
+                    f.write("v %s %s %s\n" % tuple(str(x) for x in p))
+            for i in range(tris.shape[0]):
+                f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+            return
+        verts, idx = np.unique(tris.reshape(-1, 3).view(np.uint32), axis=0, return_inverse=True)
+        for p in verts.view(np.float32):
+            f.write("v %s %s %s\n" % tuple(str(x) for x in p))
+        for t in idx.reshape(-1, 3):
+            f.write("f %d %d %d\n" % tuple(int(k) + 1 for k in t))

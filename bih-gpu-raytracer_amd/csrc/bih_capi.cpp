@@ -158,6 +158,8 @@ const char *bih_strerror(int code) {
     case BIH_ERR_NONFINITE: return "scene holds a non-finite coordinate";
     case BIH_ERR_TOO_LARGE: return "too many triangles";
     case BIH_ERR_MISMATCH: return "scene does not match the tree";
+    case BIH_ERR_IO: return "file could not be opened or read";
+    case BIH_ERR_PARSE: return "malformed scene file";
     default: return "unknown error";
     }
 }

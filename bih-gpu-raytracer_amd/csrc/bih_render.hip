@@ -355,8 +355,8 @@ struct Walker {
         const bool push = goN && !B && !leafF;               // both internal: stack far
         // leaf ranges, computed unconditionally: left [mid-cL, mid), right [mid, mid+cR)
         uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
-        const bool escL = testN | testF ? (leafL && cL == 0) : false;   // count > 3
-        const bool escR = testN | testF ? (leafR && cR == 0) : false;
+        const bool escL = (testN | testF) ? (leafL && cL == 0) : false;   // count > 3
+        const bool escR = (testN | testF) ? (leafR && cR == 0) : false;
         if (__builtin_expect(__any(escL | escR), 0)) {
             if (escL) cL = s.dup_cnt[split];
             if (escR) cR = s.dup_cnt[split + 1];

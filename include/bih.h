@@ -45,6 +45,8 @@ extern "C" {
 #define BIH_ERR_NONFINITE   -5   /* scene holds a NaN/Inf coordinate         */
 #define BIH_ERR_TOO_LARGE   -6   /* more than BIH_MAX_TRIS triangles         */
 #define BIH_ERR_MISMATCH    -7   /* scene does not belong to this tree       */
+#define BIH_ERR_IO          -8   /* file could not be opened / read          */
+#define BIH_ERR_PARSE       -9   /* malformed scene file                     */
 
 #define BIH_MAX_TRIS (1u << 27)
 
@@ -121,6 +123,15 @@ const char *bih_strerror(int code);
 int bih_abi_version(void);
 
 int bih_camera_reference(uint32_t w, uint32_t h, bih_camera *out);
+
+/* Scene ingestion (host only, no device): a Wavefront OBJ file flattened to a
+ * triangle soup in file order, replacing Model::LoadModel's assimp import
+ * (src/Model.cpp:10-95, aiProcess_Triangulate) and the mesh -> triangle walk
+ * of App::LoadModels (src/App.cpp:65-121).  On success out->v is allocated by
+ * the library (free it with bih_scene_free); on BIH_ERR_PARSE *err_line (may
+ * be NULL) holds the 1-based offending line. */
+int bih_scene_load_obj(const char *path, bih_scene *out, uint32_t *err_line);
+void bih_scene_free(bih_scene *scene);
 
 /* Build from a host soup (copied H2D) or a device-resident soup. */
 int bih_build(const bih_scene *scene, int device, bih_tree **out);
