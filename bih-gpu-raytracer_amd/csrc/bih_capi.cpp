@@ -515,6 +515,10 @@ int bih_sync(const bih_tree *tr, void *stream) {
             for (int k = 0; k < 32; ++k) fprintf(stderr, " %u", c[24 + k]);
             fprintf(stderr, " mt");
             for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[56 + k]);
+            fprintf(stderr, " lanes-node(log2)");
+            for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[bih::kHistWord + k]);
+            fprintf(stderr, " lanes-tri(log2)");
+            for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[bih::kHistWord + 8 + k]);
             fprintf(stderr, "\n");
         }
     }

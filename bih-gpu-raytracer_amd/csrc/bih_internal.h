@@ -37,7 +37,8 @@ constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bi
 constexpr int kLdsStack = BIH_LDS_STACK;
 // work buffer: [0..8) chunk counters (one per image band / XCD); [16..56) walk
 // counters of BIH_PACKET_COUNTERS builds; [64..2112) per-CU tile slots (u64)
-constexpr uint32_t kWorkWords = 64 + 2 * 1024;
+constexpr uint32_t kWorkWords = 64 + 2 * 1024 + 16;   // + active-lane histograms (counter builds)
+constexpr uint32_t kHistWord = 64 + 2 * 1024;
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif

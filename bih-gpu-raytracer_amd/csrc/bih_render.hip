@@ -1062,6 +1062,7 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 }
 #if BIH_PACKET_COUNTERS
                 ++pk[3];
+                if (lane == 0) atomicAdd(a.work + kHistWord + 8 + (31 - __builtin_clz(__popcll(m))), 1u);
 #endif
                 if (STATS && (m & me)) ++c_tris;
 #if BIH_PACKET_COUNTERS
@@ -1084,6 +1085,7 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 if (STATS && (act & me)) ++c_nodes;
 #if BIH_PACKET_COUNTERS
                 ++pk[1];
+                if (lane == 0) atomicAdd(a.work + kHistWord + (31 - __builtin_clz(__popcll(act))), 1u);
 #endif
                 const su32x4 nd = nodes[cur];
                 const uint32_t ax = nd.z & 3u;          // prim record layout (k_node_prim)
