@@ -53,6 +53,11 @@ struct bih_tree {
     uint32_t *work = nullptr;        // persistent-kernel tile counters, kWorkWords per slot
     uint32_t *spill = nullptr;       // traversal stack spill area, spill_words per slot
     size_t spill_per_slot = 0;       // u32
+    // cost-ordered tile queue: per slot {cost, order} of chunk_cap u32 each;
+    // the cost a render accumulates orders the next render of the same slot
+    uint32_t *chunk_buf = nullptr;
+    size_t chunk_cap = 0;
+    uint32_t chunk_key[kSlots][6] = {};
     float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
@@ -94,6 +99,54 @@ int wait_renders(bih_tree *tr, hipStream_t st) {
             hipError_t e = hipStreamWaitEvent(st, tr->ev1[k], 0);
             if (e != hipSuccess) return map_hip((int)e);
         }
+    return BIH_OK;
+}
+
+// Cost-ordered tile queue of the packet kernel (bih::launch_chunk_order):
+// the chunks of this render start in descending order of the cycles they
+// took in the last render of the same slot and geometry (frame f - kSlots in
+// a frame sequence), so the slow part of the image starts first and the frame
+// does not end on one long packet.  The order never changes a pixel.
+// Called after `st` waits for the slot's previous render.  BIH_CHUNK_ORDER=0
+// turns it off (tuning / A-B).
+int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &rows, int slot,
+                        hipStream_t st, bih::RenderArgs &a) {
+    static const bool enabled = [] {
+        const char *e = getenv("BIH_CHUNK_ORDER");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    a.chunk_order = nullptr;
+    a.chunk_cost = nullptr;
+    uint32_t cx = 0;
+    const uint32_t n = bih::chunk_count(w, rows.nrows, spp, &cx);
+    if (!enabled || n == 0) return BIH_OK;
+    if (tr->chunk_cap < n) {
+        // every render that may still use the old buffers has finished
+        for (int k = 0; k < kSlots; ++k)
+            if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+        if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
+        tr->chunk_buf = nullptr;
+        tr->chunk_cap = 0;
+        hipError_t e = hipMalloc((void **)&tr->chunk_buf, (size_t)kSlots * 2 * n * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->chunk_cap = n;
+        memset(tr->chunk_key, 0, sizeof tr->chunk_key);
+    }
+    uint32_t *cost = tr->chunk_buf + (size_t)slot * 2 * tr->chunk_cap;
+    uint32_t *order = cost + tr->chunk_cap;
+    const uint32_t key[6] = {w, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step};
+    hipError_t e = hipSuccess;
+    if (memcmp(key, tr->chunk_key[slot], sizeof key) != 0) {
+        e = hipMemsetAsync(cost, 0, n * sizeof(uint32_t), st);   // no history: identity order
+        if (e != hipSuccess) return map_hip((int)e);
+        memcpy(tr->chunk_key[slot], key, sizeof key);
+    }
+    int le = bih::launch_chunk_order(cost, cx, n, order, st);
+    if (le) return map_hip(le);
+    e = hipMemsetAsync(cost, 0, n * sizeof(uint32_t), st);
+    if (e != hipSuccess) return map_hip((int)e);
+    a.chunk_order = order;
+    a.chunk_cost = cost;
     return BIH_OK;
 }
 
@@ -253,6 +306,7 @@ void bih_free(bih_tree *tr) {
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
     if (tr->spill) (void)hipFree(tr->spill);
+    if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
     if (tr->prim) (void)hipFree(tr->prim);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
@@ -463,6 +517,8 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         }
     }
     bih::RenderArgs a;
+    rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
+    if (rc) return rc;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;
@@ -476,6 +532,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.d_base = d0 + (uint32_t)((uint64_t)2 * spp * frame) * 362437u;
     a.hdr = tr->t.hdr;
     a.hdr_n_tris = tr->t.n;
+    a.n_nodes = n_int;
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
     a.tri_prim = tr->prim;
@@ -519,7 +576,11 @@ int bih_sync(const bih_tree *tr, void *stream) {
             for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[bih::kHistWord + k]);
             fprintf(stderr, " lanes-tri(log2)");
             for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", c[bih::kHistWord + 8 + k]);
-            fprintf(stderr, "\n");
+            fprintf(stderr, "\npackets by log2(node steps): bin count nodes tris\n");
+            for (int k = 0; k < 16; ++k)
+                if (c[bih::kHistWord + 16 + k])
+                    fprintf(stderr, "  %2d %8u %10u %10u\n", k, c[bih::kHistWord + 16 + k],
+                            c[bih::kHistWord + 32 + k], c[bih::kHistWord + 48 + k]);
         }
     }
 #endif

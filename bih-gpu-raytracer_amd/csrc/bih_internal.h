@@ -37,7 +37,7 @@ constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bi
 constexpr int kLdsStack = BIH_LDS_STACK;
 // work buffer: [0..8) chunk counters (one per image band / XCD); [16..56) walk
 // counters of BIH_PACKET_COUNTERS builds; [64..2112) per-CU tile slots (u64)
-constexpr uint32_t kWorkWords = 64 + 2 * 1024 + 16;   // + active-lane histograms (counter builds)
+constexpr uint32_t kWorkWords = 64 + 2 * 1024 + 64;   // + histograms (counter builds)
 constexpr uint32_t kHistWord = 64 + 2 * 1024;
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
@@ -62,6 +62,7 @@ struct RenderArgs {
     uint32_t row0, nrows, band_h, band_step;
     uint32_t d_base;        // XORWOW Weyl counter at the start of this frame
     uint32_t hdr_n_tris;    // host copy of hdr->n_tris (kernel choice)
+    uint32_t n_nodes = 0;   // host copy of U-1, the internal nodes (kernel choice)
     const TreeHeader *hdr;
     const uint4 *nodes;
     const float *tris;
@@ -75,6 +76,8 @@ struct RenderArgs {
     uint32_t *ray_stats;    // optional 3 u32 per ray {nodes, leaves, tris}
     uint32_t *work;         // tile counter of the persistent kernel (zeroed per launch)
     uint32_t *spill;        // per-lane stack spill area (spill_words(grid) u32)
+    const uint32_t *chunk_order = nullptr;  // packet kernel: chunk permutation (launch_chunk_order)
+    uint32_t *chunk_cost = nullptr;         // packet kernel: per-chunk cycle accumulator (zeroed)
 };
 
 // Device buffers of one tree.
@@ -119,6 +122,11 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);
+// chunks of the packet kernel's tile queue for a w x nrows launch (0: no packet kernel)
+uint32_t chunk_count(uint32_t w, uint32_t nrows, uint32_t spp, uint32_t *chunks_x);
+// order[] = the chunks of every band by descending cost[] (k_chunk_order)
+int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks, uint32_t *order,
+                       void *stream);
 // primary-ray records for camera origin `origin`: n triangle records
 // (16 f32, k_tri_prim), then m = U-1 node records (u32x4, k_node_prim) + 1
 // pad, then the same m + 1 records with unhittable subtrees cut off, then

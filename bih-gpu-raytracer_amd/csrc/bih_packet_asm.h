@@ -24,7 +24,8 @@
 //   s[36:51] triangle record          EXEC = the active lanes   s[54:55] gL
 //   s[56:57] gR       s[58:59] lanes running -axis     s[60:61] tmp / hit mask
 //   s[62:63] tmp      s[64:65] left-leaf lanes         s[66:67] right-leaf lanes
-//   s[68:69] tmp      s70 cur (pop)  s71 sp  s72 axis  s73 split  s74-s76 tmp
+//   s[68:69] tmp      s70 cur (pop)  s71 sp  s73 pair offset  s74-s76 tmp
+//   M0[7:0] the node's axis (s_set_gpr_idx_on) until a push
 //   s77 b  s78 e  s79 saved m0  s80 w (mid | counts)  s81 leaf bits  s82 mid
 //   s[84:91] record pair (prefetch)
 //   v62-v64 {ix, iy, iz} (inv = v[62 + axis], gpr-indexed)
@@ -202,11 +203,13 @@
     BIH_TRIS("R" TAG, ANY("s[66:67]", ".LBIH_TR" TAG "E_%="), CNT_TRI)                \
     ".LBIH_RR" TAG "_%=:\n\t"
 
-// Consume the node record (d0 d1 z' w in 4 SGPRs, z' = split << 4 | leafR << 3
-// | leafL << 2 | axis): the lane's inv and -axis mask (VALU), t0/t1.
+// Consume the node record (d0 d1 z w in 4 SGPRs, z = split << 8 | axis, w =
+// mid | leafL << 26 | cntL << 27 | cntR << 29 | leafR << 31): the lane's inv
+// and -axis mask (VALU), t0/t1.  s_set_gpr_idx_on takes the index from z's
+// low byte (= axis) and leaves it in M0[7:0], where the near-order tests of
+// this node read it (bit M0[4:0] of %[near]) until a push rewrites M0.
 #define BIH_NODE_REC(D0, D1, Z)                                                       \
-    "s_and_b32 s72, " Z ", 3\n\t"           /* axis */                               \
-    "s_set_gpr_idx_on s72, gpr_idx(SRC0)\n\t"                                         \
+    "s_set_gpr_idx_on " Z ", gpr_idx(SRC0)\n\t"                                       \
     "v_mov_b32_e32 v24, v62\n\t"            /* inv = {ix,iy,iz}[axis] (v62-v64) */    \
     "s_set_gpr_idx_off\n\t"                                                          \
     "v_cmp_gt_f32_e64 s[58:59], 0, v24\n\t" /* this lane runs -axis: sign = inv < 0 */ \
@@ -216,15 +219,17 @@
 // Per-lane child decisions (EXEC = the node's lanes; compares give 0 off
 // EXEC), then: a leaf child -> LV<X> (w still in the record registers); two
 // internal children -> request their record pair into s[84:91] (the current
-// record's registers are free by then) and continue at D (TAIL).
-#define BIH_NODE_NC(Z, X, TAIL)                                                       \
+// record's registers are free by then) and continue at D (TAIL).  s[54:55] /
+// s[56:57] leave here as the raw compares; gL = s[54:55] ^ neg is formed
+// before D (SCC = gL != 0), gR = s[56:57] ^ neg where it is first tested (its
+// SCC then replaces a compare with 0).
+#define BIH_NODE_NC(Z, W, X, TAIL)                                                    \
     "v_cndmask_b32_e64 v27, %[tmin], %[tmax], s[58:59]\n\t"   /* sL = neg ? tMax : tMin */ \
     "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
     "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
     "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR = !(t1 > sR) ^ neg */ \
-    "s_andn2_b32 s73, " Z ", 15\n\t"         /* byte offset of the children's pair */ \
-    "s_and_b32 s81, " Z ", 12\n\t"          /* leaf bits: 4 left, 8 right */          \
+    "s_lshr_b32 s73, " Z ", 4\n\t"           /* byte offset of the children's pair */ \
+    "s_and_b32 s81, " W ", 0x84000000\n\t"  /* leaf bits: 1<<26 left, 1<<31 right */  \
     "s_cbranch_scc1 .LBIH_LV" X "_%=\n\t"                                              \
     "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"  /* gL = (t0 > sL) ^ neg; SCC = gL != 0 */ \
@@ -277,18 +282,18 @@
     ".LBIH_NB0_%=:\n\t"                                                               \
     CNT_NODE                                                                          \
     BIH_NODE_REC("s84", "s85", "s86")                                                 \
-    BIH_NODE_NC("s86", "0", "s_branch .LBIH_D_%=\n\t")                                \
+    BIH_NODE_NC("s86", "s87", "0", "s_branch .LBIH_D_%=\n\t")                         \
     /* ---- node step, record in s[88:91] (right child) ---- */                       \
     ".LBIH_NB1_%=:\n\t"                                                               \
     CNT_NODE                                                                          \
     BIH_NODE_REC("s88", "s89", "s90")                                                 \
-    BIH_NODE_NC("s90", "1", "")                                                       \
+    BIH_NODE_NC("s90", "s91", "1", "")                                                \
     /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
     ".LBIH_D_%=:\n\t"                        /* SCC = (gL != 0) */                     \
     "s_cbranch_scc0 .LBIH_DN_%=\n\t"                                                  \
-    "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR = !(t1 > sR) ^ neg; SCC = gR != 0 */ \
     "s_cbranch_scc0 .LBIH_TL_%=\n\t"         /* only the left child */                \
-    "s_bitcmp1_b32 %[near], s72\n\t"        /* both: near first, stack the other */  \
+    "s_bitcmp1_b32 %[near], m0\n\t"         /* both: near first, stack the other */  \
     "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
     "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
     "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
@@ -310,7 +315,7 @@
     "s_waitcnt lgkmcnt(0)\n\t"                                                        \
     "s_branch .LBIH_NB1_%=\n\t"                                                       \
     ".LBIH_DN_%=:\n\t"                       /* no left: right or pop */              \
-    "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR; SCC = gR != 0 */             \
     "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
     /* ---- pop until an entry has a searching lane ---- */                           \
     ".LBIH_P_%=:\n\t"                                                                 \
@@ -344,20 +349,22 @@
     /* ---- leaves of this node: test them (near first), then descend ---- */         \
     ".LBIH_LV0_%=:\n\t"                                                               \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL */                    \
-    "s_mov_b32 s80, s87\n\t"                 /* w: mid | counts */                     \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR */                    \
+    "s_mov_b32 s80, s87\n\t"                 /* w: mid | leaf bits | counts */         \
     "s_branch .LBIH_L_%=\n\t"                                                         \
     ".LBIH_LV1_%=:\n\t"                                                               \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"                                      \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"                                      \
     "s_mov_b32 s80, s91\n\t"                                                          \
     ".LBIH_L_%=:\n\t"                                                                 \
-    "s_and_b32 s82, s80, 0x7ffffff\n\t"      /* mid */                                \
-    "s_cmp_eq_u32 s81, 4\n\t"                                                         \
+    "s_and_b32 s82, s80, 0x3ffffff\n\t"      /* mid */                                \
+    "s_cmp_eq_u32 s81, 0x4000000\n\t"       /* left leaf only */                     \
     "s_cbranch_scc1 .LBIH_L1_%=\n\t"                                                  \
-    "s_cmp_eq_u32 s81, 8\n\t"                                                         \
+    "s_cmp_eq_u32 s81, 0x80000000\n\t"      /* right leaf only */                    \
     "s_cbranch_scc1 .LBIH_L2_%=\n\t"                                                  \
     "s_mov_b64 s[64:65], s[54:55]\n\t"       /* both children are leaves */           \
     "s_mov_b64 s[66:67], s[56:57]\n\t"                                                \
-    "s_bitcmp1_b32 %[near], s72\n\t"                                                  \
+    "s_bitcmp1_b32 %[near], m0\n\t"                                                   \
     "s_cbranch_scc0 .LBIH_LR_%=\n\t"                                                  \
     BIH_LEAF_L("a", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     BIH_LEAF_R("a", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \

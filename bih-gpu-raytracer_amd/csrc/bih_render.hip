@@ -1098,8 +1098,9 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
                 unsigned long long gR = ~(__ballot(t1 > (neg ? tMin : tMax)) ^ mneg) & act;
                 const float lo_L = neg ? t0 : tMin, hi_L = neg ? tMax : t0;
                 const float lo_R = neg ? tMin : t1, hi_R = neg ? t1 : tMax;
-                const uint32_t split = nd.z >> 4, mid = nd.w & kIdxMask;
-                const uint32_t leaf = (nd.z >> 2) & 3u;  // bit 0: left is a leaf, bit 1: right
+                const uint32_t split = nd.z >> 8, mid = nd.w & 0x3ffffffu;
+                // bit 0: left is a leaf, bit 1: right (w' bits 26, 31)
+                const uint32_t leaf = ((nd.w >> 26) & 1u) | ((nd.w >> 30) & 2u);
                 const uint32_t nearL = (nearbits >> ax) & 1u;
                 if (leaf) {
                     const unsigned long long tL = (leaf & 1u) ? gL : 0ull;
@@ -1193,6 +1194,11 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
         if (lane == 0) {
             for (int k = 0; k < 6; ++k) atomicAdd(a.work + 16 + k, pk[k]);
             atomicMax(a.work + 22, pk[6]);
+            // packets by log2(node steps): count, node steps, triangle tests
+            const uint32_t bin = pk[1] ? 31 - __builtin_clz(pk[1]) : 0;
+            atomicAdd(a.work + kHistWord + 16 + bin, 1u);
+            atomicAdd(a.work + kHistWord + 32 + bin, pk[1]);
+            atomicAdd(a.work + kHistWord + 48 + bin, pk[3]);
         }
 #endif
         if (STATS && valid) {
@@ -1241,8 +1247,10 @@ __device__ __forceinline__ uint32_t cu_key() {
 struct TileQueue {
     uint32_t *work;
     unsigned long long *slot;
+    const uint32_t *order;             // chunk permutation (k_chunk_order) or null
     uint32_t tiles_x, tiles_y, chunks_x, nchunks;
     uint32_t band, left;
+    uint32_t chunk;                    // chunk of the tile next() returned
 
     __device__ uint32_t band_begin(uint32_t b) const {
         const uint32_t rows = (nchunks / chunks_x);
@@ -1263,6 +1271,7 @@ struct TileQueue {
                 const uint32_t ty = (g / chunks_x) * kChunkH + lo / kChunkW;
                 if (tx < tiles_x && ty < tiles_y) {
                     tile = ty * tiles_x + tx;
+                    chunk = g;
                     return true;
                 }
                 continue;                                // edge chunk: position off the image
@@ -1275,9 +1284,10 @@ struct TileQueue {
                     c = __builtin_amdgcn_readfirstlane(c);
                     const uint32_t b0 = band_begin(band), b1 = band_begin(band + 1);
                     if (c < b1 - b0) {
-                        const uint32_t g = b0 + c;
+                        const uint32_t g = order ? order[b0 + c] : b0 + c;
                         if (lane == 0) atomicExch(slot, ((unsigned long long)(g + 1) << 32) | 1ull);
                         tile = (g / chunks_x) * kChunkH * tiles_x + (g % chunks_x) * kChunkW;
+                        chunk = g;
                         return true;                     // position 0: always on the image
                     }
                     band = (band + 1) & (kRegions - 1);
@@ -1300,8 +1310,10 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
     q.tiles_y = tiles_y;
     q.chunks_x = (tiles_x + kChunkW - 1) / kChunkW;
     q.nchunks = q.chunks_x * ((tiles_y + kChunkH - 1) / kChunkH);
+    q.order = a.chunk_order;
     q.band = xcc_id();
     q.left = kRegions;
+    q.chunk = 0;
     return q;
 }
 
@@ -1339,6 +1351,7 @@ k_render_packet_asm(const RenderArgs a) {
     uint32_t tile = 0;
     (void)ntiles;
     while (queue.next(lane, tile)) {
+        const uint64_t t_start = __builtin_amdgcn_s_memtime();
         uint32_t x, lr, s;
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
@@ -1445,6 +1458,44 @@ k_render_packet_asm(const RenderArgs a) {
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
             a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
+        // the packet's cycles feed the next frames' chunk order (k_chunk_order)
+        if (a.chunk_cost && lane == 0)
+            atomicAdd(a.chunk_cost + queue.chunk,
+                      (uint32_t)(__builtin_amdgcn_s_memtime() - t_start));
+    }
+}
+
+// Chunk order of the persistent packet kernel: within each of the kRegions
+// bands (TileQueue::band_begin), chunks by descending cost (cycles their
+// packets took in an earlier frame of the same geometry), ties by index, so
+// that the slow chunks start first and the frame does not end on one long
+// packet (longest-processing-time-first).  One block per band; the rank of
+// chunk i is the number of band chunks that sort before it.  Bands of more
+// than kOrderMax chunks keep the identity order.  Only the order of the work
+// changes, never a pixel.
+constexpr uint32_t kOrderMax = 4096;
+__global__ void __launch_bounds__(kThreads) k_chunk_order(const uint32_t *__restrict__ cost,
+                                                          uint32_t chunks_x, uint32_t nchunks,
+                                                          uint32_t *__restrict__ order) {
+    __shared__ uint32_t c[kOrderMax];
+    const uint32_t rows = nchunks / chunks_x, b = blockIdx.x;
+    const uint32_t b0 = (uint32_t)(((uint64_t)rows * b) / kRegions) * chunks_x;
+    const uint32_t b1 = (uint32_t)(((uint64_t)rows * (b + 1)) / kRegions) * chunks_x;
+    const uint32_t n = b1 - b0;
+    if (n > kOrderMax) {
+        for (uint32_t i = threadIdx.x; i < n; i += kThreads) order[b0 + i] = b0 + i;
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += kThreads) c[i] = cost[b0 + i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
+        const uint32_t ci = c[i];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t cj = c[j];
+            r += (cj > ci || (cj == ci && j < i)) ? 1u : 0u;
+        }
+        order[b0 + r] = b0 + i;
     }
 }
 
@@ -1488,9 +1539,12 @@ __global__ void __launch_bounds__(kThreads) k_node_alive(const uint4 *__restrict
     if (!aL && !aR) node_alive[p] = 0;
 }
 
-// Camera-relative node records {clip0 - O[axis], clip1 - O[axis], z', w} with
-// z' = split << 4 | leafR << 3 | leafL << 2 | axis (split << 4: the byte
-// offset of the children's record pair; w as in the packed nodes), and the
+// Camera-relative node records {clip0 - O[axis], clip1 - O[axis], z', w'} with
+// z' = split << 8 | axis (z' >> 4: the byte offset of the children's record
+// pair; the low byte is the axis alone, an s_set_gpr_idx_on index) and w' =
+// the packed w (mid | cntL << 27 | cntR << 29) | leafL << 26 | leafR << 31 --
+// for split < 2^24 and mid < 2^26, the scenes the packet kernels take
+// (packet_records_fit) -- and the
 // same records with every child subtree that no primary ray from O can
 // hit (all its triangles dead, tri_alive) cut off: clip0 - O = -inf (left) /
 // clip1 - O = +inf (right) make t0 = -inf*inv / t1 = +inf*inv fail the
@@ -1510,9 +1564,10 @@ __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict_
     const uint32_t ax = (nd.z >> 27) & 3u;
     const float org = sel3(ax, ox, oy, oz);
     const uint32_t split = nd.z & 0x7ffffffu;
-    const uint32_t z = (split << 4) | (((nd.z >> 30) & 1u) << 3) | (((nd.z >> 29) & 1u) << 2) | ax;
+    const uint32_t z = (split << 8) | ax;
+    const uint32_t w = nd.w | (((nd.z >> 29) & 1u) << 26) | (((nd.z >> 30) & 1u) << 31);
     uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
-                         __float_as_uint(__uint_as_float(nd.y) - org), z, nd.w);
+                         __float_as_uint(__uint_as_float(nd.y) - org), z, w);
     out[i] = r;
     const bool aL = ((nd.z >> 29) & 1u) ? leaf_alive[split] : node_alive[split];
     const bool aR = ((nd.z >> 30) & 1u) ? leaf_alive[split + 1] : node_alive[split + 1];
@@ -1561,6 +1616,12 @@ Variant variant_from_env() {
     return Variant::PacketAsm;
 }
 
+// The camera-relative records (k_node_prim) hold split << 8 and mid < 2^26,
+// and the asm walk forms 32-bit triangle byte offsets (64 B records).
+bool packet_records_fit(const RenderArgs &a) {
+    return a.hdr_n_tris < (1u << 26) && a.n_nodes < (1u << 24);
+}
+
 template <int L>
 hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse, hipStream_t st,
                              uint32_t blocks) {
@@ -1582,7 +1643,8 @@ hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse
             if (stats) hipLaunchKernelGGL((k_render_refill<false, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_refill<false, false, L>), g, b, 0, st, a);
         }
-    } else if (var == Variant::Packet1) {
+    } else if (var == Variant::Packet1 || !packet_records_fit(a)) {
+        // packed canonical nodes: any scene size
         if (traverse == 0) {
             if (stats) hipLaunchKernelGGL((k_render_packet<true, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet<true, false, L>), g, b, 0, st, a);
@@ -1590,7 +1652,7 @@ hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse
             if (stats) hipLaunchKernelGGL((k_render_packet<false, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet<false, false, L>), g, b, 0, st, a);
         }
-    } else if (var == Variant::PacketAsm && a.hdr_n_tris < (1u << 26)) {
+    } else if (var == Variant::PacketAsm) {
         if (traverse == 0) {
             if (stats) hipLaunchKernelGGL((k_render_packet_asm<true, true, L>), g, b, 0, st, a);
             else hipLaunchKernelGGL((k_render_packet_asm<true, false, L>), g, b, 0, st, a);
@@ -1736,6 +1798,25 @@ size_t spill_words(uint32_t blocks) {
     const size_t lane_k = (size_t)kThreads * (kStackDepth - kLdsStack) * 3;
     const size_t packet_k = (size_t)(kThreads / 64) * (kStackDepth - kPacketRegs) * 3 * 64;
     return (size_t)blocks * (lane_k > packet_k ? lane_k : packet_k);
+}
+
+uint32_t chunk_count(uint32_t w, uint32_t nrows, uint32_t spp, uint32_t *chunks_x) {
+    if (spp == 0 || spp > 64 || (spp & (spp - 1)) != 0) return 0;
+    const int L = __builtin_ctz(spp);
+    const uint32_t pix = 64u >> L;
+    const uint32_t tw = 1u << ((6 - L + 1) / 2), th = pix / tw;
+    const uint32_t tiles_x = (w + tw - 1) / tw, tiles_y = (nrows + th - 1) / th;
+    const uint32_t cx = (tiles_x + kChunkW - 1) / kChunkW;
+    if (chunks_x) *chunks_x = cx;
+    return cx * ((tiles_y + kChunkH - 1) / kChunkH);
+}
+
+int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks, uint32_t *order,
+                       void *stream) {
+    if (nchunks == 0) return 0;
+    hipLaunchKernelGGL(k_chunk_order, dim3(kRegions), dim3(kThreads), 0, (hipStream_t)stream, cost,
+                       chunks_x, nchunks, order);
+    return (int)hipGetLastError();
 }
 
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
