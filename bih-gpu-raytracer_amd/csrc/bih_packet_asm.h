@@ -235,11 +235,13 @@
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"  /* gL = (t0 > sL) ^ neg; SCC = gL != 0 */ \
     TAIL
 
-// Stack entry {lane lo/hi (sentinel outside MASK), node = byte offset of its
-// record s73 + NODE_OFS}; written on every lane (EXEC = all; the caller sets
-// EXEC afterwards).  Deep slots go to the wave's spill area in the
-// out-of-line block BIH_PUSH_SPILL(TAG) emits.
-#define BIH_PUSH(TAG, MASK, LO, HI, NODE_OFS)                                         \
+// Stack entry {lane lo/hi (sentinel outside MASK), node = NODE, the byte
+// offset of its record (NODE_SET forms it in s74 where it is not s73)};
+// written on every lane (EXEC = all; the caller sets EXEC afterwards).
+// s_set_gpr_idx_on leaves the slot index in M0[7:0], the lane v_writelane
+// selects.  Deep slots go to the wave's spill area in the out-of-line block
+// BIH_PUSH_SPILL(TAG) emits (which sets M0 itself).
+#define BIH_PUSH(TAG, MASK, LO, HI, NODE_SET, NODE)                                   \
     "s_mov_b64 exec, -1\n\t"                                                          \
     "v_cndmask_b32_e64 v33, %[snan], " LO ", " MASK "\n\t"                            \
     "s_cmp_ge_u32 s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                  \
@@ -249,14 +251,13 @@
     "v_mov_b32_e32 v51, " HI "\n\t"                                                   \
     "s_set_gpr_idx_off\n\t"                                                           \
     ".LBIH_PN" TAG "_%=:\n\t"                                                         \
-    "s_add_u32 s74, s73, " NODE_OFS "\n\t"                                            \
-    "s_mov_b32 m0, s71\n\t"                                                           \
-    "s_nop 0\n\t"                                                                     \
-    "v_writelane_b32 v39, s74, m0\n\t"                                                \
+    NODE_SET                                                                          \
+    "v_writelane_b32 v39, " NODE ", m0\n\t"                                           \
     "s_add_u32 s71, s71, 1\n\t"
 
 #define BIH_PUSH_SPILL(TAG, HI)                                                       \
     ".LBIH_SP" TAG "_%=:\n\t"                /* deep slot: wave spill area */         \
+    "s_mov_b32 m0, s71\n\t"                  /* the lane v_writelane selects */     \
     "s_sub_u32 s74, s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                \
     "s_lshl_b32 s74, s74, 9\n\t"                                                      \
     "v_add_u32_e32 v35, s74, %[lane4]\n\t"                                            \
@@ -297,7 +298,7 @@
     "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
     "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
     "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
-    BIH_PUSH("r", "s[56:57]", "v31", "v32", "16")                                     \
+    BIH_PUSH("r", "s[56:57]", "v31", "v32", "s_add_u32 s74, s73, 16\n\t", "s74")    \
     ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
     "s_mov_b64 exec, s[54:55]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
@@ -307,7 +308,7 @@
     ".LBIH_BR_%=:\n\t"                                                                \
     "v_cndmask_b32_e64 v29, %[tmin], v25, s[58:59]\n\t"   /* left  [neg ? t0 : tMin, */ \
     "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
-    BIH_PUSH("l", "s[54:55]", "v29", "v30", "0")                                      \
+    BIH_PUSH("l", "s[54:55]", "v29", "v30", "", "s73")                              \
     ".LBIH_TR_%=:\n\t"                       /* take right: record in s[88:91] */     \
     "s_mov_b64 exec, s[56:57]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[58:59]\n\t" /* [neg ? tMin : t1,    */ \
@@ -321,9 +322,8 @@
     ".LBIH_P_%=:\n\t"                                                                 \
     "s_waitcnt lgkmcnt(0)\n\t"               /* the pair prefetch lands in s[84:91] */ \
     ".LBIH_PL_%=:\n\t"                                                                \
-    "s_cmp_eq_u32 s71, 0\n\t"                                                         \
+    "s_sub_u32 s71, s71, 1\n\t"              /* SCC = borrow: the stack was empty */  \
     "s_cbranch_scc1 .LBIH_X_%=\n\t"                                                   \
-    "s_sub_u32 s71, s71, 1\n\t"                                                       \
     "s_mov_b64 exec, -1\n\t"                                                          \
     "s_cmp_ge_u32 s71, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                  \
     "s_cbranch_scc1 .LBIH_SQ_%=\n\t"                                                  \
