@@ -217,23 +217,75 @@
     "v_mul_f32_e32 v26, " D1 ", v24\n\t"     /* t1 */
 
 // Per-lane child decisions (EXEC = the node's lanes; compares give 0 off
-// EXEC), then: a leaf child -> LV<X> (w still in the record registers); two
-// internal children -> request their record pair into s[84:91] (the current
-// record's registers are free by then) and continue at D (TAIL).  s[54:55] /
-// s[56:57] leave here as the raw compares; gL = s[54:55] ^ neg is formed
-// before D (SCC = gL != 0), gR = s[56:57] ^ neg where it is first tested (its
-// SCC then replaces a compare with 0).
-#define BIH_NODE_NC(Z, W, X, TAIL)                                                    \
+// EXEC).  s[54:55] / s[56:57] leave here as the raw compares; gL = s[54:55] ^
+// neg is formed before D (SCC = gL != 0), gR = s[56:57] ^ neg where it is
+// first tested (its SCC then replaces a compare with 0).
+#define BIH_NODE_DEC                                                                  \
     "v_cndmask_b32_e64 v27, %[tmin], %[tmax], s[58:59]\n\t"   /* sL = neg ? tMax : tMin */ \
     "v_cndmask_b32_e64 v28, %[tmax], %[tmin], s[58:59]\n\t"   /* sR = neg ? tMin : tMax */ \
     "v_cmp_gt_f32_e64 s[54:55], v25, v27\n\t"                                         \
-    "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"                                        \
+    "v_cmp_ngt_f32_e64 s[56:57], v26, v28\n\t"
+
+// Node step of the record {D0 D1 Z W} held in one half of a record buffer.
+// Two internal children: their record pair is requested into the OTHER
+// buffer (YREGS) before the decisions are computed, so the load overlaps
+// them, and the walk continues at D<DY> (DTAIL: a branch, or nothing where
+// D<DY> follows).  A leaf child: LV<TAG> (out of line, BIH_NODE_LV).
+#define BIH_NODE_STEP(TAG, CNT_NODE, D0, D1, Z, W, YREGS, DTAIL)                       \
+    ".LBIH_NB" TAG "_%=:\n\t"                                                         \
+    CNT_NODE                                                                          \
     "s_lshr_b32 s73, " Z ", 4\n\t"           /* byte offset of the children's pair */ \
     "s_and_b32 s81, " W ", 0x84000000\n\t"  /* leaf bits: 1<<26 left, 1<<31 right */  \
-    "s_cbranch_scc1 .LBIH_LV" X "_%=\n\t"                                              \
-    "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
+    "s_cbranch_scc1 .LBIH_LV" TAG "_%=\n\t"                                           \
+    "s_load_dwordx8 " YREGS ", %[nodes], s73\n\t"                                     \
+    BIH_NODE_REC(D0, D1, Z)                                                           \
+    BIH_NODE_DEC                                                                      \
     "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"  /* gL = (t0 > sL) ^ neg; SCC = gL != 0 */ \
-    TAIL
+    DTAIL
+
+// The same node step when a child is a leaf: decisions, w to s80, then the
+// shared leaf section L.
+#define BIH_NODE_LV(TAG, D0, D1, Z, W)                                                \
+    ".LBIH_LV" TAG "_%=:\n\t"                                                         \
+    BIH_NODE_REC(D0, D1, Z)                                                           \
+    BIH_NODE_DEC                                                                      \
+    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL */                    \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR */                    \
+    "s_mov_b32 s80, " W "\n\t"               /* w: mid | leaf bits | counts */         \
+    "s_branch .LBIH_L_%=\n\t"
+
+// Descend with the children's records in buffer Y (Y0 = left, Y1 = right):
+// the near child (majority order) if visited, the other stacked.
+#define BIH_DESCEND(Y)                                                                \
+    ".LBIH_D" Y "_%=:\n\t"                   /* SCC = (gL != 0) */                     \
+    "s_cbranch_scc0 .LBIH_DN" Y "_%=\n\t"                                             \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR = !(t1 > sR) ^ neg; SCC = gR != 0 */ \
+    "s_cbranch_scc0 .LBIH_TL" Y "_%=\n\t"    /* only the left child */                \
+    "s_bitcmp1_b32 %[near], m0\n\t"         /* both: near first, stack the other */  \
+    "s_cbranch_scc0 .LBIH_BR" Y "_%=\n\t"                                             \
+    "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
+    "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
+    BIH_PUSH("r" Y, "s[56:57]", "v31", "v32", "s_add_u32 s74, s73, 16\n\t", "s74")  \
+    ".LBIH_TL" Y "_%=:\n\t"                  /* take left: record in Y0 */             \
+    "s_mov_b64 exec, s[54:55]\n\t"                                                    \
+    "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
+    "v_cndmask_b32_e64 %[tmax], v25, %[tmax], s[58:59]\n\t" /*  neg ? tMax : t0]    */ \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
+    "s_branch .LBIH_NB" Y "0_%=\n\t"                                                  \
+    ".LBIH_BR" Y "_%=:\n\t"                                                           \
+    "v_cndmask_b32_e64 v29, %[tmin], v25, s[58:59]\n\t"   /* left  [neg ? t0 : tMin, */ \
+    "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
+    BIH_PUSH("l" Y, "s[54:55]", "v29", "v30", "", "s73")                              \
+    ".LBIH_TR" Y "_%=:\n\t"                  /* take right: record in Y1 */            \
+    "s_mov_b64 exec, s[56:57]\n\t"                                                    \
+    "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[58:59]\n\t" /* [neg ? tMin : t1,    */ \
+    "v_cndmask_b32_e64 %[tmax], %[tmax], v26, s[58:59]\n\t" /*  neg ? t1 : tMax]    */ \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
+    "s_branch .LBIH_NB" Y "1_%=\n\t"                                                  \
+    ".LBIH_DN" Y "_%=:\n\t"                  /* no left: right or pop */              \
+    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR; SCC = gR != 0 */             \
+    "s_cbranch_scc1 .LBIH_TR" Y "_%=\n\t"                                             \
+    "s_branch .LBIH_P_%=\n\t"
 
 // Stack entry {lane lo/hi (sentinel outside MASK), node = NODE, the byte
 // offset of its record (NODE_SET forms it in s74 where it is not s73)};
@@ -278,49 +330,17 @@
     /* ---- record of node s70 from memory (root, pops) ---- */                       \
     ".LBIH_N_%=:\n\t"                        /* s70 = the record's byte offset */      \
     "s_load_dwordx4 s[84:87], %[nodes], s70\n\t"                                      \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
-    /* ---- node step, record in s[84:87] (left child / loaded) ---- */               \
-    ".LBIH_NB0_%=:\n\t"                                                               \
-    CNT_NODE                                                                          \
-    BIH_NODE_REC("s84", "s85", "s86")                                                 \
-    BIH_NODE_NC("s86", "s87", "0", "s_branch .LBIH_D_%=\n\t")                         \
-    /* ---- node step, record in s[88:91] (right child) ---- */                       \
-    ".LBIH_NB1_%=:\n\t"                                                               \
-    CNT_NODE                                                                          \
-    BIH_NODE_REC("s88", "s89", "s90")                                                 \
-    BIH_NODE_NC("s90", "s91", "1", "")                                                \
-    /* ---- descend: near child (majority order) if visited, stack the other ---- */  \
-    ".LBIH_D_%=:\n\t"                        /* SCC = (gL != 0) */                     \
-    "s_cbranch_scc0 .LBIH_DN_%=\n\t"                                                  \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR = !(t1 > sR) ^ neg; SCC = gR != 0 */ \
-    "s_cbranch_scc0 .LBIH_TL_%=\n\t"         /* only the left child */                \
-    "s_bitcmp1_b32 %[near], m0\n\t"         /* both: near first, stack the other */  \
-    "s_cbranch_scc0 .LBIH_BR_%=\n\t"                                                  \
-    "v_cndmask_b32_e64 v31, v26, %[tmin], s[58:59]\n\t"   /* right [neg ? tMin : t1, */ \
-    "v_cndmask_b32_e64 v32, %[tmax], v26, s[58:59]\n\t"   /*        neg ? t1 : tMax] */ \
-    BIH_PUSH("r", "s[56:57]", "v31", "v32", "s_add_u32 s74, s73, 16\n\t", "s74")    \
-    ".LBIH_TL_%=:\n\t"                       /* take left: record in s[84:87] */      \
-    "s_mov_b64 exec, s[54:55]\n\t"                                                    \
-    "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[58:59]\n\t" /* [neg ? t0 : tMin,    */ \
-    "v_cndmask_b32_e64 %[tmax], v25, %[tmax], s[58:59]\n\t" /*  neg ? tMax : t0]    */ \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
-    "s_branch .LBIH_NB0_%=\n\t"                                                       \
-    ".LBIH_BR_%=:\n\t"                                                                \
-    "v_cndmask_b32_e64 v29, %[tmin], v25, s[58:59]\n\t"   /* left  [neg ? t0 : tMin, */ \
-    "v_cndmask_b32_e64 v30, v25, %[tmax], s[58:59]\n\t"   /*        neg ? tMax : t0] */ \
-    BIH_PUSH("l", "s[54:55]", "v29", "v30", "", "s73")                              \
-    ".LBIH_TR_%=:\n\t"                       /* take right: record in s[88:91] */     \
-    "s_mov_b64 exec, s[56:57]\n\t"                                                    \
-    "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[58:59]\n\t" /* [neg ? tMin : t1,    */ \
-    "v_cndmask_b32_e64 %[tmax], %[tmax], v26, s[58:59]\n\t" /*  neg ? t1 : tMax]    */ \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                        \
-    "s_branch .LBIH_NB1_%=\n\t"                                                       \
-    ".LBIH_DN_%=:\n\t"                       /* no left: right or pop */              \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"  /* gR; SCC = gR != 0 */             \
-    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
+    "s_waitcnt lgkmcnt(0)\n\t"                 /* falls into node step A0 */           \
+    /* ---- node steps: record buffers A = s[84:91], B = s[92:99] ---- */             \
+    BIH_NODE_STEP("A0", CNT_NODE, "s84", "s85", "s86", "s87", "s[92:99]", "s_branch .LBIH_DB_%=\n\t") \
+    BIH_NODE_STEP("A1", CNT_NODE, "s88", "s89", "s90", "s91", "s[92:99]", "")          \
+    BIH_DESCEND("B")                                                                  \
+    BIH_NODE_STEP("B0", CNT_NODE, "s92", "s93", "s94", "s95", "s[84:91]", "s_branch .LBIH_DA_%=\n\t") \
+    BIH_NODE_STEP("B1", CNT_NODE, "s96", "s97", "s98", "s99", "s[84:91]", "")          \
+    BIH_DESCEND("A")                                                                  \
     /* ---- pop until an entry has a searching lane ---- */                           \
     ".LBIH_P_%=:\n\t"                                                                 \
-    "s_waitcnt lgkmcnt(0)\n\t"               /* the pair prefetch lands in s[84:91] */ \
+    "s_waitcnt lgkmcnt(0)\n\t"               /* a pair prefetch may be in flight */    \
     ".LBIH_PL_%=:\n\t"                                                                \
     "s_sub_u32 s71, s71, 1\n\t"              /* SCC = borrow: the stack was empty */  \
     "s_cbranch_scc1 .LBIH_X_%=\n\t"                                                   \
@@ -347,15 +367,10 @@
     "s_waitcnt vmcnt(0)\n\t"                                                          \
     "s_branch .LBIH_PQ_%=\n\t"                                                        \
     /* ---- leaves of this node: test them (near first), then descend ---- */         \
-    ".LBIH_LV0_%=:\n\t"                                                               \
-    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"          /* gL */                    \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"          /* gR */                    \
-    "s_mov_b32 s80, s87\n\t"                 /* w: mid | leaf bits | counts */         \
-    "s_branch .LBIH_L_%=\n\t"                                                         \
-    ".LBIH_LV1_%=:\n\t"                                                               \
-    "s_xor_b64 s[54:55], s[54:55], s[58:59]\n\t"                                      \
-    "s_xor_b64 s[56:57], s[56:57], s[58:59]\n\t"                                      \
-    "s_mov_b32 s80, s91\n\t"                                                          \
+    BIH_NODE_LV("A0", "s84", "s85", "s86", "s87")                                     \
+    BIH_NODE_LV("A1", "s88", "s89", "s90", "s91")                                     \
+    BIH_NODE_LV("B0", "s92", "s93", "s94", "s95")                                     \
+    BIH_NODE_LV("B1", "s96", "s97", "s98", "s99")                                     \
     ".LBIH_L_%=:\n\t"                                                                 \
     "s_and_b32 s82, s80, 0x3ffffff\n\t"      /* mid */                                \
     "s_cmp_eq_u32 s81, 0x4000000\n\t"       /* left leaf only */                     \
@@ -379,7 +394,7 @@
     BIH_LEAF_L("c", ANY, CNT_LEAF_L, CNT_TRI_L)                                       \
     CLR("s[56:57]")                                                                   \
     "s_cmp_lg_u64 s[56:57], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_TR_%=\n\t"                                                  \
+    "s_cbranch_scc1 .LBIH_TRA_%=\n\t"                                                 \
     "s_branch .LBIH_P_%=\n\t"                                                         \
     ".LBIH_L2_%=:\n\t"                       /* right leaf, left internal */          \
     "s_load_dwordx8 s[84:91], %[nodes], s73\n\t"                                      \
@@ -387,10 +402,12 @@
     BIH_LEAF_R("d", ANY, CNT_LEAF_R, CNT_TRI_R)                                       \
     CLR("s[54:55]")                                                                   \
     "s_cmp_lg_u64 s[54:55], 0\n\t"                                                    \
-    "s_cbranch_scc1 .LBIH_TL_%=\n\t"                                                  \
+    "s_cbranch_scc1 .LBIH_TLA_%=\n\t"                                                 \
     "s_branch .LBIH_P_%=\n\t"                                                         \
-    BIH_PUSH_SPILL("r", "v32")                                                        \
-    BIH_PUSH_SPILL("l", "v30")                                                        \
+    BIH_PUSH_SPILL("rA", "v32")                                                       \
+    BIH_PUSH_SPILL("lA", "v30")                                                       \
+    BIH_PUSH_SPILL("rB", "v32")                                                       \
+    BIH_PUSH_SPILL("lB", "v30")                                                       \
     ".LBIH_X_%=:\n\t"                                                                 \
     "s_mov_b64 exec, -1\n\t"               /* the statement runs on a full wave */    \
     "s_mov_b32 m0, s79"
@@ -401,6 +418,7 @@
     "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
     "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82",       \
     "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",                           \
+    "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99",                           \
     "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
     "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", \
