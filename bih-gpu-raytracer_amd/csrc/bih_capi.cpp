@@ -12,6 +12,7 @@
 
 #include <mutex>
 #include <new>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/bih.h"
@@ -562,6 +563,67 @@ int bih_sync(const bih_tree *tr, void *stream) {
     if (!tr) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+#if BIH_WAVE_TIMELINE
+    if (tr->spill && tr->last_slot >= 0 && hipStreamSynchronize(st) == hipSuccess) {
+        // per-wave records of k_render_packet_asm at each wave's spill base
+        const size_t per = (size_t)(bih::kStackDepth - 16) * 3 * 64;   // kPacketRegs = 16
+        const size_t waves = tr->spill_per_slot / per;
+        std::vector<uint32_t> h(tr->spill_per_slot);
+        if (hipMemcpy(h.data(), tr->spill + (size_t)tr->last_slot * tr->spill_per_slot,
+                      h.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+            // times: s_memrealtime (100 MHz), relative to the XCD's first
+            // wave start and its last wave end
+            uint64_t x0[16], x1[16];
+            for (int x = 0; x < 16; ++x) { x0[x] = ~0ull; x1[x] = 0; }
+            for (size_t w = 0; w < waves; ++w) {
+                const uint32_t *r = h.data() + w * per;
+                const uint64_t b = r[0] | ((uint64_t)r[1] << 32), e = r[2] | ((uint64_t)r[3] << 32);
+                const uint32_t x = r[9] & 15;
+                if (!b || e < b) continue;
+                x0[x] = b < x0[x] ? b : x0[x];
+                x1[x] = e > x1[x] ? e : x1[x];
+            }
+            double life = 0, spans = 0;
+            uint64_t npk = 0, nlive = 0, maxpk = 0;
+            double maxpk_at = 0, maxpk_frac = 0;
+            std::vector<double> ends, lasts;
+            for (size_t w = 0; w < waves; ++w) {
+                const uint32_t *r = h.data() + w * per;
+                const uint64_t b = r[0] | ((uint64_t)r[1] << 32), e = r[2] | ((uint64_t)r[3] << 32);
+                const uint64_t l = r[4] | ((uint64_t)r[5] << 32);
+                const uint64_t m = r[10] | ((uint64_t)r[11] << 32);
+                const uint32_t x = r[9] & 15;
+                if (!b || e < b) continue;
+                const double span = (double)(x1[x] - x0[x]);
+                life += (double)(e - b) / span;
+                ends.push_back((double)(e - x0[x]) / span);
+                lasts.push_back((double)(l - x0[x]) / span);
+                npk += r[6];
+                nlive += r[7];
+                if (r[8] > maxpk) {
+                    maxpk = r[8];
+                    maxpk_at = (double)(m - x0[x]) / span;
+                    maxpk_frac = (double)r[8] / span;
+                }
+            }
+            for (int x = 0; x < 16; ++x)
+                if (x1[x]) spans = spans > (double)(x1[x] - x0[x]) ? spans : (double)(x1[x] - x0[x]);
+            if (!ends.empty()) {
+                std::sort(ends.begin(), ends.end());
+                std::sort(lasts.begin(), lasts.end());
+                auto q = [](const std::vector<double> &v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
+                fprintf(stderr,
+                        "wave-timeline waves %zu xcd-span max %.0f x10ns mean-life %.3f packets %llu live %llu "
+                        "max-packet %llu x10ns = %.3f span, starts at %.3f | wave end q10 %.3f q50 %.3f q90 %.3f | "
+                        "last packet start q50 %.3f q90 %.3f q99 %.3f max %.3f\n",
+                        ends.size(), spans, life / ends.size(), (unsigned long long)npk,
+                        (unsigned long long)nlive, (unsigned long long)maxpk, maxpk_frac, maxpk_at,
+                        q(ends, 0.1), q(ends, 0.5), q(ends, 0.9), q(lasts, 0.5), q(lasts, 0.9),
+                        q(lasts, 0.99), q(lasts, 1.0));
+            }
+        }
+    }
+#endif
 #if BIH_PACKET_COUNTERS
     if (tr->work && tr->last_slot >= 0) {
         uint32_t c[bih::kWorkWords];

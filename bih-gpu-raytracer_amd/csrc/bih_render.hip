@@ -1350,6 +1350,12 @@ k_render_packet_asm(const RenderArgs a) {
     TileQueue queue = make_queue(a, tiles_x, (a.nrows + TH - 1) / TH);
     uint32_t tile = 0;
     (void)ntiles;
+#if BIH_WAVE_TIMELINE
+    const uint64_t tl_begin = __builtin_amdgcn_s_memrealtime();
+    uint64_t tl_last = tl_begin;
+    uint32_t tl_packets = 0, tl_live = 0, tl_max = 0;
+    uint64_t tl_max_at = tl_begin, tl_pk = tl_begin;
+#endif
     while (queue.next(lane, tile)) {
         const uint64_t t_start = __builtin_amdgcn_s_memtime();
         uint32_t x, lr, s;
@@ -1462,7 +1468,42 @@ k_render_packet_asm(const RenderArgs a) {
         if (a.chunk_cost && lane == 0)
             atomicAdd(a.chunk_cost + queue.chunk,
                       (uint32_t)(__builtin_amdgcn_s_memtime() - t_start));
+#if BIH_WAVE_TIMELINE
+        {
+            // 100 MHz real-time clock (one time base for every XCD)
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            const uint32_t dt = (uint32_t)(now - tl_pk);
+            const uint64_t t_start = tl_pk;
+            tl_pk = now;
+            tl_last = t_start;
+            ++tl_packets;
+            tl_live += live ? 1u : 0u;
+            if (dt > tl_max) {
+                tl_max = dt;
+                tl_max_at = t_start;
+            }
+        }
+#endif
     }
+#if BIH_WAVE_TIMELINE
+    // debug builds: {begin, end, last packet start} u64, packets, live packets,
+    // longest packet (cycles) at the wave's spill base (bih_sync prints them)
+    if (lane == 0) {
+        uint32_t *r = const_cast<uint32_t *>(wspill);
+        const uint64_t tl_end = __builtin_amdgcn_s_memrealtime();
+        const uint64_t v[3] = {tl_begin, tl_end, tl_last};
+        for (int k = 0; k < 3; ++k) {
+            r[2 * k] = (uint32_t)v[k];
+            r[2 * k + 1] = (uint32_t)(v[k] >> 32);
+        }
+        r[6] = tl_packets;
+        r[7] = tl_live;
+        r[8] = tl_max;
+        r[9] = xcc_id();
+        r[10] = (uint32_t)tl_max_at;
+        r[11] = (uint32_t)(tl_max_at >> 32);
+    }
+#endif
 }
 
 // Chunk order of the persistent packet kernel: within each of the kRegions
