@@ -104,7 +104,8 @@ int wait_renders(bih_tree *tr, hipStream_t st) {
 }
 
 // Cost-ordered tile queue of the packet kernel (bih::launch_chunk_order):
-// the chunks of this render start in descending order of the cycles they
+// the chunks of this render start in descending order of the cycles their
+// longest packet
 // took in the last render of the same slot and geometry (frame f - kSlots in
 // a frame sequence), so the slow part of the image starts first and the frame
 // does not end on one long packet.  The order never changes a pixel.

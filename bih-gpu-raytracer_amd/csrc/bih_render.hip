@@ -1464,9 +1464,11 @@ k_render_packet_asm(const RenderArgs a) {
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
             a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
-        // the packet's cycles feed the next frames' chunk order (k_chunk_order)
+        // the longest packet of a chunk (cycles) orders the chunk in the next
+        // frames (k_chunk_order): a chunk's packets run side by side on one
+        // CU, so its longest packet is what has to start early
         if (a.chunk_cost && lane == 0)
-            atomicAdd(a.chunk_cost + queue.chunk,
+            atomicMax(a.chunk_cost + queue.chunk,
                       (uint32_t)(__builtin_amdgcn_s_memtime() - t_start));
 #if BIH_WAVE_TIMELINE
         {
@@ -1507,8 +1509,8 @@ k_render_packet_asm(const RenderArgs a) {
 }
 
 // Chunk order of the persistent packet kernel: within each of the kRegions
-// bands (TileQueue::band_begin), chunks by descending cost (cycles their
-// packets took in an earlier frame of the same geometry), ties by index, so
+// bands (TileQueue::band_begin), chunks by descending cost (the cycles their
+// longest packet took in an earlier frame of the same geometry), ties by index, so
 // that the slow chunks start first and the frame does not end on one long
 // packet (longest-processing-time-first).  One block per band; the rank of
 // chunk i is the number of band chunks that sort before it.  Bands of more
