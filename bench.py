@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--no-reference-leg", action="store_true")
     ap.add_argument("--no-rebuild-leg", action="store_true",
                     help="skip the leg that rebuilds the BIH every frame (as the reference does)")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="time the headline leg only (no side legs), e.g. under rocprofv3 so that "
+                         "its kernel average is the headline's launches")
     return ap.parse_args()
 
 
@@ -182,6 +185,8 @@ def main():
     elapsed, kernel_ms, fps = timed(mode, trav, 0)
     value = fps * rays_per_frame * args.steps / elapsed
 
+    if args.headline_only:
+        args.no_reference_leg = args.no_rebuild_leg = True
     ref_leg = None
     if not args.no_reference_leg:
         other = bihrt.TRAVERSE_REFERENCE if trav == bihrt.TRAVERSE_ANYHIT else bihrt.TRAVERSE_ANYHIT
@@ -193,7 +198,7 @@ def main():
 
     # one frame at a time (frame latency): informational when frames overlap
     serial_leg = None
-    if F > 1:
+    if F > 1 and not args.headline_only:
         el5, kms5, fps5 = timed(mode, trav, 4000, nf=1)
         serial_leg = {"value": fps5 * rays_per_frame * args.steps / el5, "unit": "rays/s",
                       "ms_per_step": 1e3 * el5 / args.steps, "kernel_ms": kms5,
@@ -201,7 +206,7 @@ def main():
 
     # N > 1: the other decomposition, informational
     side_leg = None
-    if world > 1:
+    if world > 1 and not args.headline_only:
         other_mode = "strong" if mode == "weak" else "weak"
         el4, kms4, fps4 = timed(other_mode, trav, 3000)
         side_leg = {"mode": other_mode,
@@ -236,7 +241,12 @@ def main():
     rays_all = rays_per_frame
     b_ray = (NODE_B * n_node + LEAF_B * n_leaf + TRI_B * n_tri) / rays_all + (FB_B + RNG_B) / SPP
     launch_rays = rows.nrows * W * SPP
-    achieved = b_ray * launch_rays / (kernel_ms * 1e-3) / 1e9
+    # per-launch duration of the kernel: with frames in flight a launch's
+    # events also count the time it queues behind the other stream's frame,
+    # so the isolated launches of the one-in-flight leg give the duration
+    # (what rocprofv3 reports for `--headline-only --in-flight 1`)
+    launch_ms = serial_leg["kernel_ms"] if serial_leg else kernel_ms
+    achieved = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9
 
     cpu = None
     parity_rows = None
@@ -273,7 +283,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "bytes_per_ray": b_ray,
-                "launch_ms": kernel_ms,
+                "launch_ms": launch_ms,
+                "launch_ms_source": "one_in_flight leg (isolated launches)" if serial_leg
+                                    else "headline leg",
                 "effective_gbs": b_ray * launch_rays / (elapsed / args.steps) / 1e9,
                 "counters_per_ray": {"nodes": n_node / rays_all, "leaves": n_leaf / rays_all,
                                      "tris": n_tri / rays_all},
