@@ -111,6 +111,16 @@ int wait_renders(bih_tree *tr, hipStream_t st) {
 // does not end on one long packet.  The order never changes a pixel.
 // Called after `st` waits for the slot's previous render.  BIH_CHUNK_ORDER=0
 // turns it off (tuning / A-B).
+// The any-hit walk's shortcut pass (k_render_packet_asm, bih_render.hip):
+// on unless BIH_FAST=0 (A-B).  It never changes a pixel.
+bool fast_enabled() {
+    static const bool enabled = [] {
+        const char *e = getenv("BIH_FAST");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return enabled;
+}
+
 int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &rows, int slot,
                         hipStream_t st, bih::RenderArgs &a) {
     static const bool enabled = [] {
@@ -510,7 +520,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
             int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
-                                      tr->t.dup_cnt, n_int,
+                                      tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
                                       cam->origin,
                                       tr->prim, st);
             if (le) return map_hip(le);
@@ -541,6 +551,9 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
     a.node_cull = a.node_prim ? a.node_prim + (n_int + 1) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
+    if (tr->prim && n_int > 0 && fast_enabled())
+        a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
+                                                 bih::fast_offset(tr->t.n, n_int));
     a.rng_in = rng_buf(tr, cur);
     a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;
     a.out = d_out;

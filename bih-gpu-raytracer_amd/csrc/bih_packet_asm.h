@@ -18,7 +18,8 @@
 // requested with one s_load_dwordx8 into the other of two record buffers
 // (A = s[76:83], B = s[36:43]) before the node's decisions are computed;
 // descending to the left child continues at NB<buf>0, to the right at
-// NB<buf>1.  Pops and the root load their record into A0 = s[76:79].
+// NB<buf>1.  The root loads its record into A0 = s[76:79]; a pop reads it
+// there from the VGPR stack (BIH_STACK_REC) or loads it like the root.
 //
 // Register map (physical registers, listed as clobbers so hipcc keeps its own
 // values out of them; the stack lives only inside the statement).  Kept at or
@@ -35,7 +36,8 @@
 //   v24 inv  v25 t0  v26 t1  v27 sL  v28 sR  v29-v32 {lo,hi} of a stacked child
 //   (MT: v24, v27-v30 division temps; t0/t1 survive the leaf tests)
 //   v33-v38 temps (MT: v35-v37 p, v38 det then 1/det)  v39 stacked node ids
-//   (lane k = slot k)  v40-v50 stacked lo (slot = gpr index)  v51-v61 stacked hi
+//   (lane k = slot k; BIH_STACK_REC: v39/v65/v66/v67 lane k = the 4 dwords of
+//   slot k's record)  v40-v50 stacked lo (slot = gpr index)  v51-v61 stacked hi
 //   (11 slots)
 // Slots >= BIH_ASM_SLOTS go to the wave's HBM spill area, [slot - BIH_ASM_SLOTS]
 // x {lo[64], hi[64]} f32.  Lanes outside a stacked entry's mask hold the
@@ -259,7 +261,7 @@
 
 // Descend with the children's records in buffer Y (Y0 = left, Y1 = right):
 // the near child (majority order) if visited, the other stacked.
-#define BIH_DESCEND(Y)                                                                \
+#define BIH_DESCEND(Y, RECL, RECR)                                                                \
     ".LBIH_D" Y "_%=:\n\t"                   /* SCC = (gL != 0) */                     \
     "s_cbranch_scc0 .LBIH_DN" Y "_%=\n\t"                                             \
     "s_xor_b64 s[54:55], s[54:55], s[56:57]\n\t"  /* gR = !(t1 > sR) ^ neg; SCC = gR != 0 */ \
@@ -268,7 +270,7 @@
     "s_cbranch_scc0 .LBIH_BR" Y "_%=\n\t"                                             \
     "v_cndmask_b32_e64 v31, v26, %[tmin], s[56:57]\n\t"   /* right [neg ? tMin : t1, */ \
     "v_cndmask_b32_e64 v32, %[tmax], v26, s[56:57]\n\t"   /*        neg ? t1 : tMax] */ \
-    BIH_PUSH("r" Y, "s[54:55]", "v31", "v32", "s_add_u32 s65, s64, 16\n\t", "s65")  \
+    BIH_PUSH("r" Y, "s[54:55]", "v31", "v32", "s_add_u32 s65, s64, 16\n\t", "s65", RECR)  \
     ".LBIH_TL" Y "_%=:\n\t"                  /* take left: record in Y0 */             \
     "s_mov_b64 exec, s[52:53]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], %[tmin], v25, s[56:57]\n\t" /* [neg ? t0 : tMin,    */ \
@@ -278,7 +280,7 @@
     ".LBIH_BR" Y "_%=:\n\t"                                                           \
     "v_cndmask_b32_e64 v29, %[tmin], v25, s[56:57]\n\t"   /* left  [neg ? t0 : tMin, */ \
     "v_cndmask_b32_e64 v30, v25, %[tmax], s[56:57]\n\t"   /*        neg ? tMax : t0] */ \
-    BIH_PUSH("l" Y, "s[52:53]", "v29", "v30", "", "s64")                              \
+    BIH_PUSH("l" Y, "s[52:53]", "v29", "v30", "", "s64", RECL)                              \
     ".LBIH_TR" Y "_%=:\n\t"                  /* take right: record in Y1 */            \
     "s_mov_b64 exec, s[54:55]\n\t"                                                    \
     "v_cndmask_b32_e64 %[tmin], v26, %[tmin], s[56:57]\n\t" /* [neg ? tMin : t1,    */ \
@@ -296,7 +298,7 @@
 // s_set_gpr_idx_on leaves the slot index in M0[7:0], the lane v_writelane
 // selects.  Deep slots go to the wave's spill area in the out-of-line block
 // BIH_PUSH_SPILL(TAG) emits (which sets M0 itself).
-#define BIH_PUSH(TAG, MASK, LO, HI, NODE_SET, NODE)                                   \
+#define BIH_PUSH(TAG, MASK, LO, HI, NODE_SET, NODE, R)                                \
     "s_mov_b64 exec, -1\n\t"                                                          \
     "v_cndmask_b32_e64 v33, %[snan], " LO ", " MASK "\n\t"                            \
     "s_cmp_ge_u32 s63, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                  \
@@ -306,9 +308,50 @@
     "v_mov_b32_e32 v51, " HI "\n\t"                                                   \
     "s_set_gpr_idx_off\n\t"                                                           \
     ".LBIH_PN" TAG "_%=:\n\t"                                                         \
-    NODE_SET                                                                          \
-    "v_writelane_b32 v39, " NODE ", m0\n\t"                                           \
+    BIH_PUSH_NODE(NODE_SET, NODE, R)                                                  \
     "s_add_u32 s63, s63, 1\n\t"
+
+// The stacked node itself.  BIH_STACK_REC: its whole 16-byte record (already
+// in the pair buffer, R = its 4 SGPRs) goes to lane <slot> of v39/v65/v66/v67,
+// so a pop reads it back with v_readlane and starts the node step without a
+// load.  Else: its byte offset to lane <slot> of v39, and the pop loads it.
+#ifndef BIH_STACK_REC
+#define BIH_STACK_REC 0
+#endif
+#if BIH_STACK_REC
+#define BIH_PUSH_NODE(NODE_SET, NODE, R) R
+#define BIH_REC(R0, R1, R2, R3)                                                       \
+    "s_waitcnt lgkmcnt(0)\n\t"               /* the pair prefetch has landed */       \
+    "v_writelane_b32 v39, " R0 ", m0\n\t"                                             \
+    "v_writelane_b32 v65, " R1 ", m0\n\t"                                             \
+    "v_writelane_b32 v66, " R2 ", m0\n\t"                                             \
+    "v_writelane_b32 v67, " R3 ", m0\n\t"
+#define BIH_REC_CLOBBERS "v65", "v66", "v67",
+// Pop: EXEC = the entry's lanes, then its record straight into buffer A
+// (v_readlane ignores EXEC) and the node step A0.
+#define BIH_POP_NODE(ANY_TEXT)                                                        \
+    "s_nop 0\n\t"                                                                     \
+    "v_cmpx_ne_u32_e32 vcc, %[snan], %[tmin]\n\t"  /* EXEC = the entry's lanes */      \
+    ANY_TEXT                                                                          \
+    "v_readlane_b32 s76, v39, s63\n\t"                                                \
+    "v_readlane_b32 s77, v65, s63\n\t"                                                \
+    "v_readlane_b32 s78, v66, s63\n\t"                                                \
+    "v_readlane_b32 s79, v67, s63\n\t"                                                \
+    "s_nop 1\n\t"                                                                     \
+    "s_branch .LBIH_NBA0_%=\n\t"
+#else
+#define BIH_PUSH_NODE(NODE_SET, NODE, R) NODE_SET "v_writelane_b32 v39, " NODE ", m0\n\t"
+#define BIH_REC(R0, R1, R2, R3) ""
+#define BIH_REC_CLOBBERS
+// Pop: EXEC = the entry's lanes, its record's offset for the load at N.
+#define BIH_POP_NODE(ANY_TEXT)                                                        \
+    "s_nop 0\n\t"                                                                     \
+    "v_readlane_b32 s62, v39, s63\n\t"                                                \
+    "v_cmpx_ne_u32_e32 vcc, %[snan], %[tmin]\n\t"  /* EXEC = the entry's lanes */      \
+    ANY_TEXT                                                                          \
+    "s_nop 1\n\t"                                                                     \
+    "s_branch .LBIH_N_%=\n\t"
+#endif
 
 #define BIH_PUSH_SPILL(TAG, HI)                                                       \
     ".LBIH_SP" TAG "_%=:\n\t"                /* deep slot: wave spill area */         \
@@ -337,10 +380,10 @@
     /* ---- node steps: record buffers A = s[76:83], B = s[36:43] ---- */             \
     BIH_NODE_STEP("A0", CNT_NODE, "s76", "s77", "s78", "s79", "s[36:43]", "s_branch .LBIH_DB_%=\n\t") \
     BIH_NODE_STEP("A1", CNT_NODE, "s80", "s81", "s82", "s83", "s[36:43]", "")          \
-    BIH_DESCEND("B")                                                                  \
+    BIH_DESCEND("B", BIH_REC("s36", "s37", "s38", "s39"), BIH_REC("s40", "s41", "s42", "s43"))                                                                  \
     BIH_NODE_STEP("B0", CNT_NODE, "s36", "s37", "s38", "s39", "s[76:83]", "s_branch .LBIH_DA_%=\n\t") \
     BIH_NODE_STEP("B1", CNT_NODE, "s40", "s41", "s42", "s43", "s[76:83]", "")          \
-    BIH_DESCEND("A")                                                                  \
+    BIH_DESCEND("A", BIH_REC("s76", "s77", "s78", "s79"), BIH_REC("s80", "s81", "s82", "s83"))                                                                  \
     /* ---- pop until an entry has a searching lane ---- */                           \
     ".LBIH_P_%=:\n\t"                                                                 \
     "s_waitcnt lgkmcnt(0)\n\t"               /* a pair prefetch may be in flight */    \
@@ -355,13 +398,8 @@
     "v_mov_b32_e32 %[tmax], v51\n\t"                                                  \
     "s_set_gpr_idx_off\n\t"                                                           \
     ".LBIH_PQ_%=:\n\t"                                                                \
-    "s_nop 0\n\t"                                                                     \
-    "v_readlane_b32 s62, v39, s63\n\t"                                                \
-    "v_cmpx_ne_u32_e32 vcc, %[snan], %[tmin]\n\t"  /* EXEC = the entry's lanes */      \
-    ANY_TEXT                                                                          \
-    "s_nop 1\n\t"                                                                     \
-    "s_branch .LBIH_N_%=\n\t"                                                         \
-    ".LBIH_SQ_%=:\n\t"                                                                \
+    BIH_POP_NODE(ANY_TEXT)                                                            \
+    ".LBIH_SQ_%=:\n\t"                                                              \
     "s_sub_u32 s65, s63, " BIH_S(BIH_ASM_SLOTS) "\n\t"                                \
     "s_lshl_b32 s65, s65, 9\n\t"                                                      \
     "v_add_u32_e32 v35, s65, %[lane4]\n\t"                                            \
@@ -423,4 +461,4 @@
     "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
     "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
     "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", \
-    "v60", "v61", "v62", "v63", "v64", "vcc", "scc", "memory"
+    "v60", "v61", "v62", "v63", "v64", BIH_REC_CLOBBERS "vcc", "scc", "memory"

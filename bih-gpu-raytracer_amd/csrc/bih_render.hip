@@ -651,6 +651,8 @@ __global__ void __launch_bounds__(kThreads) k_render_pixel(const RenderArgs a) {
 #define BIH_PACKET_REGS 16
 #endif
 constexpr int kPacketRegs = BIH_PACKET_REGS;
+// child refs of the any-hit shortcut records (k_fast_refs)
+constexpr uint32_t kFastLeaf = 0x80000000u, kFastDead = 0xffffffffu;
 
 __device__ __forceinline__ unsigned long long lane_bit(uint32_t lane) { return 1ull << lane; }
 
@@ -1327,6 +1329,135 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
 }
 
 // ---------------------------------------------------------------------------
+// Any-hit shortcut, pass 1: the packet walks the shortcut boxes (k_fast_fit:
+// tight boxes of the alive triangles) near-first and tests leaves with the
+// exact intersector (prim_hits).  A lane stops at its first hit and keeps
+// that leaf in `cand`.  Returns the lanes with a candidate.  Nothing is
+// decided here: the candidate stands only if fast_verify passes.
+constexpr int kFastStack = 64;
+__device__ __forceinline__ unsigned long long fast_walk(const RenderArgs &a, const cprim_t *prims,
+                                                        const cu32_t *dupc, float dx, float dy,
+                                                        float dz, float ix, float iy, float iz,
+                                                        unsigned long long live, uint32_t lane,
+                                                        uint32_t *snode,
+                                                        unsigned long long *smask,
+                                                        uint32_t &cand) {
+    const cprim_t *fast = (const cprim_t *)(const void *)a.fast;
+    const unsigned long long me = lane_bit(lane);
+    unsigned long long found = 0ull;
+    uint32_t node = 0;
+    unsigned long long mask = live;
+    int sp = 0;
+    while (true) {
+        const sf32x16 r = fast[node];
+        const uint32_t ref0 = __float_as_uint(r[12]), ref1 = __float_as_uint(r[13]);
+        // slab test of both child boxes (camera-relative: t = box * inv)
+        const float a0 = r[0] * ix, a1 = r[3] * ix, b0 = r[1] * iy, b1 = r[4] * iy;
+        const float c0 = r[2] * iz, c1 = r[5] * iz;
+        const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fminf(c0, c1));
+        const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1));
+        const float d0 = r[6] * ix, d1 = r[9] * ix, e0 = r[7] * iy, e1 = r[10] * iy;
+        const float f0 = r[8] * iz, f1 = r[11] * iz;
+        const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fminf(f0, f1));
+        const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1));
+        unsigned long long m0 = ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0 && tf0 >= 0.f) & mask);
+        unsigned long long m1 = ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1 && tf1 >= 0.f) & mask);
+        // leaf children: test now (near one first)
+        const bool first1 = 2 * __popcll(__ballot(tn1 < tn0) & m0 & m1) > __popcll(m0 & m1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int s = q ^ (first1 ? 1 : 0);
+            const uint32_t ref = s ? ref1 : ref0;
+            unsigned long long ms = (s ? m1 : m0) & ~found;
+            if (!(ref & kFastLeaf) || ref == kFastDead || !ms) continue;
+            const uint32_t k = ref & ~kFastLeaf;
+            const uint32_t b = __float_as_uint(s ? r[15] : r[14]);
+            const uint32_t c = dupc[k];
+            for (uint32_t i = b; i < b + c && ms; ++i) {
+                const unsigned long long h = prim_hits(prims[i], dx, dy, dz, ms);
+                if (h & me) cand = k;
+                found |= h;
+                ms &= ~h;
+            }
+        }
+        if ((ref0 & kFastLeaf) || ref0 == kFastDead) m0 = 0ull;
+        if ((ref1 & kFastLeaf) || ref1 == kFastDead) m1 = 0ull;
+        m0 &= ~found;
+        m1 &= ~found;
+        if (m0 && m1) {
+            const uint32_t nf = first1 ? ref0 : ref1;
+            const unsigned long long mf = first1 ? m0 : m1;
+            if (sp < kFastStack) {
+                snode[sp] = nf;
+                smask[sp] = mf;
+                ++sp;
+            }   // (a full stack drops the subtree: its lanes run the exact walk)
+            node = first1 ? ref1 : ref0;
+            mask = first1 ? m1 : m0;
+        } else if (m0 | m1) {
+            node = m0 ? ref0 : ref1;
+            mask = m0 | m1;
+        } else {
+            mask = 0ull;
+            while (sp > 0) {
+                --sp;
+                mask = smask[sp] & ~found;
+                if (mask) {
+                    node = snode[sp];
+                    break;
+                }
+            }
+            if (!mask) break;
+        }
+        node = __builtin_amdgcn_readfirstlane(node);
+    }
+    return found;
+}
+
+// Any-hit shortcut, pass 2: does the reference's own walk reach leaf `k`?
+// Per lane, the exact BIH decisions of TraverseTree (CUDAKernels.cu:264-366)
+// along the root path of leaf k (left iff k <= split: the Karras ranges),
+// on the exact camera-relative records (k_node_prim): visit the near child
+// iff tMin < t[near], the far child iff !(tMax < t[far]), intervals [tMin,
+// t[near]] / [t[far], tMax] -- the same expressions as the packet walk's
+// (BIH_NODE_DEC, BIH_DESCEND).  Every leaf the reference reaches is fully
+// tested there, so a lane whose candidate triangle (an exact MT hit with
+// 0 < t < FLT_MAX) lies in a reached leaf is a hit of the reference.
+__device__ __forceinline__ bool fast_verify(const uint4 *__restrict__ rec, uint32_t k, float ix,
+                                            float iy, float iz, float lo, float hi) {
+    uint32_t n = 0;
+    for (int d = 0; d < 64; ++d) {
+        const uint4 r = rec[n];
+        const uint32_t ax = r.z & 0xffu, split = r.z >> 8;
+        const float inv = sel3(ax, ix, iy, iz);
+        const bool neg = 0.0f > inv;
+        const bool left = k <= split;
+        bool g;
+        float nlo, nhi;
+        if (left) {
+            const float t0 = __uint_as_float(r.x) * inv;
+            const float sL = neg ? hi : lo;
+            g = (t0 > sL) != neg;
+            nlo = neg ? t0 : lo;
+            nhi = neg ? hi : t0;
+        } else {
+            const float t1 = __uint_as_float(r.y) * inv;
+            const float sR = neg ? lo : hi;
+            g = (!(t1 > sR)) != neg;
+            nlo = neg ? lo : t1;
+            nhi = neg ? t1 : hi;
+        }
+        if (!g) return false;
+        lo = nlo;
+        hi = nhi;
+        const uint32_t c = split + (left ? 0u : 1u);
+        const bool leaf = left ? ((r.w >> 26) & 1u) : (r.w >> 31);
+        if (leaf) return c == k;
+        n = c;
+    }
+    return false;
+}
+
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
 // loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
 // offsets are 32-bit in the loop: used for scenes of < 2^26 triangles.
@@ -1359,6 +1490,8 @@ k_render_packet_asm(const RenderArgs a) {
     TileQueue queue = make_queue(a, tiles_x, (a.nrows + TH - 1) / TH);
     uint32_t tile = 0;
     (void)ntiles;
+    __shared__ uint32_t s_fnode[kThreads / 64][kFastStack];              // shortcut pass stack
+    __shared__ unsigned long long s_fmask[kThreads / 64][kFastStack];
 #if BIH_WAVE_TIMELINE
     const uint64_t tl_begin = __builtin_amdgcn_s_memrealtime();
     uint64_t tl_last = tl_begin;
@@ -1394,8 +1527,20 @@ k_render_packet_asm(const RenderArgs a) {
         if (tzmin > tMin) tMin = tzmin;
         if (tzmax < tMax) tMax = tzmax;
         uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
-        const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
-        unsigned long long hits = 0ull;
+        unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+        unsigned long long hits = 0ull, shortcut = 0ull;
+        if (ANYHIT && !STATS && a.fast && live && sc.U > 1) {
+            // any-hit shortcut: lanes whose shortcut hit the reference's walk
+            // provably reaches are done; the others take the exact walk below
+            uint32_t cand = 0;
+            const unsigned long long found =
+                fast_walk(a, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz, live, lane,
+                          s_fnode[wv], s_fmask[wv], cand);
+            const bool ok = ((found >> lane) & 1ull) &&
+                            fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
+            shortcut = __ballot(ok);
+            live &= ~shortcut;
+        }
         uint32_t nearbits = 0;
 #pragma unroll
         for (uint32_t k = 0; k < 3; ++k) {
@@ -1462,6 +1607,7 @@ k_render_packet_asm(const RenderArgs a) {
                              : BIH_PACKET_CLOBBERS);
             }
         }
+        hits |= shortcut;
 
         if (STATS && valid) {
             const uint64_t rid = lp * SPP + s;
@@ -1654,6 +1800,110 @@ __global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__
     o[3] = make_float4(tn, 0.f, 0.f, 0.f);
 }
 
+// ---------------------------------------------------------------------------
+// Shortcut boxes (the any-hit walk's first pass, k_render_packet_asm): per
+// internal node p a 64-byte record {box of child 0 (lo xyz, hi xyz), box of
+// child 1, ref 0, ref 1, first 0, first 1}, camera-relative (box - O), each
+// box the tight AABB of the child subtree's ALIVE triangles (tri_alive: the
+// only ones that can produce a hit from O).  ref = internal node index, or
+// kFastLeaf | leaf index, or kFastDead (no alive triangle below).  The
+// topology is the BIH's own (children {split, split+1}); only the culling
+// geometry differs.  Nothing here decides a pixel: a hit found through these
+// boxes is kept only after the exact BIH decisions are replayed along the
+// leaf's root path (fast_verify), every other lane runs the exact walk.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fbox_put(float *slot, const float lo[3], const float hi[3]) {
+    int32_t acc = 0;
+    int32_t *s = reinterpret_cast<int32_t *>(slot);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        acc ^= atomicExch(s + c, __float_as_int(lo[c]));
+        acc ^= atomicExch(s + 3 + c, __float_as_int(hi[c]));
+    }
+    asm volatile("" ::"v"(acc) : "memory");
+}
+__device__ __forceinline__ void fbox_get(float *slot, float lo[3], float hi[3]) {
+    int32_t *s = reinterpret_cast<int32_t *>(slot);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = __int_as_float(atomicOr(s + c, 0));
+        hi[c] = __int_as_float(atomicOr(s + 3 + c, 0));
+    }
+}
+
+// One thread per leaf: the leaf's box of alive triangles (empty: lo = +inf,
+// hi = -inf), then up the parent chain; the second arriver at a node unions
+// both slots and climbs on (the same hand-off as the builder's k_fit).
+__global__ void __launch_bounds__(kThreads) k_fast_fit(const float *__restrict__ tris,
+                                                       const float *__restrict__ prim,
+                                                       const int32_t *__restrict__ first,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       const int32_t *__restrict__ leaf_parent,
+                                                       const int32_t *__restrict__ parent,
+                                                       const uint4 *__restrict__ nodes, uint32_t U,
+                                                       float ox, float oy, float oz,
+                                                       uint32_t *__restrict__ arrive,
+                                                       float *fast) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (U < 2 || k >= U) return;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    const uint32_t b = (uint32_t)first[k], c = cnt[k];
+    const float o[3] = {ox, oy, oz};
+    for (uint32_t i = b; i < b + c; ++i) {
+        if (!tri_alive(prim, i)) continue;
+        const float *t = tris + 9ull * i;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v0 = t[a] - o[a], v1 = v0 + t[3 + a], v2 = v0 + t[6 + a];
+            lo[a] = fminf(lo[a], fminf(v0, fminf(v1, v2)));
+            hi[a] = fmaxf(hi[a], fmaxf(v0, fmaxf(v1, v2)));
+        }
+    }
+    int32_t prev = (int32_t)k;
+    bool prev_leaf = true;
+    int32_t p = leaf_parent[k];
+    while (p >= 0) {
+        const uint32_t z = nodes[p].z;
+        const uint32_t split = z & kIdxMask;
+        const bool leafL = (z >> 29) & 1u;
+        // child 0 is `split` (a leaf iff leafL), child 1 is split + 1
+        const int side = ((uint32_t)prev == split && prev_leaf == leafL) ? 0 : 1;
+        const int32_t pp = parent[p];
+        fbox_put(fast + 16ull * p + 6 * side, lo, hi);
+        if (atomicAdd(arrive + p, 1u) == 0u) return;
+        float slo[3], shi[3];
+        fbox_get(fast + 16ull * p + 6 * (1 - side), slo, shi);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { lo[a] = fminf(lo[a], slo[a]); hi[a] = fmaxf(hi[a], shi[a]); }
+        prev = p;
+        prev_leaf = false;
+        p = pp;
+    }
+}
+
+// Child refs of every record, once both boxes are in.
+__global__ void __launch_bounds__(kThreads) k_fast_refs(const uint4 *__restrict__ nodes, uint32_t m,
+                                                        const int32_t *__restrict__ first,
+                                                        float *__restrict__ fast) {
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= m) return;
+    const uint32_t z = nodes[p].z;
+    const uint32_t split = z & kIdxMask;
+    float *r = fast + 16ull * p;
+    uint32_t ref[2], fst[2] = {0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const bool leaf = (z >> (29 + s)) & 1u;
+        const bool dead = !(r[6 * s] <= r[6 * s + 3]);   // empty box (or never reached)
+        ref[s] = dead ? kFastDead : leaf ? (kFastLeaf | (split + s)) : (split + s);
+        if (leaf) fst[s] = (uint32_t)first[split + s];
+    }
+    r[12] = __uint_as_float(ref[0]);
+    r[13] = __uint_as_float(ref[1]);
+    r[14] = __uint_as_float(fst[0]);
+    r[15] = __uint_as_float(fst[1]);
+}
+
 std::mutex g_tab_mu;
 uint32_t *g_tab_dev[64] = {nullptr};
 
@@ -1773,13 +2023,18 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
 // one record of padding (the packet walk prefetches the record pair {split,
 // split+1}, and split+1 may be one past the last internal node), then the
 // leaf and node alive bytes
+size_t alive_bytes(uint32_t m) { return ((size_t)(m + 1) + m + 15) & ~(size_t)15; }
 size_t prim_bytes(uint32_t n, uint32_t m) {
-    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + (((size_t)(m + 1) + m + 15) & ~(size_t)15);
+    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + alive_bytes(m) + (size_t)(m + 1) * 64 +
+           (size_t)m * 4;
+}
+size_t fast_offset(uint32_t n, uint32_t m) {
+    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + alive_bytes(m);
 }
 
 int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
-                const uint32_t *dup_cnt, uint32_t m, const float origin[3], float *prim,
-                void *stream) {
+                const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
+                uint32_t m, const float origin[3], float *prim, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     if (n > 0)
         hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
@@ -1800,6 +2055,15 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
                                node_alive);
         hipLaunchKernelGGL(k_node_prim, gn, dim3(kThreads), 0, st, nodes, m, origin[0], origin[1],
                            origin[2], leaf_alive, node_alive, rec, rec + (m + 1));
+        // shortcut boxes of the any-hit walk's first pass
+        float *fast = reinterpret_cast<float *>(reinterpret_cast<char *>(prim) + fast_offset(n, m));
+        uint32_t *arrive = reinterpret_cast<uint32_t *>(fast + 16ull * (m + 1));
+        e = hipMemsetAsync(arrive, 0, sizeof(uint32_t) * m, st);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_fast_fit, gl, dim3(kThreads), 0, st, tris, prim, first_idx, dup_cnt,
+                           leaf_parent, parent, nodes, m + 1, origin[0], origin[1], origin[2],
+                           arrive, fast);
+        hipLaunchKernelGGL(k_fast_refs, gn, dim3(kThreads), 0, st, nodes, m, first_idx, fast);
     }
     return (int)hipGetLastError();
 }
