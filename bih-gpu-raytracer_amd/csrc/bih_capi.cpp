@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "../../include/bih.h"
@@ -62,7 +63,7 @@ struct bih_tree {
     float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
-    uint32_t prim_origin[3] = {0, 0, 0};   // bit patterns of the origin they were built for
+    uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
 };
 
 namespace {
@@ -111,14 +112,17 @@ int wait_renders(bih_tree *tr, hipStream_t st) {
 // does not end on one long packet.  The order never changes a pixel.
 // Called after `st` waits for the slot's previous render.  BIH_CHUNK_ORDER=0
 // turns it off (tuning / A-B).
-// The any-hit walk's shortcut pass (k_render_packet_asm, bih_render.hip):
-// on unless BIH_FAST=0 (A-B).  It never changes a pixel.
-bool fast_enabled() {
-    static const bool enabled = [] {
+// The any-hit walk's shortcut passes (k_render_packet_asm, bih_render.hip):
+// 2 = hit shortcut + miss proof (default), BIH_FAST=1 the hit shortcut only,
+// BIH_FAST=0 neither (A-B).  They never change a pixel.
+int fast_enabled() {
+    static const int level = [] {
         const char *e = getenv("BIH_FAST");
-        return !(e && strcmp(e, "0") == 0);
+        if (e && strcmp(e, "0") == 0) return 0;
+        if (e && strcmp(e, "1") == 0) return 1;
+        return 2;
     }();
-    return enabled;
+    return level;
 }
 
 int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &rows, int slot,
@@ -495,11 +499,13 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     hipError_t e = hipEventRecord(tr->ev_rng, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
-    // primary-ray triangle records follow the camera origin
+    // primary-ray records follow the camera (the origin; the miss-proof boxes
+    // also the direction bounds)
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
     if (bih::render_uses_prim(spp) && tr->t.n > 0) {
-        uint32_t ob[3];
-        memcpy(ob, cam->origin, sizeof ob);
+        uint32_t ob[12];
+        static_assert(sizeof(bih_camera) == sizeof ob, "bih_camera is 12 f32");
+        memcpy(ob, cam, sizeof ob);
         const size_t need = bih::prim_bytes(tr->t.n, n_int);
         const bool grow = tr->prim_cap < need;
         if (grow || !tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
@@ -519,10 +525,23 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             tr->prim_valid = false;
         }
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
+            // |D| per component over the primary rays: D = (llc + u h + v vert) - O
+            // (Camera.cu:18-20) is affine in (u, v) in [0, 1]^2, so its largest
+            // magnitude is at a corner; slack for the f32 evaluation
+            float dmax[3];
+            for (int c = 0; c < 3; ++c) {
+                float mx = 0.0f;
+                for (int k = 0; k < 4; ++k) {
+                    const float u = (float)(k & 1), v = (float)(k >> 1);
+                    const float d = ((cam->lower_left[c] + u * cam->horizontal[c]) +
+                                     v * cam->vertical[c]) - cam->origin[c];
+                    mx = std::max(mx, std::fabs(d));
+                }
+                dmax[c] = mx * 1.001f + 1e-6f;
+            }
             int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
                                       tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
-                                      cam->origin,
-                                      tr->prim, st);
+                                      cam->origin, dmax, tr->prim, st);
             if (le) return map_hip(le);
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
@@ -551,9 +570,11 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
     a.node_cull = a.node_prim ? a.node_prim + (n_int + 1) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
-    if (tr->prim && n_int > 0 && fast_enabled())
+    if (tr->prim && n_int > 0 && fast_enabled() > 0) {
         a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
                                                  bih::fast_offset(tr->t.n, n_int));
+        if (fast_enabled() > 1) a.fast2 = a.fast + 16ull * (n_int + 1);
+    }
     a.rng_in = rng_buf(tr, cur);
     a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;
     a.out = d_out;

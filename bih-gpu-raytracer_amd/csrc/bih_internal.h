@@ -79,6 +79,7 @@ struct RenderArgs {
     const uint32_t *chunk_order = nullptr;  // packet kernel: chunk permutation (launch_chunk_order)
     uint32_t *chunk_cost = nullptr;         // packet kernel: per-chunk cycle accumulator (zeroed)
     const float *fast = nullptr;            // any-hit shortcut boxes (k_fast_fit); null: exact walk only
+    const float *fast2 = nullptr;           // miss-proof boxes (miss_box); null: no miss proof
 };
 
 // Device buffers of one tree.
@@ -131,14 +132,15 @@ int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks
 // primary-ray records for camera origin `origin`: n triangle records
 // (16 f32, k_tri_prim), then m = U-1 node records (u32x4, k_node_prim) + 1
 // pad, then the same m + 1 records with unhittable subtrees cut off, then
-// per-leaf and per-node alive bytes, then the any-hit walk's shortcut boxes
-// (m + 1 records of 16 x 32 bit, k_fast_fit / k_fast_refs) and m arrival
-// counters
+// per-leaf and per-node alive bytes, then the any-hit walk's two shortcut
+// box sets (m + 1 records of 16 x 32 bit each, k_fast_fit / k_fast_refs:
+// tight, then miss-proof for |D| <= dmax per component) and m arrival counters
 size_t prim_bytes(uint32_t n, uint32_t m);
 size_t fast_offset(uint32_t n, uint32_t m);   // byte offset of the shortcut boxes
 int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
                 const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
-                uint32_t m, const float origin[3], float *prim, void *stream);
+                uint32_t m, const float origin[3], const float dmax[3], float *prim,
+                void *stream);
 bool render_uses_prim(uint32_t spp);
 
 // host XORWOW helpers (xorwow_host.cpp)

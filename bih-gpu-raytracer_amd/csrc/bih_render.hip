@@ -1329,20 +1329,27 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
 }
 
 // ---------------------------------------------------------------------------
-// Any-hit shortcut, pass 1: the packet walks the shortcut boxes (k_fast_fit:
-// tight boxes of the alive triangles) near-first and tests leaves with the
-// exact intersector (prim_hits).  A lane stops at its first hit and keeps
-// that leaf in `cand`.  Returns the lanes with a candidate.  Nothing is
-// decided here: the candidate stands only if fast_verify passes.
+// Any-hit shortcut walk over one shortcut box set (k_fast_fit): the packet
+// walks the boxes near-first and tests leaves with the exact intersector
+// (prim_hits).  A lane stops at its first hit and keeps that leaf in `cand`.
+// Returns the lanes with a candidate.  Nothing is decided here: a candidate
+// stands only if fast_verify passes.
+//   pass 1 (tight boxes, cons = false): finds the hits of most lanes fast;
+//   pass 2 (miss-proof boxes, miss_box; cons = true): the whole line is
+//     tested against every box, so a lane of `live` that ends with no
+//     candidate and not in `incomplete` (its subtree dropped by a full stack)
+//     has no triangle the exact intersector accepts: a reference miss.
 constexpr int kFastStack = 64;
-__device__ __forceinline__ unsigned long long fast_walk(const RenderArgs &a, const cprim_t *prims,
+__device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool cons,
+                                                        const cprim_t *prims,
                                                         const cu32_t *dupc, float dx, float dy,
                                                         float dz, float ix, float iy, float iz,
                                                         unsigned long long live, uint32_t lane,
                                                         uint32_t *snode,
                                                         unsigned long long *smask,
-                                                        uint32_t &cand) {
-    const cprim_t *fast = (const cprim_t *)(const void *)a.fast;
+                                                        uint32_t &cand,
+                                                        unsigned long long &incomplete) {
+    const cprim_t *fast = (const cprim_t *)(const void *)boxes;
     const unsigned long long me = lane_bit(lane);
     unsigned long long found = 0ull;
     uint32_t node = 0;
@@ -1360,8 +1367,10 @@ __device__ __forceinline__ unsigned long long fast_walk(const RenderArgs &a, con
         const float f0 = r[8] * iz, f1 = r[11] * iz;
         const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fminf(f0, f1));
         const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1));
-        unsigned long long m0 = ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0 && tf0 >= 0.f) & mask);
-        unsigned long long m1 = ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1 && tf1 >= 0.f) & mask);
+        unsigned long long m0 =
+            ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0 && (cons || tf0 >= 0.f)) & mask);
+        unsigned long long m1 =
+            ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1 && (cons || tf1 >= 0.f)) & mask);
         // leaf children: test now (near one first)
         const bool first1 = 2 * __popcll(__ballot(tn1 < tn0) & m0 & m1) > __popcll(m0 & m1);
 #pragma unroll
@@ -1391,7 +1400,9 @@ __device__ __forceinline__ unsigned long long fast_walk(const RenderArgs &a, con
                 snode[sp] = nf;
                 smask[sp] = mf;
                 ++sp;
-            }   // (a full stack drops the subtree: its lanes run the exact walk)
+            } else {
+                incomplete |= mf;   // a full stack drops the subtree: exact walk
+            }
             node = first1 ? ref1 : ref0;
             mask = first1 ? m1 : m0;
         } else if (m0 | m1) {
@@ -1533,13 +1544,31 @@ k_render_packet_asm(const RenderArgs a) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
             // provably reaches are done; the others take the exact walk below
             uint32_t cand = 0;
+            unsigned long long inc = 0ull;
             const unsigned long long found =
-                fast_walk(a, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz, live, lane,
-                          s_fnode[wv], s_fmask[wv], cand);
+                fast_walk(a.fast, false, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
+                          live, lane, s_fnode[wv], s_fmask[wv], cand, inc);
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
             shortcut = __ballot(ok);
             live &= ~shortcut;
+            // miss proof for the rest (lanes with an infinite 1/D component
+            // keep the exact walk: 0 * inf in a slab test)
+            const unsigned long long m2 =
+                a.fast2 ? live & __ballot(__builtin_isfinite(ix) && __builtin_isfinite(iy) &&
+                                          __builtin_isfinite(iz))
+                        : 0ull;
+            if (m2) {
+                inc = 0ull;
+                const unsigned long long found2 =
+                    fast_walk(a.fast2, true, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
+                              m2, lane, s_fnode[wv], s_fmask[wv], cand, inc);
+                const bool ok2 = ((found2 >> lane) & 1ull) &&
+                                 fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
+                const unsigned long long hit2 = __ballot(ok2);
+                shortcut |= hit2;
+                live &= ~(hit2 | (m2 & ~found2 & ~inc));   // proven misses are done too
+            }
         }
         uint32_t nearbits = 0;
 #pragma unroll
@@ -1831,6 +1860,66 @@ __device__ __forceinline__ void fbox_get(float *slot, float lo[3], float hi[3]) 
     }
 }
 
+// Miss-proof box of one alive triangle (camera-relative), from its primary-ray
+// record r = {e1, e2, s = O - v0, q = cross(s, e1), tnum} and dmax[] >= |D|
+// per component for every primary ray of the camera.  Claim: if the exact
+// intersector (RayTriangleIntersection, CUDAKernels.cu:17-50, as the kernels
+// evaluate it: f32, no contraction) returns a hit for direction D, the line
+// O + t D passes through this box.  Proof sketch: the exact line meets the
+// plane of the triangle {v0' + u e1 + v e2} (v0' = O - s, the f32 values MT
+// uses) at barycentrics u* = s.p/det*, v* = D.q/det*, p = D x e2.  The f32
+// evaluation errs by at most (unit roundoff e = 2^-24, first order):
+//   |p_c - p| <= 2e P,  P = (|dy||e2z| + |e2y||dz|, ...)   (abs cross product)
+//   |un_c - s.p|   <= 5e |s|.P     =: Eu
+//   |det_c - e1.p| <= 5e |e1|.P    =: Ed
+//   |vn_c - D.q|   <= 5e |D|.Q     =: Ev,  Q = abs cross(|s|, |e1|) (q_c's own
+//                                           rounding included)
+// A hit has det_c > 1e-6 (kDetEps), u_c in [0, 1], v_c >= 0, u_c + v_c <= 1,
+// so with den = 0.99e-6 - Ed > 0:  u* >= -(4e + Eu/den) =: -a,
+// v* >= -(4e + Ev/den) =: -b,  u* + v* <= 1 + 8e + 1.01 (Eu + Ev + 2 Ed)/den =: 1 + c.
+// The point lies in the triangle of barycentric corners (-a, -b), (1+b+c, -b),
+// (-a, 1+a+c); the box is that triangle's AABB padded by 1e-5 + 1e-6|x| (far
+// more than the slab test's own rounding).  The constants are taken 8e, not 5e.
+// A non-finite bound or den <= 0.5e-6 gives the unbounded box.
+__device__ __forceinline__ void miss_box(const float *r, const float *dmax, float lo[3],
+                                         float hi[3]) {
+    const float E = 8.0f * 0x1p-24f;
+    const float e1[3] = {r[0], r[1], r[2]}, e2[3] = {r[3], r[4], r[5]};
+    const float sv[3] = {r[6], r[7], r[8]};
+    const float ae1[3] = {fabsf(e1[0]), fabsf(e1[1]), fabsf(e1[2])};
+    const float ae2[3] = {fabsf(e2[0]), fabsf(e2[1]), fabsf(e2[2])};
+    const float as[3] = {fabsf(sv[0]), fabsf(sv[1]), fabsf(sv[2])};
+    const float P[3] = {dmax[1] * ae2[2] + ae2[1] * dmax[2], dmax[2] * ae2[0] + ae2[2] * dmax[0],
+                        dmax[0] * ae2[1] + ae2[0] * dmax[1]};
+    const float Q[3] = {as[1] * ae1[2] + ae1[1] * as[2], as[2] * ae1[0] + ae1[2] * as[0],
+                        as[0] * ae1[1] + ae1[0] * as[1]};
+    const float Eu = E * (as[0] * P[0] + as[1] * P[1] + as[2] * P[2]);
+    const float Ed = E * (ae1[0] * P[0] + ae1[1] * P[1] + ae1[2] * P[2]);
+    const float Ev = E * (dmax[0] * Q[0] + dmax[1] * Q[1] + dmax[2] * Q[2]);
+    const float den = 0.99e-6f - Ed;
+    const float a = 4.0f * E + Eu / den, bb = 4.0f * E + Ev / den;
+    const float c = 8.0f * E + 1.01f * (Eu + Ev + 2.0f * Ed) / den;
+    bool ok = den > 0.5e-6f && a < 1e30f && bb < 1e30f && c < 1e30f;
+    const float cu[3] = {-a, 1.0f + bb + c, -a}, cv[3] = {-bb, -bb, 1.0f + a + c};
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+        float l = INFINITY, h = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float x = (cu[j] * e1[ax] + cv[j] * e2[ax]) - sv[ax];
+            l = fminf(l, x);
+            h = fmaxf(h, x);
+        }
+        lo[ax] = l - (1e-5f + 1e-6f * fabsf(l));
+        hi[ax] = h + (1e-5f + 1e-6f * fabsf(h));
+        ok = ok && lo[ax] > -1e30f && hi[ax] < 1e30f;
+    }
+    if (!ok) {
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) { lo[ax] = -INFINITY; hi[ax] = INFINITY; }
+    }
+}
+
 // One thread per leaf: the leaf's box of alive triangles (empty: lo = +inf,
 // hi = -inf), then up the parent chain; the second arriver at a node unions
 // both slots and climbs on (the same hand-off as the builder's k_fit).
@@ -1842,6 +1931,7 @@ __global__ void __launch_bounds__(kThreads) k_fast_fit(const float *__restrict__
                                                        const int32_t *__restrict__ parent,
                                                        const uint4 *__restrict__ nodes, uint32_t U,
                                                        float ox, float oy, float oz,
+                                                       bool cons, float dmx, float dmy, float dmz,
                                                        uint32_t *__restrict__ arrive,
                                                        float *fast) {
     const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
@@ -1851,12 +1941,23 @@ __global__ void __launch_bounds__(kThreads) k_fast_fit(const float *__restrict__
     const float o[3] = {ox, oy, oz};
     for (uint32_t i = b; i < b + c; ++i) {
         if (!tri_alive(prim, i)) continue;
-        const float *t = tris + 9ull * i;
+        float tlo[3], thi[3];
+        if (cons) {
+            const float dmax[3] = {dmx, dmy, dmz};
+            miss_box(prim + 16ull * i, dmax, tlo, thi);
+        } else {
+            const float *t = tris + 9ull * i;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float v0 = t[a] - o[a], v1 = v0 + t[3 + a], v2 = v0 + t[6 + a];
+                tlo[a] = fminf(v0, fminf(v1, v2));
+                thi[a] = fmaxf(v0, fmaxf(v1, v2));
+            }
+        }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float v0 = t[a] - o[a], v1 = v0 + t[3 + a], v2 = v0 + t[6 + a];
-            lo[a] = fminf(lo[a], fminf(v0, fminf(v1, v2)));
-            hi[a] = fmaxf(hi[a], fmaxf(v0, fmaxf(v1, v2)));
+            lo[a] = fminf(lo[a], tlo[a]);
+            hi[a] = fmaxf(hi[a], thi[a]);
         }
     }
     int32_t prev = (int32_t)k;
@@ -2025,8 +2126,8 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
 // leaf and node alive bytes
 size_t alive_bytes(uint32_t m) { return ((size_t)(m + 1) + m + 15) & ~(size_t)15; }
 size_t prim_bytes(uint32_t n, uint32_t m) {
-    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + alive_bytes(m) + (size_t)(m + 1) * 64 +
-           (size_t)m * 4;
+    return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + alive_bytes(m) +
+           2 * (size_t)(m + 1) * 64 + (size_t)m * 4;
 }
 size_t fast_offset(uint32_t n, uint32_t m) {
     return (size_t)n * 64 + 2 * (size_t)(m + 1) * 16 + alive_bytes(m);
@@ -2034,7 +2135,8 @@ size_t fast_offset(uint32_t n, uint32_t m) {
 
 int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
                 const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
-                uint32_t m, const float origin[3], float *prim, void *stream) {
+                uint32_t m, const float origin[3], const float dmax[3], float *prim,
+                void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     if (n > 0)
         hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
@@ -2055,15 +2157,18 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
                                node_alive);
         hipLaunchKernelGGL(k_node_prim, gn, dim3(kThreads), 0, st, nodes, m, origin[0], origin[1],
                            origin[2], leaf_alive, node_alive, rec, rec + (m + 1));
-        // shortcut boxes of the any-hit walk's first pass
+        // shortcut boxes of the any-hit walk: tight (pass 1), miss-proof (pass 2)
         float *fast = reinterpret_cast<float *>(reinterpret_cast<char *>(prim) + fast_offset(n, m));
-        uint32_t *arrive = reinterpret_cast<uint32_t *>(fast + 16ull * (m + 1));
-        e = hipMemsetAsync(arrive, 0, sizeof(uint32_t) * m, st);
-        if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(k_fast_fit, gl, dim3(kThreads), 0, st, tris, prim, first_idx, dup_cnt,
-                           leaf_parent, parent, nodes, m + 1, origin[0], origin[1], origin[2],
-                           arrive, fast);
-        hipLaunchKernelGGL(k_fast_refs, gn, dim3(kThreads), 0, st, nodes, m, first_idx, fast);
+        uint32_t *arrive = reinterpret_cast<uint32_t *>(fast + 2 * 16ull * (m + 1));
+        for (int pass = 0; pass < 2; ++pass) {
+            float *boxes = fast + pass * 16ull * (m + 1);
+            e = hipMemsetAsync(arrive, 0, sizeof(uint32_t) * m, st);
+            if (e != hipSuccess) return (int)e;
+            hipLaunchKernelGGL(k_fast_fit, gl, dim3(kThreads), 0, st, tris, prim, first_idx,
+                               dup_cnt, leaf_parent, parent, nodes, m + 1, origin[0], origin[1],
+                               origin[2], pass == 1, dmax[0], dmax[1], dmax[2], arrive, boxes);
+            hipLaunchKernelGGL(k_fast_refs, gn, dim3(kThreads), 0, st, nodes, m, first_idx, boxes);
+        }
     }
     return (int)hipGetLastError();
 }

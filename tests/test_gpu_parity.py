@@ -292,3 +292,48 @@ def test_frames_in_flight_on_two_streams(gpu, bihrt_mod, oracle_mod):
     for k, f in enumerate(frames):
         ref, _ = ot.render(w, h, frame=f)
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32).reshape(h, w), ref), (k, f)
+
+
+def _grazing_scene(n, seed):
+    """Triangles seen almost edge-on: the view ray through each triangle's
+    centre meets its plane at an angle of 1e-4 .. 0.3 rad, so det of the
+    rays that cross it sits near the 1e-6 threshold, where the intersector's
+    rounding is at its worst (the miss-proof boxes' error bound)."""
+    rng = np.random.default_rng(seed)
+    O = np.array([2.0, 0.0, -2.0])
+    P = np.stack([rng.uniform(0.0, 2.6667, n), rng.uniform(-1, 1, n), rng.uniform(0, 2, n)], 1)
+    d = P - O
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    side = np.cross(d, rng.normal(size=(n, 3)))
+    side /= np.linalg.norm(side, axis=1, keepdims=True)
+    normal = np.cross(d, side)
+    th = 10.0 ** rng.uniform(-4, -0.5, n)[:, None]
+    wdir = np.cos(th) * d + np.sin(th) * normal
+    size = rng.uniform(0.01, 0.06, (n, 1))
+    v0 = P - 0.5 * size * (wdir + side)
+    v1 = v0 + size * wdir
+    v2 = v0 + size * side
+    flip = rng.random(n) < 0.5
+    v1[flip], v2[flip] = v2[flip].copy(), v1[flip].copy()
+    return np.concatenate([v0, v1, v2], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("scene", ["soup200k", "grazing", "grazing_dense", "torus", "clustered",
+                                   "cornell", "signed_zero", "flat_z"])
+def test_anyhit_shortcut_matches_exact_walk(scene, gpu, bihrt_mod):
+    """The any-hit shortcut passes (tight-box hit + root-path check, and the
+    miss-proof boxes) against the exact BIH walk of the same kernel family,
+    every pixel of several frames: the reference traversal
+    (TRAVERSE_REFERENCE) never takes a shortcut."""
+    S = bihrt_mod.scenes
+    tris = {"soup200k": lambda: S.soup(200_000, seed=11),
+            "grazing": lambda: _grazing_scene(20_000, 1),
+            "grazing_dense": lambda: np.concatenate([_grazing_scene(60_000, 2),
+                                                     S.soup(60_000, seed=12)]),
+            "torus": S.torus}.get(scene, lambda: SCENES[scene])()
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 480, 270
+    for frame in (0, 3):
+        a = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_ANYHIT)
+        b = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_REFERENCE)
+        assert np.array_equal(a, b), (scene, frame, int((a != b).sum()))
