@@ -659,6 +659,22 @@ int bih_sync(const bih_tree *tr, void *stream) {
         }
     }
 #endif
+#if BIH_FAST_COUNTERS
+    if (tr->work && tr->last_slot >= 0) {
+        uint32_t c[64];
+        if (hipMemcpyAsync(c, tr->work + (size_t)tr->last_slot * bih::kWorkWords, sizeof c,
+                           hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            const unsigned long long *cy = reinterpret_cast<const unsigned long long *>(c + 32);
+            fprintf(stderr,
+                    "fast-counters packets %u lanes %u | pass1 steps %u tests %u cand %u verified %u"
+                    " | pass2 packets %u steps %u tests %u verified %u proven-miss %u incomplete %u"
+                    " | exact packets %u lanes %u | cycles pass1 %llu pass2 %llu exact %llu\n",
+                    c[16], c[17], c[18], c[19], c[20], c[21], c[22], c[23], c[24], c[25], c[26],
+                    c[27], c[28], c[29], cy[0], cy[1], cy[2]);
+        }
+    }
+#endif
 #if BIH_PACKET_COUNTERS
     if (tr->work && tr->last_slot >= 0) {
         uint32_t c[bih::kWorkWords];

@@ -1340,6 +1340,45 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
 //     candidate and not in `incomplete` (its subtree dropped by a full stack)
 //     has no triangle the exact intersector accepts: a reference miss.
 constexpr int kFastStack = 64;
+// Entry/exit parameters of the line O + t D against a camera-relative box,
+// entry clamped below at cl.  Plain v_min/v_max (no NaN canonicalisation):
+// no operand is NaN -- boxes are finite or +-inf, |1/D| >= 1/|D|max > 0 --
+// and pass 2 only runs lanes with finite 1/D.
+__device__ __forceinline__ void slab_t(float lx, float ly, float lz, float hx, float hy, float hz,
+                                       float ix, float iy, float iz, float cl, float &tn,
+                                       float &tf) {
+    const float a0 = lx * ix, a1 = hx * ix, b0 = ly * iy, b1 = hy * iy;
+    const float c0 = lz * iz, c1 = hz * iz;
+    float n0, n1, n2, f0, f1, f2;
+    asm("v_min_f32 %[n0], %[a0], %[a1]\n\t"
+        "v_max_f32 %[f0], %[a0], %[a1]\n\t"
+        "v_min_f32 %[n1], %[b0], %[b1]\n\t"
+        "v_max_f32 %[f1], %[b0], %[b1]\n\t"
+        "v_min_f32 %[n2], %[c0], %[c1]\n\t"
+        "v_max_f32 %[f2], %[c0], %[c1]\n\t"
+        "v_max3_f32 %[n0], %[n0], %[n1], %[n2]\n\t"
+        "v_min3_f32 %[f0], %[f0], %[f1], %[f2]\n\t"
+        "v_max_f32 %[n0], %[cl], %[n0]"
+        : [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [f0] "=&v"(f0), [f1] "=&v"(f1),
+          [f2] "=&v"(f2)
+        : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1),
+          [cl] "s"(cl));
+    tn = n0;
+    tf = f0;
+}
+#ifndef BIH_FAST_PF
+#define BIH_FAST_PF 0   // child-pair prefetch in the shortcut walk (slower: 1.08 -> 1.43 ms)
+#endif
+// BIH_FAST_COUNTERS builds: per-frame work of the shortcut passes in
+// work[16..32) and their cycles in work[32..38) (printed by bih_sync)
+#ifndef BIH_FAST_COUNTERS
+#define BIH_FAST_COUNTERS 0
+#endif
+#if BIH_FAST_COUNTERS
+#define BIH_FC(x) x
+#else
+#define BIH_FC(x)
+#endif
 __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool cons,
                                                         const cprim_t *prims,
                                                         const cu32_t *dupc, float dx, float dy,
@@ -1348,29 +1387,36 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                                                         uint32_t *snode,
                                                         unsigned long long *smask,
                                                         uint32_t &cand,
-                                                        unsigned long long &incomplete) {
+                                                        unsigned long long &incomplete,
+                                                        uint32_t &fc_steps, uint32_t &fc_tests) {
     const cprim_t *fast = (const cprim_t *)(const void *)boxes;
     const unsigned long long me = lane_bit(lane);
     unsigned long long found = 0ull;
     uint32_t node = 0;
     unsigned long long mask = live;
     int sp = 0;
+    sf32x16 r = fast[0];
     while (true) {
-        const sf32x16 r = fast[node];
+        BIH_FC(++fc_steps);
         const uint32_t ref0 = __float_as_uint(r[12]), ref1 = __float_as_uint(r[13]);
-        // slab test of both child boxes (camera-relative: t = box * inv)
-        const float a0 = r[0] * ix, a1 = r[3] * ix, b0 = r[1] * iy, b1 = r[4] * iy;
-        const float c0 = r[2] * iz, c1 = r[5] * iz;
-        const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fminf(c0, c1));
-        const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1));
-        const float d0 = r[6] * ix, d1 = r[9] * ix, e0 = r[7] * iy, e1 = r[10] * iy;
-        const float f0 = r[8] * iz, f1 = r[11] * iz;
-        const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fminf(f0, f1));
-        const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1));
-        unsigned long long m0 =
-            ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0 && (cons || tf0 >= 0.f)) & mask);
-        unsigned long long m1 =
-            ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1 && (cons || tf1 >= 0.f)) & mask);
+#if BIH_FAST_PF
+        // the internal children {split, split + 1} have adjacent records: both
+        // are requested before this node's tests (one of them is next)
+        const uint32_t pb = (ref0 & kFastLeaf) ? ref1 - 1u : ref0;
+        sf32x16 rA = r, rB = r;
+        if (!(ref0 & ref1 & kFastLeaf)) {
+            rA = fast[pb];
+            rB = fast[pb + 1];
+        }
+#endif
+        // slab test of both child boxes (camera-relative: t = box * inv); pass
+        // 1 clamps the entry at t = 0 (the ray), pass 2 tests the whole line
+        const float cl = cons ? -INFINITY : 0.0f;
+        float tn0, tf0, tn1, tf1;
+        slab_t(r[0], r[1], r[2], r[3], r[4], r[5], ix, iy, iz, cl, tn0, tf0);
+        slab_t(r[6], r[7], r[8], r[9], r[10], r[11], ix, iy, iz, cl, tn1, tf1);
+        unsigned long long m0 = ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0) & mask);
+        unsigned long long m1 = ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1) & mask);
         // leaf children: test now (near one first)
         const bool first1 = 2 * __popcll(__ballot(tn1 < tn0) & m0 & m1) > __popcll(m0 & m1);
 #pragma unroll
@@ -1380,12 +1426,14 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
             unsigned long long ms = (s ? m1 : m0) & ~found;
             if (!(ref & kFastLeaf) || ref == kFastDead || !ms) continue;
             const uint32_t k = ref & ~kFastLeaf;
-            const uint32_t b = __float_as_uint(s ? r[15] : r[14]);
-            const uint32_t c = dupc[k];
+            const uint32_t fc = __float_as_uint(s ? r[15] : r[14]);
+            const uint32_t b = fc & 0x3ffffffu;
+            const uint32_t c = (fc >> 26) == 63u ? dupc[k] : (fc >> 26);
             for (uint32_t i = b; i < b + c && ms; ++i) {
                 const unsigned long long h = prim_hits(prims[i], dx, dy, dz, ms);
                 if (h & me) cand = k;
                 found |= h;
+                BIH_FC(++fc_tests);
                 ms &= ~h;
             }
         }
@@ -1419,8 +1467,16 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                 }
             }
             if (!mask) break;
+            node = __builtin_amdgcn_readfirstlane(node);
+            r = fast[node];
+            continue;
         }
         node = __builtin_amdgcn_readfirstlane(node);
+#if BIH_FAST_PF
+        r = node == pb ? rA : rB;
+#else
+        r = fast[node];
+#endif
     }
     return found;
 }
@@ -1540,18 +1596,26 @@ k_render_packet_asm(const RenderArgs a) {
         uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
         unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
         unsigned long long hits = 0ull, shortcut = 0ull;
+#if BIH_FAST_COUNTERS
+        uint64_t fc_walk0 = __builtin_amdgcn_s_memtime();
+#endif
         if (ANYHIT && !STATS && a.fast && live && sc.U > 1) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
             // provably reaches are done; the others take the exact walk below
-            uint32_t cand = 0;
+            uint32_t cand = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0;
             unsigned long long inc = 0ull;
+            (void)s1, (void)n1, (void)s2, (void)n2;
+            BIH_FC(const uint64_t fc_t0 = __builtin_amdgcn_s_memtime());
             const unsigned long long found =
                 fast_walk(a.fast, false, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                          live, lane, s_fnode[wv], s_fmask[wv], cand, inc);
+                          live, lane, s_fnode[wv], s_fmask[wv], cand, inc, s1, n1);
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
             shortcut = __ballot(ok);
+            BIH_FC(const unsigned long long fc_live0 = live);
+            BIH_FC(const uint32_t fc_v1 = (uint32_t)__popcll(shortcut));
             live &= ~shortcut;
+            BIH_FC(const uint64_t fc_t1 = __builtin_amdgcn_s_memtime());
             // miss proof for the rest (lanes with an infinite 1/D component
             // keep the exact walk: 0 * inf in a slab test)
             const unsigned long long m2 =
@@ -1562,13 +1626,38 @@ k_render_packet_asm(const RenderArgs a) {
                 inc = 0ull;
                 const unsigned long long found2 =
                     fast_walk(a.fast2, true, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                              m2, lane, s_fnode[wv], s_fmask[wv], cand, inc);
+                              m2, lane, s_fnode[wv], s_fmask[wv], cand, inc, s2, n2);
                 const bool ok2 = ((found2 >> lane) & 1ull) &&
                                  fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
                 const unsigned long long hit2 = __ballot(ok2);
                 shortcut |= hit2;
                 live &= ~(hit2 | (m2 & ~found2 & ~inc));   // proven misses are done too
+                BIH_FC(if (lane == 0) {
+                    atomicAdd(a.work + 22, 1u);
+                    atomicAdd(a.work + 23, s2);
+                    atomicAdd(a.work + 24, n2);
+                    atomicAdd(a.work + 25, (uint32_t)__popcll(hit2));
+                    atomicAdd(a.work + 26, (uint32_t)__popcll(m2 & ~found2 & ~inc));
+                    atomicAdd(a.work + 27, (uint32_t)__popcll(inc));
+                })
             }
+#if BIH_FAST_COUNTERS
+            const uint64_t fc_t2 = __builtin_amdgcn_s_memtime();
+            if (lane == 0) {
+                unsigned long long *cy = reinterpret_cast<unsigned long long *>(a.work + 32);
+                atomicAdd(a.work + 16, 1u);
+                atomicAdd(a.work + 17, (uint32_t)__popcll(fc_live0));
+                atomicAdd(a.work + 18, s1);
+                atomicAdd(a.work + 19, n1);
+                atomicAdd(a.work + 20, (uint32_t)__popcll(found));
+                atomicAdd(a.work + 21, fc_v1);
+                atomicAdd(a.work + 28, live ? 1u : 0u);
+                atomicAdd(a.work + 29, (uint32_t)__popcll(live));
+                atomicAdd(cy, (unsigned long long)(fc_t1 - fc_t0));
+                atomicAdd(cy + 1, (unsigned long long)(fc_t2 - fc_t1));
+            }
+            fc_walk0 = __builtin_amdgcn_s_memtime();
+#endif
         }
         uint32_t nearbits = 0;
 #pragma unroll
@@ -1637,6 +1726,11 @@ k_render_packet_asm(const RenderArgs a) {
             }
         }
         hits |= shortcut;
+#if BIH_FAST_COUNTERS
+        if (lane == 0 && live)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.work + 32) + 2,
+                      (unsigned long long)(__builtin_amdgcn_s_memtime() - fc_walk0));
+#endif
 
         if (STATS && valid) {
             const uint64_t rid = lp * SPP + s;
@@ -1830,16 +1924,19 @@ __global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Shortcut boxes (the any-hit walk's first pass, k_render_packet_asm): per
-// internal node p a 64-byte record {box of child 0 (lo xyz, hi xyz), box of
-// child 1, ref 0, ref 1, first 0, first 1}, camera-relative (box - O), each
-// box the tight AABB of the child subtree's ALIVE triangles (tri_alive: the
-// only ones that can produce a hit from O).  ref = internal node index, or
-// kFastLeaf | leaf index, or kFastDead (no alive triangle below).  The
-// topology is the BIH's own (children {split, split+1}); only the culling
-// geometry differs.  Nothing here decides a pixel: a hit found through these
-// boxes is kept only after the exact BIH decisions are replayed along the
-// leaf's root path (fast_verify), every other lane runs the exact walk.
+// Shortcut boxes (the any-hit walk's shortcut passes, k_render_packet_asm):
+// per internal node p a 64-byte record {box of child 0 (lo xyz, hi xyz), box
+// of child 1, ref 0, ref 1, leaf 0, leaf 1}, camera-relative (box - O), each
+// box an AABB of the child subtree's ALIVE triangles (tri_alive: the only
+// ones that can produce a hit from O) -- set 1 tight, set 2 the miss-proof
+// boxes (miss_box).  ref = internal node index, or kFastLeaf | leaf index,
+// or kFastDead (no alive triangle below); leaf s = first | min(count, 63) << 26
+// for a leaf child (63: read dup_cnt).  The topology is the BIH's own
+// (children {split, split+1}); only the culling geometry differs.  Nothing
+// here decides a pixel by itself: a hit found through these boxes is kept
+// only after the exact BIH decisions are replayed along the leaf's root path
+// (fast_verify); a miss only when the miss-proof walk finds no triangle the
+// exact intersector accepts; every other lane runs the exact walk.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void fbox_put(float *slot, const float lo[3], const float hi[3]) {
     int32_t acc = 0;
@@ -1985,6 +2082,7 @@ __global__ void __launch_bounds__(kThreads) k_fast_fit(const float *__restrict__
 // Child refs of every record, once both boxes are in.
 __global__ void __launch_bounds__(kThreads) k_fast_refs(const uint4 *__restrict__ nodes, uint32_t m,
                                                         const int32_t *__restrict__ first,
+                                                        const uint32_t *__restrict__ cnt,
                                                         float *__restrict__ fast) {
     const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
     if (p >= m) return;
@@ -1997,7 +2095,12 @@ __global__ void __launch_bounds__(kThreads) k_fast_refs(const uint4 *__restrict_
         const bool leaf = (z >> (29 + s)) & 1u;
         const bool dead = !(r[6 * s] <= r[6 * s + 3]);   // empty box (or never reached)
         ref[s] = dead ? kFastDead : leaf ? (kFastLeaf | (split + s)) : (split + s);
-        if (leaf) fst[s] = (uint32_t)first[split + s];
+        if (leaf) {
+            // first | count << 26 (count 63: read dup_cnt; first < 2^26 for
+            // the scenes the packet kernel takes, packet_records_fit)
+            const uint32_t c = cnt[split + s];
+            fst[s] = (uint32_t)first[split + s] | ((c < 63u ? c : 63u) << 26);
+        }
     }
     r[12] = __uint_as_float(ref[0]);
     r[13] = __uint_as_float(ref[1]);
@@ -2167,7 +2270,8 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
             hipLaunchKernelGGL(k_fast_fit, gl, dim3(kThreads), 0, st, tris, prim, first_idx,
                                dup_cnt, leaf_parent, parent, nodes, m + 1, origin[0], origin[1],
                                origin[2], pass == 1, dmax[0], dmax[1], dmax[2], arrive, boxes);
-            hipLaunchKernelGGL(k_fast_refs, gn, dim3(kThreads), 0, st, nodes, m, first_idx, boxes);
+            hipLaunchKernelGGL(k_fast_refs, gn, dim3(kThreads), 0, st, nodes, m, first_idx, dup_cnt,
+                               boxes);
         }
     }
     return (int)hipGetLastError();
