@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--band", type=int, default=8)
-    ap.add_argument("--in-flight", type=int, default=2,
+    ap.add_argument("--in-flight", type=int, default=3,
                     help="frames in flight: consecutive frames on this many streams, so the "
                          "next frame fills the tail of the one before (1 = one frame at a time)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",

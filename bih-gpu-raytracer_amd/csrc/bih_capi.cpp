@@ -24,7 +24,7 @@
 // area, events} in turn, and reads its frame's XORWOW state from a ring of
 // kSlots + 1 buffers that k_rng_advance fills one frame ahead.
 #ifndef BIH_RENDER_SLOTS
-#define BIH_RENDER_SLOTS 2
+#define BIH_RENDER_SLOTS 3
 #endif
 constexpr int kSlots = BIH_RENDER_SLOTS;
 constexpr int kRngBufs = kSlots + 1;
@@ -669,9 +669,10 @@ int bih_sync(const bih_tree *tr, void *stream) {
             fprintf(stderr,
                     "fast-counters packets %u lanes %u | pass1 steps %u tests %u cand %u verified %u"
                     " | pass2 packets %u steps %u tests %u verified %u proven-miss %u incomplete %u"
-                    " | exact packets %u lanes %u | cycles pass1 %llu pass2 %llu exact %llu\n",
+                    " | exact packets %u lanes %u | cycles pass1 %llu (walk %llu) pass2 %llu"
+                    " exact %llu\n",
                     c[16], c[17], c[18], c[19], c[20], c[21], c[22], c[23], c[24], c[25], c[26],
-                    c[27], c[28], c[29], cy[0], cy[1], cy[2]);
+                    c[27], c[28], c[29], cy[0], cy[3], cy[1], cy[2]);
         }
     }
 #endif

@@ -1366,9 +1366,39 @@ __device__ __forceinline__ void slab_t(float lx, float ly, float lz, float hx, f
     tn = n0;
     tf = f0;
 }
-#ifndef BIH_FAST_PF
-#define BIH_FAST_PF 0   // child-pair prefetch in the shortcut walk (slower: 1.08 -> 1.43 ms)
+// shortcut records through the vector memory path (every lane the same
+// address: one request per line) instead of scalar loads
+#ifndef BIH_FAST_VLOAD
+#define BIH_FAST_VLOAD 0
 #endif
+#ifndef BIH_FAST_NOEXACT
+#define BIH_FAST_NOEXACT 0
+#endif
+__device__ __forceinline__ sf32x16 fast_rec(const float *boxes, uint32_t node) {
+#if BIH_FAST_VLOAD
+    float4 q0, q1, q2, q3;
+    const float *p = boxes + 16ull * node;
+    asm volatile("global_load_dwordx4 %0, %4, %5\n\t"
+                 "global_load_dwordx4 %1, %4, %5 offset:16\n\t"
+                 "global_load_dwordx4 %2, %4, %5 offset:32\n\t"
+                 "global_load_dwordx4 %3, %4, %5 offset:48\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
+                 : "v"(0u), "s"(p)
+                 : "memory");
+    sf32x16 r;
+    r[0] = q0.x; r[1] = q0.y; r[2] = q0.z; r[3] = q0.w;
+    r[4] = q1.x; r[5] = q1.y; r[6] = q1.z; r[7] = q1.w;
+    r[8] = q2.x; r[9] = q2.y; r[10] = q2.z; r[11] = q2.w;
+    r[12] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q3.x)));
+    r[13] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q3.y)));
+    r[14] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q3.z)));
+    r[15] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q3.w)));
+    return r;
+#else
+    return ((const cprim_t *)(const void *)boxes)[node];
+#endif
+}
 // BIH_FAST_COUNTERS builds: per-frame work of the shortcut passes in
 // work[16..32) and their cycles in work[32..38) (printed by bih_sync)
 #ifndef BIH_FAST_COUNTERS
@@ -1389,58 +1419,52 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                                                         uint32_t &cand,
                                                         unsigned long long &incomplete,
                                                         uint32_t &fc_steps, uint32_t &fc_tests) {
-    const cprim_t *fast = (const cprim_t *)(const void *)boxes;
     const unsigned long long me = lane_bit(lane);
     unsigned long long found = 0ull;
     uint32_t node = 0;
     unsigned long long mask = live;
     int sp = 0;
-    sf32x16 r = fast[0];
+    sf32x16 r = fast_rec(boxes, 0);
     while (true) {
         BIH_FC(++fc_steps);
         const uint32_t ref0 = __float_as_uint(r[12]), ref1 = __float_as_uint(r[13]);
-#if BIH_FAST_PF
-        // the internal children {split, split + 1} have adjacent records: both
-        // are requested before this node's tests (one of them is next)
-        const uint32_t pb = (ref0 & kFastLeaf) ? ref1 - 1u : ref0;
-        sf32x16 rA = r, rB = r;
-        if (!(ref0 & ref1 & kFastLeaf)) {
-            rA = fast[pb];
-            rB = fast[pb + 1];
-        }
-#endif
         // slab test of both child boxes (camera-relative: t = box * inv); pass
-        // 1 clamps the entry at t = 0 (the ray), pass 2 tests the whole line
+        // 1 clamps the entry at t = 0 (the ray), pass 2 tests the whole line.
+        // A dead child's box is NaN: never entered.
         const float cl = cons ? -INFINITY : 0.0f;
         float tn0, tf0, tn1, tf1;
         slab_t(r[0], r[1], r[2], r[3], r[4], r[5], ix, iy, iz, cl, tn0, tf0);
         slab_t(r[6], r[7], r[8], r[9], r[10], r[11], ix, iy, iz, cl, tn1, tf1);
-        unsigned long long m0 = ref0 == kFastDead ? 0ull : (__ballot(tn0 <= tf0) & mask);
-        unsigned long long m1 = ref1 == kFastDead ? 0ull : (__ballot(tn1 <= tf1) & mask);
-        // leaf children: test now (near one first)
-        const bool first1 = 2 * __popcll(__ballot(tn1 < tn0) & m0 & m1) > __popcll(m0 & m1);
+        unsigned long long m0 = __ballot(tn0 <= tf0) & mask;
+        unsigned long long m1 = __ballot(tn1 <= tf1) & mask;
+        // near child first, as the lowest lane entering both sees it
+        const unsigned long long both = m0 & m1;
+        const bool first1 = (__ballot(tn1 < tn0) & both & (0ull - both)) != 0ull;
+        if ((ref0 | ref1) & kFastLeaf) {
+            // leaf children: test now (near one first)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int s = q ^ (first1 ? 1 : 0);
-            const uint32_t ref = s ? ref1 : ref0;
-            unsigned long long ms = (s ? m1 : m0) & ~found;
-            if (!(ref & kFastLeaf) || ref == kFastDead || !ms) continue;
-            const uint32_t k = ref & ~kFastLeaf;
-            const uint32_t fc = __float_as_uint(s ? r[15] : r[14]);
-            const uint32_t b = fc & 0x3ffffffu;
-            const uint32_t c = (fc >> 26) == 63u ? dupc[k] : (fc >> 26);
-            for (uint32_t i = b; i < b + c && ms; ++i) {
-                const unsigned long long h = prim_hits(prims[i], dx, dy, dz, ms);
-                if (h & me) cand = k;
-                found |= h;
-                BIH_FC(++fc_tests);
-                ms &= ~h;
+            for (int q = 0; q < 2; ++q) {
+                const int s = q ^ (first1 ? 1 : 0);
+                const uint32_t ref = s ? ref1 : ref0;
+                unsigned long long ms = (s ? m1 : m0) & ~found;
+                if (!(ref & kFastLeaf) || !ms) continue;
+                const uint32_t k = ref & ~kFastLeaf;
+                const uint32_t fc = __float_as_uint(s ? r[15] : r[14]);
+                const uint32_t b = fc & 0x3ffffffu;
+                const uint32_t c = (fc >> 26) == 63u ? dupc[k] : (fc >> 26);
+                for (uint32_t i = b; i < b + c && ms; ++i) {
+                    const unsigned long long h = prim_hits(prims[i], dx, dy, dz, ms);
+                    if (h & me) cand = k;
+                    found |= h;
+                    BIH_FC(++fc_tests);
+                    ms &= ~h;
+                }
             }
+            if (ref0 & kFastLeaf) m0 = 0ull;
+            if (ref1 & kFastLeaf) m1 = 0ull;
+            m0 &= ~found;
+            m1 &= ~found;
         }
-        if ((ref0 & kFastLeaf) || ref0 == kFastDead) m0 = 0ull;
-        if ((ref1 & kFastLeaf) || ref1 == kFastDead) m1 = 0ull;
-        m0 &= ~found;
-        m1 &= ~found;
         if (m0 && m1) {
             const uint32_t nf = first1 ? ref0 : ref1;
             const unsigned long long mf = first1 ? m0 : m1;
@@ -1467,16 +1491,9 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                 }
             }
             if (!mask) break;
-            node = __builtin_amdgcn_readfirstlane(node);
-            r = fast[node];
-            continue;
         }
         node = __builtin_amdgcn_readfirstlane(node);
-#if BIH_FAST_PF
-        r = node == pb ? rA : rB;
-#else
-        r = fast[node];
-#endif
+        r = fast_rec(boxes, node);
     }
     return found;
 }
@@ -1609,6 +1626,7 @@ k_render_packet_asm(const RenderArgs a) {
             const unsigned long long found =
                 fast_walk(a.fast, false, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
                           live, lane, s_fnode[wv], s_fmask[wv], cand, inc, s1, n1);
+            BIH_FC(const uint64_t fc_tw = __builtin_amdgcn_s_memtime());
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
             shortcut = __ballot(ok);
@@ -1655,6 +1673,7 @@ k_render_packet_asm(const RenderArgs a) {
                 atomicAdd(a.work + 29, (uint32_t)__popcll(live));
                 atomicAdd(cy, (unsigned long long)(fc_t1 - fc_t0));
                 atomicAdd(cy + 1, (unsigned long long)(fc_t2 - fc_t1));
+                atomicAdd(cy + 3, (unsigned long long)(fc_tw - fc_t0));
             }
             fc_walk0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1679,6 +1698,9 @@ k_render_packet_asm(const RenderArgs a) {
             }
         } else if (live) {
             if constexpr (ANYHIT && !STATS) {
+#if BIH_FAST_NOEXACT
+                // timing experiments only (wrong for unresolved lanes)
+#else
                 asm volatile(BIH_PACKET_WALK(BIH_ANY_ON, BIH_CLR_ON,
                                              BIH_POP_ANY,
                                              "", "", "", "", "")
@@ -1689,6 +1711,7 @@ k_render_packet_asm(const RenderArgs a) {
                                [lane4] "v"(lane4), [dx] "v"(dx), [dy] "v"(dy), [dz] "v"(dz),
                                [ix] "v"(ix), [iy] "v"(iy), [iz] "v"(iz), [sgn] "v"(sg)
                              : BIH_PACKET_CLOBBERS);
+#endif
             } else if constexpr (ANYHIT && STATS) {
                 asm volatile(BIH_PACKET_WALK(BIH_ANY_ON, BIH_CLR_ON,
                                              BIH_POP_ANY,
@@ -2095,6 +2118,8 @@ __global__ void __launch_bounds__(kThreads) k_fast_refs(const uint4 *__restrict_
         const bool leaf = (z >> (29 + s)) & 1u;
         const bool dead = !(r[6 * s] <= r[6 * s + 3]);   // empty box (or never reached)
         ref[s] = dead ? kFastDead : leaf ? (kFastLeaf | (split + s)) : (split + s);
+        if (dead)   // NaN box: every slab test of it fails
+            for (int c = 0; c < 6; ++c) r[6 * s + c] = __uint_as_float(0x7fc00000u);
         if (leaf) {
             // first | count << 26 (count 63: read dup_cnt; first < 2^26 for
             // the scenes the packet kernel takes, packet_records_fit)

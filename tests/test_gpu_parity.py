@@ -270,8 +270,9 @@ def test_frame_gaps_match_oracle(gpu, bihrt_mod, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_frames_in_flight_on_two_streams(gpu, bihrt_mod, oracle_mod):
-    """Consecutive frames issued on two streams overlap on the GPU (the
+@pytest.mark.parametrize("nstreams", [2, 3, 4])
+def test_frames_in_flight_on_streams(nstreams, gpu, bihrt_mod, oracle_mod):
+    """Consecutive frames issued on 2-4 streams overlap on the GPU (the
     library orders only what they share: tile queues, spill areas, the RNG
     ring); a gap, a rebuild and a 1M-scale frame mid-sequence keep every frame
     equal to the oracle's."""
@@ -281,13 +282,13 @@ def test_frames_in_flight_on_two_streams(gpu, bihrt_mod, oracle_mod):
     ot = oracle_mod.OracleTree(tris)
     w, h = 160, 96
     r = bihrt_mod.Renderer(g, w, h)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
     frames = [0, 1, 2, 3, 7, 8, 9, 30, 31, 2, 3]
     outs = [torch.zeros(h * w, dtype=torch.int32, device="cuda") for _ in frames]
     for k, f in enumerate(frames):
         if k == 6:
             g.rebuild()
-        r.render_device(outs[k].data_ptr(), f, stream=streams[k % 2].cuda_stream)
+        r.render_device(outs[k].data_ptr(), f, stream=streams[k % nstreams].cuda_stream)
     torch.cuda.synchronize()
     for k, f in enumerate(frames):
         ref, _ = ot.render(w, h, frame=f)
