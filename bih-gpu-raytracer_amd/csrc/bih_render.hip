@@ -1414,8 +1414,6 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                                                         const cu32_t *dupc, float dx, float dy,
                                                         float dz, float ix, float iy, float iz,
                                                         unsigned long long live, uint32_t lane,
-                                                        uint32_t *snode,
-                                                        unsigned long long *smask,
                                                         uint32_t &cand,
                                                         unsigned long long &incomplete,
                                                         uint32_t &fc_steps, uint32_t &fc_tests) {
@@ -1424,6 +1422,7 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
     uint32_t node = 0;
     unsigned long long mask = live;
     int sp = 0;
+    uint32_t st_node = 0, st_lo = 0, st_hi = 0;
     sf32x16 r = fast_rec(boxes, 0);
     while (true) {
         BIH_FC(++fc_steps);
@@ -1469,8 +1468,17 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
             const uint32_t nf = first1 ? ref0 : ref1;
             const unsigned long long mf = first1 ? m0 : m1;
             if (sp < kFastStack) {
-                snode[sp] = nf;
-                smask[sp] = mf;
+                // stack entry sp in lane sp of three VGPRs (SGPR results on pop)
+                uint32_t keep;   // M0 (the lane select) saved and restored
+                asm volatile("s_mov_b32 %3, m0\n\t"
+                             "s_mov_b32 m0, %7\n\t"
+                             "s_nop 0\n\t"
+                             "v_writelane_b32 %0, %4, m0\n\t"
+                             "v_writelane_b32 %1, %5, m0\n\t"
+                             "v_writelane_b32 %2, %6, m0\n\t"
+                             "s_mov_b32 m0, %3"
+                             : "+v"(st_node), "+v"(st_lo), "+v"(st_hi), "=&s"(keep)
+                             : "s"(nf), "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"(sp));
                 ++sp;
             } else {
                 incomplete |= mf;   // a full stack drops the subtree: exact walk
@@ -1484,15 +1492,15 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
             mask = 0ull;
             while (sp > 0) {
                 --sp;
-                mask = smask[sp] & ~found;
+                mask = (((unsigned long long)__builtin_amdgcn_readlane(st_hi, sp) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane(st_lo, sp)) & ~found;
                 if (mask) {
-                    node = snode[sp];
+                    node = __builtin_amdgcn_readlane(st_node, sp);
                     break;
                 }
             }
             if (!mask) break;
         }
-        node = __builtin_amdgcn_readfirstlane(node);
         r = fast_rec(boxes, node);
     }
     return found;
@@ -1574,8 +1582,6 @@ k_render_packet_asm(const RenderArgs a) {
     TileQueue queue = make_queue(a, tiles_x, (a.nrows + TH - 1) / TH);
     uint32_t tile = 0;
     (void)ntiles;
-    __shared__ uint32_t s_fnode[kThreads / 64][kFastStack];              // shortcut pass stack
-    __shared__ unsigned long long s_fmask[kThreads / 64][kFastStack];
 #if BIH_WAVE_TIMELINE
     const uint64_t tl_begin = __builtin_amdgcn_s_memrealtime();
     uint64_t tl_last = tl_begin;
@@ -1625,7 +1631,7 @@ k_render_packet_asm(const RenderArgs a) {
             BIH_FC(const uint64_t fc_t0 = __builtin_amdgcn_s_memtime());
             const unsigned long long found =
                 fast_walk(a.fast, false, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                          live, lane, s_fnode[wv], s_fmask[wv], cand, inc, s1, n1);
+                          live, lane, cand, inc, s1, n1);
             BIH_FC(const uint64_t fc_tw = __builtin_amdgcn_s_memtime());
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
@@ -1644,7 +1650,7 @@ k_render_packet_asm(const RenderArgs a) {
                 inc = 0ull;
                 const unsigned long long found2 =
                     fast_walk(a.fast2, true, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                              m2, lane, s_fnode[wv], s_fmask[wv], cand, inc, s2, n2);
+                              m2, lane, cand, inc, s2, n2);
                 const bool ok2 = ((found2 >> lane) & 1ull) &&
                                  fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
                 const unsigned long long hit2 = __ballot(ok2);
