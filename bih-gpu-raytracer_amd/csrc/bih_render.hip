@@ -1374,6 +1374,9 @@ __device__ __forceinline__ void slab_t(float lx, float ly, float lz, float hx, f
 #ifndef BIH_FAST_NOEXACT
 #define BIH_FAST_NOEXACT 0
 #endif
+#ifndef BIH_FAST_SINGLE
+#define BIH_FAST_SINGLE 0
+#endif
 __device__ __forceinline__ sf32x16 fast_rec(const float *boxes, uint32_t node) {
 #if BIH_FAST_VLOAD
     float4 q0, q1, q2, q3;
@@ -1396,7 +1399,15 @@ __device__ __forceinline__ sf32x16 fast_rec(const float *boxes, uint32_t node) {
     r[15] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q3.w)));
     return r;
 #else
-    return ((const cprim_t *)(const void *)boxes)[node];
+    // one s_load with a 32-bit byte offset (no 64-bit address arithmetic);
+    // loaded and waited for inside the statement
+    sf32x16 r;
+    asm volatile("s_load_dwordx16 %0, %1, %2\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=s"(r)
+                 : "s"(boxes), "s"(node << 6)
+                 : "memory");
+    return r;
 #endif
 }
 // BIH_FAST_COUNTERS builds: per-frame work of the shortcut passes in
@@ -1629,9 +1640,18 @@ k_render_packet_asm(const RenderArgs a) {
             unsigned long long inc = 0ull;
             (void)s1, (void)n1, (void)s2, (void)n2;
             BIH_FC(const uint64_t fc_t0 = __builtin_amdgcn_s_memtime());
+            const unsigned long long fin =
+                __ballot(__builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz));
+#if BIH_FAST_SINGLE
+            // one conservative pass: hits and miss proofs together
+            const bool single = a.fast2 != nullptr;
+#else
+            const bool single = false;
+#endif
+            const unsigned long long m1 = single ? live & fin : live;
             const unsigned long long found =
-                fast_walk(a.fast, false, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                          live, lane, cand, inc, s1, n1);
+                fast_walk(single ? a.fast2 : a.fast, single, prims, (const cu32_t *)dupc, dx, dy,
+                          dz, ix, iy, iz, m1, lane, cand, inc, s1, n1);
             BIH_FC(const uint64_t fc_tw = __builtin_amdgcn_s_memtime());
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
@@ -1639,13 +1659,11 @@ k_render_packet_asm(const RenderArgs a) {
             BIH_FC(const unsigned long long fc_live0 = live);
             BIH_FC(const uint32_t fc_v1 = (uint32_t)__popcll(shortcut));
             live &= ~shortcut;
+            if (single) live &= ~(m1 & ~found & ~inc);   // proven misses
             BIH_FC(const uint64_t fc_t1 = __builtin_amdgcn_s_memtime());
             // miss proof for the rest (lanes with an infinite 1/D component
             // keep the exact walk: 0 * inf in a slab test)
-            const unsigned long long m2 =
-                a.fast2 ? live & __ballot(__builtin_isfinite(ix) && __builtin_isfinite(iy) &&
-                                          __builtin_isfinite(iz))
-                        : 0ull;
+            const unsigned long long m2 = a.fast2 && !single ? live & fin : 0ull;
             if (m2) {
                 inc = 0ull;
                 const unsigned long long found2 =
