@@ -668,11 +668,11 @@ int bih_sync(const bih_tree *tr, void *stream) {
             const unsigned long long *cy = reinterpret_cast<const unsigned long long *>(c + 32);
             fprintf(stderr,
                     "fast-counters packets %u lanes %u | pass1 steps %u tests %u cand %u verified %u"
-                    " | pass2 packets %u steps %u tests %u verified %u proven-miss %u incomplete %u"
+                    " | pass2 packets %u steps %u tests %u verified %u proven-miss %u"
                     " | exact packets %u lanes %u | cycles pass1 %llu (walk %llu) pass2 %llu"
                     " exact %llu\n",
                     c[16], c[17], c[18], c[19], c[20], c[21], c[22], c[23], c[24], c[25], c[26],
-                    c[27], c[28], c[29], cy[0], cy[3], cy[1], cy[2]);
+                    c[28], c[29], cy[0], cy[3], cy[1], cy[2]);
         }
     }
 #endif

@@ -1337,9 +1337,8 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
 //   pass 1 (tight boxes, cons = false): finds the hits of most lanes fast;
 //   pass 2 (miss-proof boxes, miss_box; cons = true): the whole line is
 //     tested against every box, so a lane of `live` that ends with no
-//     candidate and not in `incomplete` (its subtree dropped by a full stack)
-//     has no triangle the exact intersector accepts: a reference miss.
-constexpr int kFastStack = 64;
+//     candidate has no triangle the exact intersector accepts: a reference
+//     miss.  (The walk drops nothing: its stack cannot overflow, below.)
 // Entry/exit parameters of the line O + t D against a camera-relative box,
 // entry clamped below at cl.  Plain v_min/v_max (no NaN canonicalisation):
 // no operand is NaN -- boxes are finite or +-inf, |1/D| >= 1/|D|max > 0 --
@@ -1365,6 +1364,16 @@ __device__ __forceinline__ void slab_t(float lx, float ly, float lz, float hx, f
           [cl] "s"(cl));
     tn = n0;
     tf = f0;
+}
+// primary-ray triangle record i: one s_load with a 32-bit byte offset
+__device__ __forceinline__ sf32x16 prim_rec(const cprim_t *prims, uint32_t i) {
+    sf32x16 r;
+    asm volatile("s_load_dwordx16 %0, %1, %2\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=s"(r)
+                 : "s"(prims), "s"(i << 6)
+                 : "memory");
+    return r;
 }
 // shortcut records through the vector memory path (every lane the same
 // address: one request per line) instead of scalar loads
@@ -1426,7 +1435,6 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                                                         float dz, float ix, float iy, float iz,
                                                         unsigned long long live, uint32_t lane,
                                                         uint32_t &cand,
-                                                        unsigned long long &incomplete,
                                                         uint32_t &fc_steps, uint32_t &fc_tests) {
     const unsigned long long me = lane_bit(lane);
     unsigned long long found = 0ull;
@@ -1463,7 +1471,7 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                 const uint32_t b = fc & 0x3ffffffu;
                 const uint32_t c = (fc >> 26) == 63u ? dupc[k] : (fc >> 26);
                 for (uint32_t i = b; i < b + c && ms; ++i) {
-                    const unsigned long long h = prim_hits(prims[i], dx, dy, dz, ms);
+                    const unsigned long long h = prim_hits(prim_rec(prims, i), dx, dy, dz, ms);
                     if (h & me) cand = k;
                     found |= h;
                     BIH_FC(++fc_tests);
@@ -1478,8 +1486,11 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
         if (m0 && m1) {
             const uint32_t nf = first1 ? ref0 : ref1;
             const unsigned long long mf = first1 ? m0 : m1;
-            if (sp < kFastStack) {
-                // stack entry sp in lane sp of three VGPRs (SGPR results on pop)
+            {
+                // stack entry sp in lane sp of three VGPRs (SGPR results on
+                // pop).  sp < 31 always: a push happens at most once per level
+                // and the Karras tree of distinct 30-bit codes is at most 30
+                // levels deep (each level lengthens the common prefix).
                 uint32_t keep;   // M0 (the lane select) saved and restored
                 asm volatile("s_mov_b32 %3, m0\n\t"
                              "s_mov_b32 m0, %7\n\t"
@@ -1491,8 +1502,6 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
                              : "+v"(st_node), "+v"(st_lo), "+v"(st_hi), "=&s"(keep)
                              : "s"(nf), "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"(sp));
                 ++sp;
-            } else {
-                incomplete |= mf;   // a full stack drops the subtree: exact walk
             }
             node = first1 ? ref1 : ref0;
             mask = first1 ? m1 : m0;
@@ -1637,7 +1646,6 @@ k_render_packet_asm(const RenderArgs a) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
             // provably reaches are done; the others take the exact walk below
             uint32_t cand = 0, s1 = 0, n1 = 0, s2 = 0, n2 = 0;
-            unsigned long long inc = 0ull;
             (void)s1, (void)n1, (void)s2, (void)n2;
             BIH_FC(const uint64_t fc_t0 = __builtin_amdgcn_s_memtime());
             const unsigned long long fin =
@@ -1651,7 +1659,7 @@ k_render_packet_asm(const RenderArgs a) {
             const unsigned long long m1 = single ? live & fin : live;
             const unsigned long long found =
                 fast_walk(single ? a.fast2 : a.fast, single, prims, (const cu32_t *)dupc, dx, dy,
-                          dz, ix, iy, iz, m1, lane, cand, inc, s1, n1);
+                          dz, ix, iy, iz, m1, lane, cand, s1, n1);
             BIH_FC(const uint64_t fc_tw = __builtin_amdgcn_s_memtime());
             const bool ok = ((found >> lane) & 1ull) &&
                             fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
@@ -1659,28 +1667,26 @@ k_render_packet_asm(const RenderArgs a) {
             BIH_FC(const unsigned long long fc_live0 = live);
             BIH_FC(const uint32_t fc_v1 = (uint32_t)__popcll(shortcut));
             live &= ~shortcut;
-            if (single) live &= ~(m1 & ~found & ~inc);   // proven misses
+            if (single) live &= ~(m1 & ~found);   // proven misses
             BIH_FC(const uint64_t fc_t1 = __builtin_amdgcn_s_memtime());
             // miss proof for the rest (lanes with an infinite 1/D component
             // keep the exact walk: 0 * inf in a slab test)
             const unsigned long long m2 = a.fast2 && !single ? live & fin : 0ull;
             if (m2) {
-                inc = 0ull;
                 const unsigned long long found2 =
                     fast_walk(a.fast2, true, prims, (const cu32_t *)dupc, dx, dy, dz, ix, iy, iz,
-                              m2, lane, cand, inc, s2, n2);
+                              m2, lane, cand, s2, n2);
                 const bool ok2 = ((found2 >> lane) & 1ull) &&
                                  fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
                 const unsigned long long hit2 = __ballot(ok2);
                 shortcut |= hit2;
-                live &= ~(hit2 | (m2 & ~found2 & ~inc));   // proven misses are done too
+                live &= ~(hit2 | (m2 & ~found2));   // proven misses are done too
                 BIH_FC(if (lane == 0) {
                     atomicAdd(a.work + 22, 1u);
                     atomicAdd(a.work + 23, s2);
                     atomicAdd(a.work + 24, n2);
                     atomicAdd(a.work + 25, (uint32_t)__popcll(hit2));
-                    atomicAdd(a.work + 26, (uint32_t)__popcll(m2 & ~found2 & ~inc));
-                    atomicAdd(a.work + 27, (uint32_t)__popcll(inc));
+                    atomicAdd(a.work + 26, (uint32_t)__popcll(m2 & ~found2));
                 })
             }
 #if BIH_FAST_COUNTERS
