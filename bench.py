@@ -289,7 +289,12 @@ def main():
                 "effective_gbs": b_ray * launch_rays / (elapsed / args.steps) / 1e9,
                 "counters_per_ray": {"nodes": n_node / rays_all, "leaves": n_leaf / rays_all,
                                      "tris": n_tri / rays_all},
-                "kernel": f"k_render_packet_asm ({'any-hit' if trav == 0 else 'reference'} walk)",
+                "kernel": "k_render_packet_asm (" + ("any-hit: shortcut passes + exact walk for the rest"
+                                                     if trav == 0 else "reference walk") + ")",
+                "note": "bytes_per_ray = SURVEY 8d's B_ray over the exact walk's per-ray counters "
+                        "(the reference algorithm's work); the any-hit shortcut reaches the same "
+                        "pixels with far fewer node visits, so achieved/frac count work-equivalent "
+                        "bytes; 'traffic' is the measured HBM bytes per launch",
             },
             "traffic_detail": traffic,
             "cpu_baseline": cpu,
