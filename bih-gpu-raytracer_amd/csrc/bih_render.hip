@@ -1386,6 +1386,9 @@ __device__ __forceinline__ sf32x16 prim_rec(const cprim_t *prims, uint32_t i) {
 #ifndef BIH_FAST_SINGLE
 #define BIH_FAST_SINGLE 0
 #endif
+#ifndef BIH_FAST_ASM_A
+#define BIH_FAST_ASM_A 1   // child masks + near order as one asm sequence
+#endif
 __device__ __forceinline__ sf32x16 fast_rec(const float *boxes, uint32_t node) {
 #if BIH_FAST_VLOAD
     float4 q0, q1, q2, q3;
@@ -1453,11 +1456,31 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
         float tn0, tf0, tn1, tf1;
         slab_t(r[0], r[1], r[2], r[3], r[4], r[5], ix, iy, iz, cl, tn0, tf0);
         slab_t(r[6], r[7], r[8], r[9], r[10], r[11], ix, iy, iz, cl, tn1, tf1);
+        // child masks and the near child (as the lowest lane entering both
+        // sees it), one SALU/VALU sequence (EXEC is the full wave here)
+#if BIH_FAST_ASM_A
+        unsigned long long m0, m1, lt, both;
+        uint32_t first1;
+        asm volatile("v_cmp_le_f32_e64 %[m0], %[tn0], %[tf0]\n\t"
+                     "v_cmp_le_f32_e64 %[m1], %[tn1], %[tf1]\n\t"
+                     "v_cmp_lt_f32_e64 %[lt], %[tn1], %[tn0]\n\t"
+                     "s_and_b64 %[m0], %[m0], %[mask]\n\t"
+                     "s_and_b64 %[m1], %[m1], %[mask]\n\t"
+                     "s_and_b64 %[both], %[m0], %[m1]\n\t"
+                     "s_ff1_i32_b64 %[f1], %[both]\n\t"
+                     "s_bitcmp1_b64 %[lt], %[f1]\n\t"
+                     "s_cselect_b32 %[f1], 1, 0"
+                     : [m0] "=&s"(m0), [m1] "=&s"(m1), [lt] "=&s"(lt), [both] "=&s"(both),
+                       [f1] "=&s"(first1)
+                     : [tn0] "v"(tn0), [tf0] "v"(tf0), [tn1] "v"(tn1), [tf1] "v"(tf1),
+                       [mask] "s"(mask)
+                     : "scc");
+#else
         unsigned long long m0 = __ballot(tn0 <= tf0) & mask;
         unsigned long long m1 = __ballot(tn1 <= tf1) & mask;
-        // near child first, as the lowest lane entering both sees it
         const unsigned long long both = m0 & m1;
-        const bool first1 = (__ballot(tn1 < tn0) & both & (0ull - both)) != 0ull;
+        const uint32_t first1 = (__ballot(tn1 < tn0) & both & (0ull - both)) != 0ull ? 1u : 0u;
+#endif
         if ((ref0 | ref1) & kFastLeaf) {
             // leaf children: test now (near one first)
 #pragma unroll
@@ -1483,32 +1506,34 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
             m0 &= ~found;
             m1 &= ~found;
         }
+        // descend: both children -> stack the far one (entry sp in lane sp of
+        // st_node/st_lo/st_hi; sp < 31 always: at most one push per level and
+        // the Karras tree of distinct 30-bit codes is at most 30 levels deep),
+        // one child -> it, none -> pop
+        uint32_t pop = 0;
         if (m0 && m1) {
             const uint32_t nf = first1 ? ref0 : ref1;
             const unsigned long long mf = first1 ? m0 : m1;
-            {
-                // stack entry sp in lane sp of three VGPRs (SGPR results on
-                // pop).  sp < 31 always: a push happens at most once per level
-                // and the Karras tree of distinct 30-bit codes is at most 30
-                // levels deep (each level lengthens the common prefix).
-                uint32_t keep;   // M0 (the lane select) saved and restored
-                asm volatile("s_mov_b32 %3, m0\n\t"
-                             "s_mov_b32 m0, %7\n\t"
-                             "s_nop 0\n\t"
-                             "v_writelane_b32 %0, %4, m0\n\t"
-                             "v_writelane_b32 %1, %5, m0\n\t"
-                             "v_writelane_b32 %2, %6, m0\n\t"
-                             "s_mov_b32 m0, %3"
-                             : "+v"(st_node), "+v"(st_lo), "+v"(st_hi), "=&s"(keep)
-                             : "s"(nf), "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"(sp));
-                ++sp;
-            }
+            uint32_t keep;   // M0 (the lane select) saved and restored
+            asm volatile("s_mov_b32 %3, m0\n\t"
+                         "s_mov_b32 m0, %7\n\t"
+                         "s_nop 0\n\t"
+                         "v_writelane_b32 %0, %4, m0\n\t"
+                         "v_writelane_b32 %1, %5, m0\n\t"
+                         "v_writelane_b32 %2, %6, m0\n\t"
+                         "s_mov_b32 m0, %3"
+                         : "+v"(st_node), "+v"(st_lo), "+v"(st_hi), "=&s"(keep)
+                         : "s"(nf), "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"(sp));
+            ++sp;
             node = first1 ? ref1 : ref0;
             mask = first1 ? m1 : m0;
         } else if (m0 | m1) {
             node = m0 ? ref0 : ref1;
             mask = m0 | m1;
         } else {
+            pop = 1;
+        }
+        if (pop) {
             mask = 0ull;
             while (sp > 0) {
                 --sp;
