@@ -1386,6 +1386,9 @@ __device__ __forceinline__ sf32x16 prim_rec(const cprim_t *prims, uint32_t i) {
 #ifndef BIH_FAST_SINGLE
 #define BIH_FAST_SINGLE 0
 #endif
+#ifndef BIH_FAST_MAJ
+#define BIH_FAST_MAJ 0   // near order: majority of the lanes entering both (else the lowest)
+#endif
 #ifndef BIH_FAST_ASM_A
 #define BIH_FAST_ASM_A 1   // child masks + near order as one asm sequence
 #endif
@@ -1460,18 +1463,26 @@ __device__ __forceinline__ unsigned long long fast_walk(const float *boxes, bool
         // sees it), one SALU/VALU sequence (EXEC is the full wave here)
 #if BIH_FAST_ASM_A
         unsigned long long m0, m1, lt, both;
-        uint32_t first1;
+        uint32_t first1, cnt_both;
         asm volatile("v_cmp_le_f32_e64 %[m0], %[tn0], %[tf0]\n\t"
                      "v_cmp_le_f32_e64 %[m1], %[tn1], %[tf1]\n\t"
                      "v_cmp_lt_f32_e64 %[lt], %[tn1], %[tn0]\n\t"
                      "s_and_b64 %[m0], %[m0], %[mask]\n\t"
                      "s_and_b64 %[m1], %[m1], %[mask]\n\t"
                      "s_and_b64 %[both], %[m0], %[m1]\n\t"
+#if BIH_FAST_MAJ
+                     "s_and_b64 %[lt], %[lt], %[both]\n\t"
+                     "s_bcnt1_i32_b64 %[f1], %[lt]\n\t"
+                     "s_bcnt1_i32_b64 %[c], %[both]\n\t"
+                     "s_lshl_b32 %[f1], %[f1], 1\n\t"
+                     "s_cmp_gt_u32 %[f1], %[c]\n\t"
+#else
                      "s_ff1_i32_b64 %[f1], %[both]\n\t"
                      "s_bitcmp1_b64 %[lt], %[f1]\n\t"
+#endif
                      "s_cselect_b32 %[f1], 1, 0"
                      : [m0] "=&s"(m0), [m1] "=&s"(m1), [lt] "=&s"(lt), [both] "=&s"(both),
-                       [f1] "=&s"(first1)
+                       [f1] "=&s"(first1), [c] "=&s"(cnt_both)
                      : [tn0] "v"(tn0), [tf0] "v"(tf0), [tn1] "v"(tn1), [tf1] "v"(tf1),
                        [mask] "s"(mask)
                      : "scc");
@@ -2056,9 +2067,12 @@ __device__ __forceinline__ void fbox_get(float *slot, float lo[3], float hi[3]) 
 // (-a, 1+a+c); the box is that triangle's AABB padded by 1e-5 + 1e-6|x| (far
 // more than the slab test's own rounding).  The constants are taken 8e, not 5e.
 // A non-finite bound or den <= 0.5e-6 gives the unbounded box.
+#ifndef BIH_MISS_E
+#define BIH_MISS_E 8   // error constant of miss_box in units of 2^-24 (the analysis gives 5)
+#endif
 __device__ __forceinline__ void miss_box(const float *r, const float *dmax, float lo[3],
                                          float hi[3]) {
-    const float E = 8.0f * 0x1p-24f;
+    const float E = (float)BIH_MISS_E * 0x1p-24f;
     const float e1[3] = {r[0], r[1], r[2]}, e2[3] = {r[3], r[4], r[5]};
     const float sv[3] = {r[6], r[7], r[8]};
     const float ae1[3] = {fabsf(e1[0]), fabsf(e1[1]), fabsf(e1[2])};
