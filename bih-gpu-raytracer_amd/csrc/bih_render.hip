@@ -2065,10 +2065,11 @@ __device__ __forceinline__ void fbox_get(float *slot, float lo[3], float hi[3]) 
 // v* >= -(4e + Ev/den) =: -b,  u* + v* <= 1 + 8e + 1.01 (Eu + Ev + 2 Ed)/den =: 1 + c.
 // The point lies in the triangle of barycentric corners (-a, -b), (1+b+c, -b),
 // (-a, 1+a+c); the box is that triangle's AABB padded by 1e-5 + 1e-6|x| (far
-// more than the slab test's own rounding).  The constants are taken 8e, not 5e.
+// more than the slab test's own rounding).  The constants are taken 6e (BIH_MISS_E),
+// not 5e: margin for the second-order terms and the f32 evaluation of the bound.
 // A non-finite bound or den <= 0.5e-6 gives the unbounded box.
 #ifndef BIH_MISS_E
-#define BIH_MISS_E 8   // error constant of miss_box in units of 2^-24 (the analysis gives 5)
+#define BIH_MISS_E 6   // error constant of miss_box in units of 2^-24 (the analysis gives 5)
 #endif
 __device__ __forceinline__ void miss_box(const float *r, const float *dmax, float lo[3],
                                          float hi[3]) {

@@ -45,7 +45,7 @@ def _mt(e1, e2, s, q, tn, D):
 
 def _miss_box(e1, e2, s, dmax):
     """miss_box, same f32 expressions."""
-    E = F(8.0 * 2.0 ** -24)
+    E = F(6.0 * 2.0 ** -24)
     ae1, ae2, a_s = np.abs(e1), np.abs(e2), np.abs(s)
     P = np.stack([dmax[:, 1] * ae2[:, 2] + ae2[:, 1] * dmax[:, 2],
                   dmax[:, 2] * ae2[:, 0] + ae2[:, 2] * dmax[:, 0],
@@ -87,7 +87,7 @@ def _slab(lo, hi, D):
 
 def _barycentric_bounds(e1, e2, s, dmax):
     """miss_box's a, b, c (f32, same expressions)."""
-    E = F(8.0 * 2.0 ** -24)
+    E = F(6.0 * 2.0 ** -24)
     ae1, ae2, a_s = np.abs(e1), np.abs(e2), np.abs(s)
     P = np.stack([dmax[:, 1] * ae2[:, 2] + ae2[:, 1] * dmax[:, 2],
                   dmax[:, 2] * ae2[:, 0] + ae2[:, 2] * dmax[:, 0],
