@@ -1229,11 +1229,12 @@ __global__ void __launch_bounds__(kThreads) k_render_packet2(const RenderArgs a)
 // p == chunk size (or the first one on an empty slot) refills it from the
 // band counters; waves that overdraw wait (s_sleep) for the refill.
 constexpr uint32_t kRegions = 8;
-// 4 x 4 tiles (16 x 16 pixels): the same throughput as 8 x 4 with two frames
-// in flight and a finer grain for the cost order (one frame alone 3.77 ->
-// 3.60 ms); chunks of fewer tiles than half a CU's waves refill too often
+// 8 x 4 tiles (32 x 16 pixels).  With the any-hit shortcut (short packets):
+// 8x4 0.632, 16x2 0.632, 8x2 0.649, 8x8 0.662, 4x4 0.668, 16x4 0.678, 4x2
+// 0.86 ms per frame (3 in flight); with the exact walk 4x4 and 8x4 tied.
+// Chunks of fewer tiles than half a CU's waves refill too often.
 #ifndef BIH_CHUNK_W
-#define BIH_CHUNK_W 4
+#define BIH_CHUNK_W 8
 #endif
 #ifndef BIH_CHUNK_H
 #define BIH_CHUNK_H 4
