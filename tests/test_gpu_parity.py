@@ -338,3 +338,19 @@ def test_anyhit_shortcut_matches_exact_walk(scene, gpu, bihrt_mod):
         a = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_ANYHIT)
         b = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_REFERENCE)
         assert np.array_equal(a, b), (scene, frame, int((a != b).sum()))
+
+
+def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod):
+    """Config C5's scene and size on one GPU (10M-triangle soup, 3840x2160,
+    4 spp): the any-hit shortcut and the exact walk agree on every pixel of
+    two frames; every pixel is one of the five shades."""
+    import torch
+    tris = bihrt_mod.scenes.soup(10_000_000, seed=1)
+    d = torch.from_numpy(tris).cuda()
+    g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
+    w, h = 3840, 2160
+    for frame in (0, 5):
+        a = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_ANYHIT)
+        b = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_REFERENCE)
+        assert np.array_equal(a, b), (frame, int((a != b).sum()))
+    assert set(np.unique(a).tolist()) <= {0x281414, 0x1e4e4e, 0x148989, 0x0ac4c4, 0x00ffff}
