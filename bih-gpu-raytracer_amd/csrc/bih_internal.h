@@ -36,9 +36,11 @@ constexpr int kStackDepth = 32;   // Karras path length <= 30 for distinct 30-bi
 // 1M-tri soup @1080p: 0.8 % of pushes land in slot >= 10 (12 % at >= 8).
 constexpr int kLdsStack = BIH_LDS_STACK;
 // work buffer: [0..8) chunk counters (one per image band / XCD); [16..56) walk
-// counters of BIH_PACKET_COUNTERS builds; [64..2112) per-CU tile slots (u64)
-constexpr uint32_t kWorkWords = 64 + 2 * 1024 + 64;   // + histograms (counter builds)
-constexpr uint32_t kHistWord = 64 + 2 * 1024;
+// counters of counter builds; [64..64+32*1024) per-CU tile slots (u64, one per
+// 128-byte line: no false sharing of the slot atomics between CUs)
+constexpr uint32_t kSlotStrideWords = 32;
+constexpr uint32_t kWorkWords = 64 + kSlotStrideWords * 1024 + 64;   // + histograms (counter builds)
+constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif

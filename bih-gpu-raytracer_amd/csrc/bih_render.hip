@@ -1240,7 +1240,7 @@ constexpr uint32_t kRegions = 8;
 #define BIH_CHUNK_H 4
 #endif
 constexpr uint32_t kChunkW = BIH_CHUNK_W, kChunkH = BIH_CHUNK_H, kChunk = kChunkW * kChunkH;
-constexpr uint32_t kSlotWord = 64;                     // work[64..64+2*1024): CU slots
+constexpr uint32_t kSlotWord = 64;                     // work[64..): CU slots, kSlotStrideWords apart
 constexpr unsigned long long kSlotDone = 0xFFFFFFFF00000000ull;
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -1317,7 +1317,7 @@ __device__ __forceinline__ TileQueue make_queue(const RenderArgs &a, uint32_t ti
                                                 uint32_t tiles_y) {
     TileQueue q;
     q.work = a.work;
-    q.slot = reinterpret_cast<unsigned long long *>(a.work + kSlotWord) + cu_key();
+    q.slot = reinterpret_cast<unsigned long long *>(a.work + kSlotWord + kSlotStrideWords * cu_key());
     q.tiles_x = tiles_x;
     q.tiles_y = tiles_y;
     q.chunks_x = (tiles_x + kChunkW - 1) / kChunkW;
