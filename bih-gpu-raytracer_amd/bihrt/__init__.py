@@ -36,6 +36,14 @@ def camera_reference(w: int, h: int) -> Camera:
     return cam
 
 
+def camera_ray_bound(cam: Camera) -> np.ndarray:
+    """bih_camera_ray_bound: per-component bound of |D| over the camera's
+    primary rays (host only; sizes the any-hit walk's miss-proof boxes)."""
+    out = (C.c_float * 3)()
+    check(load().bih_camera_ray_bound(C.byref(cam), out), "bih_camera_ray_bound")
+    return np.array(out[:], np.float32)
+
+
 class GPUArrayManager:
     """Scene + BIH on one device.  `tris` is a float32 (n, 9) soup."""
 
@@ -195,5 +203,5 @@ def write_ppm(path: str, img: np.ndarray):
 
 
 __all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
-           "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
+           "camera_ray_bound", "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
            "TRAVERSE_REFERENCE"]

@@ -103,6 +103,7 @@ def load():
     L.bih_strerror.argtypes = [i32]
     L.bih_strerror.restype = C.c_char_p
     L.bih_camera_reference.argtypes = [u32, u32, C.POINTER(Camera)]
+    L.bih_camera_ray_bound.argtypes = [C.POINTER(Camera), C.POINTER(C.c_float)]
     L.bih_scene_load_obj.argtypes = [C.c_char_p, C.POINTER(Scene), C.POINTER(u32)]
     L.bih_scene_free.argtypes = [C.POINTER(Scene)]
     L.bih_scene_free.restype = None
@@ -120,7 +121,7 @@ def load():
                                     C.POINTER(Rows), u32, vp, vp, vp]
     L.bih_sync.argtypes = [vp, vp]
     L.bih_last_render_ms.argtypes = [vp, C.POINTER(C.c_double)]
-    for name in ("bih_camera_reference", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
+    for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
                  "bih_render_device", "bih_sync", "bih_last_render_ms"):
         getattr(L, name).restype = i32

@@ -36,7 +36,12 @@ struct bih_tree {
     bool used[kSlots] = {};
     int slot = 0;                    // slot of the next render
     int last_slot = -1;              // slot of the last render
-    hipEvent_t ev_rng = nullptr;     // after the advance that produced rng buffer rng_cur
+    // After the last write to state every render reads, whichever stream
+    // issued it: the advance that produced rng buffer rng_cur, the per-camera
+    // records (prim) and the tree itself (a build or rebuild).  Every render
+    // waits on it, so a render on another stream never reads half-written
+    // records.
+    hipEvent_t ev_rng = nullptr;
     bool rng_pending = false;
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
@@ -177,7 +182,13 @@ int finish_build(bih_tree *tr) {
     // the per-pixel RNG state does not depend on the geometry: a rebuild (the
     // reference rebuilds every frame) keeps the frame sequence going
     tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
-    return map_hip(e);
+    if (e) return map_hip(e);
+    // renders issued on other streams order after the (re)build; tr->stream
+    // waited for every render above, so this also follows the last advance
+    hipError_t he = hipEventRecord(tr->ev_rng, tr->stream);
+    if (he != hipSuccess) return map_hip((int)he);
+    tr->rng_pending = true;
+    return BIH_OK;
 }
 
 int create_tree(int device, void *stream, bih_tree **out) {
@@ -249,6 +260,23 @@ int bih_camera_reference(uint32_t w, uint32_t h, bih_camera *out) {
     out->vertical[0] = 0.0f;
     out->vertical[1] = 2.0f;
     out->vertical[2] = 0.0f;
+    return BIH_OK;
+}
+
+int bih_camera_ray_bound(const bih_camera *cam, float dmax[3]) {
+    if (!cam || !dmax) return BIH_ERR_INVALID;
+    for (int c = 0; c < 3; ++c) {
+        float mx = 0.0f;
+        for (int k = 0; k < 4; ++k) {
+            const float u = (float)(k & 1), v = (float)(k >> 1);
+            const float d = ((cam->lower_left[c] + u * cam->horizontal[c]) + v * cam->vertical[c]) -
+                            cam->origin[c];
+            mx = std::max(mx, std::fabs(d));
+        }
+        const float mag = ((std::fabs(cam->lower_left[c]) + std::fabs(cam->horizontal[c])) +
+                           std::fabs(cam->vertical[c])) + std::fabs(cam->origin[c]);
+        dmax[c] = (mx * 1.001f + 1e-6f) + std::ldexp(mag, -21);
+    }
     return BIH_OK;
 }
 
@@ -350,7 +378,13 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
         info->scene_hi[a] = h.scene_hi[a];
     }
     info->device = tr->t.device;
-    info->device_bytes = tr->t.bytes + (tr->rng_cap * 5 + tr->fb_cap) * 4;
+    // tree + canonical arrays, the XORWOW ring (kRngBufs x 5 planes) and the
+    // per-slot accumulators, the host-path framebuffer, the per-camera
+    // records, and the per-slot tile queues, spill areas and chunk orders
+    info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 +
+                         tr->prim_cap +
+                         ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
+                          (size_t)kSlots * 2 * tr->chunk_cap) * 4;
     info->build_ms = tr->build_ms;
     return BIH_OK;
 }
@@ -496,9 +530,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     // the state cudaRender leaves behind for frame+1 (CUDAKernels.cu:419)
     rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, st));
     if (rc) return rc;
-    hipError_t e = hipEventRecord(tr->ev_rng, st);
-    if (e != hipSuccess) return map_hip((int)e);
-    tr->rng_pending = true;
+    hipError_t e = hipSuccess;
     // primary-ray records follow the camera (the origin; the miss-proof boxes
     // also the direction bounds)
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
@@ -527,18 +559,13 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
             // |D| per component over the primary rays: D = (llc + u h + v vert) - O
             // (Camera.cu:18-20) is affine in (u, v) in [0, 1]^2, so its largest
-            // magnitude is at a corner; slack for the f32 evaluation
+            // magnitude is at a corner.  The kernel evaluates it in f32: four
+            // rounded ops whose results are bounded by |llc|+|h|+|vert|+|O|,
+            // so each adds at most 2^-24 of that; the slack takes 2^-21
+            // (twice the sum) plus a relative 1e-3 (tests/test_miss_box.py
+            // checks it against the kernel's evaluation with offset origins)
             float dmax[3];
-            for (int c = 0; c < 3; ++c) {
-                float mx = 0.0f;
-                for (int k = 0; k < 4; ++k) {
-                    const float u = (float)(k & 1), v = (float)(k >> 1);
-                    const float d = ((cam->lower_left[c] + u * cam->horizontal[c]) +
-                                     v * cam->vertical[c]) - cam->origin[c];
-                    mx = std::max(mx, std::fabs(d));
-                }
-                dmax[c] = mx * 1.001f + 1e-6f;
-            }
+            (void)bih_camera_ray_bound(cam, dmax);
             int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
                                       tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
                                       cam->origin, dmax, tr->prim, st);
@@ -547,6 +574,11 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             tr->prim_valid = true;
         }
     }
+    // the next render (on any stream) orders after the advance above and after
+    // the per-camera records, which it reads as they stand now
+    e = hipEventRecord(tr->ev_rng, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_pending = true;
     bih::RenderArgs a;
     rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
     if (rc) return rc;

@@ -123,6 +123,11 @@ const char *bih_strerror(int code);
 int bih_abi_version(void);
 
 int bih_camera_reference(uint32_t w, uint32_t h, bih_camera *out);
+/* Host only: an upper bound, per component, of |D| over every primary ray of
+ * `camera` as the render kernel evaluates D = ((llc + u*h) + v*vert) - origin
+ * in f32 for u, v in [0, 1] (Camera.cu:18-20).  The any-hit walk's miss-proof
+ * boxes are sized with it. */
+int bih_camera_ray_bound(const bih_camera *camera, float dmax[3]);
 
 /* Scene ingestion (host only, no device): a Wavefront OBJ file flattened to a
  * triangle soup in file order, replacing Model::LoadModel's assimp import

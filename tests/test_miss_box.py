@@ -102,7 +102,7 @@ def _barycentric_bounds(e1, e2, s, dmax):
             F(8) * E + F(1.01) * (Eu + Ev + F(2) * Ed) / den)
 
 
-def _check(v0, v1, v2, O, D):
+def _check(v0, v1, v2, O, D, dmax=None):
     """Every accepted ray: (1) its exact line meets the triangle's plane at
     barycentrics inside miss_box's inflated triangle (float64, exact enough:
     the claim the box rests on); (2) the kernel's slab test passes on the box.
@@ -113,7 +113,10 @@ def _check(v0, v1, v2, O, D):
     s, q, tn = _tri_prim(v0, e1, e2, O)
     with np.errstate(all="ignore"):
         hit, det = _mt(e1, e2, s, q, tn, D)
-        dmax = (np.abs(D) * F(1.001) + F(1e-6)).astype(F)
+        if dmax is None:
+            dmax = (np.abs(D) * F(1.001) + F(1e-6)).astype(F)
+        else:
+            dmax = np.broadcast_to(np.asarray(dmax, F), D.shape)
         lo, hi = _miss_box(e1, e2, s, dmax)
         inside = _slab(lo, hi, D)
         a, b, c = (x.astype(np.float64) for x in _barycentric_bounds(e1, e2, s, dmax))
@@ -187,3 +190,66 @@ def test_miss_box_contains_every_accepted_ray_soup():
     D = (X - O) / (X - O)[:, 2:3]
     h, _, _ = _check(v[:, 0], v[:, 1], v[:, 2], O, D)
     assert h > 50_000
+
+
+def _camera_dir(cam, u, v):
+    """camera_dir (csrc/bih_render.hip), f32, no FMA: D = ((llc + u h) + v vert) - O."""
+    c = np.asarray(cam, F)
+    return np.stack([((c[3 + k] + u * c[6 + k]) + v * c[9 + k]) - c[k] for k in range(3)], 1).astype(F)
+
+
+def _offset_cameras():
+    """Reference-shaped cameras moved far from the origin (|O| up to 1e5 x |D|)
+    and turned, where the f32 evaluation of D rounds by ulp(|llc|+|O|)."""
+    out = []
+    for o, hx, vy, sz in [((2.0, 0.0, -2.0), 3.5555556, 2.0, 1.0),
+                          ((1000.0, -2000.0, 500.0), 3.5555556, 2.0, 1.0),
+                          ((123456.7, 0.5, -98765.4), 2.6666667, 2.0, 1.0),
+                          ((-3.0e4, 7.0e4, 1.0e3), 0.004, 0.003, 0.002)]:
+        o = np.array(o, np.float64)
+        llc = o + np.array([-hx / 2, -vy / 2, sz])
+        out.append(np.concatenate([o, llc, [hx, 0, 0], [0, vy, 0]]).astype(F))
+    return out
+
+
+def test_camera_ray_bound_covers_kernel_directions(bihrt_mod):
+    """bih_camera_ray_bound (the dmax the library sizes the miss-proof boxes
+    with) bounds |D| of every primary ray as the kernel computes it, also for
+    cameras far from the origin, whose f32 D rounds by ulp(|llc| + |O|)."""
+    rng = np.random.default_rng(3)
+    for cam in _offset_cameras():
+        dmax = bihrt_mod.camera_ray_bound(bihrt_mod.Camera.from_list(cam.tolist()))
+        g = np.linspace(0, 1, 257, dtype=F)
+        u = np.concatenate([np.repeat(g, 257), rng.random(200_000).astype(F), [F(1), F(0)]])
+        v = np.concatenate([np.tile(g, 257), rng.random(200_000).astype(F), [F(1), F(1)]])
+        # the (u, v) the kernel forms: (x + r) / W with r in (0, 1]
+        D = _camera_dir(cam, u.astype(F), v.astype(F))
+        assert np.all(np.abs(D) <= dmax[None, :]), (cam, dmax, np.abs(D).max(0))
+
+
+def test_miss_box_offset_origin_at_library_bound(bihrt_mod):
+    """The miss-proof property at the library's own dmax (one bound for all
+    rays of the camera, not the per-ray |D|) with an origin far from zero:
+    near-edge-on triangles placed on the camera's own rays."""
+    rng = np.random.default_rng(17)
+    hits = 0
+    for cam in _offset_cameras()[:3]:
+        dmax = bihrt_mod.camera_ray_bound(bihrt_mod.Camera.from_list(cam.tolist()))
+        O = cam[:3]
+        n = 200_000
+        D = _camera_dir(cam, rng.random(n).astype(F), rng.random(n).astype(F))
+        X = O.astype(np.float64) + rng.uniform(0.5, 3.0, (n, 1)) * D.astype(np.float64)
+        dh = D / np.linalg.norm(D.astype(np.float64), axis=1, keepdims=True)
+        a = np.cross(dh, rng.normal(size=(n, 3)))
+        a /= np.linalg.norm(a, axis=1, keepdims=True)
+        th = 10.0 ** rng.uniform(-6, -0.5, n)[:, None]
+        b = np.cos(th) * dh + np.sin(th) * np.cross(dh, a)
+        size = rng.uniform(0.005, 0.08, (n, 1))
+        al, be = rng.uniform(-0.3, 1.3, (n, 1)), rng.uniform(-0.3, 1.3, (n, 1))
+        v0 = X - size * (al * a + be * b)
+        v1, v2 = v0 + size * b, v0 + size * a
+        flip = rng.random(n) < 0.5
+        v1[flip], v2[flip] = v2[flip].copy(), v1[flip].copy()
+        h, _, _ = _check(v0, v1, v2, O, D, dmax=dmax)
+        hits += h
+    assert hits > 20_000
