@@ -1,0 +1,279 @@
+// bih_bins.hip -- frustum bins: the any-hit walk's acceleration structure for
+// rays that share one origin.
+//
+// Every primary ray of a frame starts at the camera origin O (Camera.cu:18-20)
+// and its direction is fixed by the pixel and the jitter, so the triangles a
+// sample can hit are the ones whose projection onto the image covers it.
+// Per camera and image size, every alive triangle (tri_alive: tnum > 0, the
+// only ones that can produce t > 0) gets a conservative pixel footprint, and
+// every TW x TH pixel tile (one 64-ray packet of the render kernel) a list of
+// the triangles whose footprint touches it:
+//
+//   footprint: the miss-proof bound (miss_bary, bih_bound.h) puts the point
+//     where the exact line of an accepted ray meets the triangle's plane in an
+//     inflated triangle with corners C_j (camera-relative, evaluated in f64
+//     from the f32 record).  When all three corners lie in front of the image
+//     plane (depth C_j . n > 0, n the camera's forward normal), that point has
+//     t > 0 and its projection (u*, v*) lies in the projection of the inflated
+//     triangle, the triangle of the projected corners.  The sample's own
+//     (u, v) -- the kernel's f32 (x + r) / W -- and the f32 D differ from
+//     (u*, v*) by ~1e-6 of the image: the footprint's pixel range is padded
+//     by half a pixel on each side;
+//   behind the camera: all corners at negative depth and tnum_c larger than
+//     its rounding bound (exact t* has the sign of tnum* and det* > 0) --
+//     no primary ray can hit the triangle: no footprint;
+//   anything else (corners on both sides, no bound): the global list, tested
+//     by every packet.
+//
+// A lane of a packet that tests every triangle of its tile's list and of the
+// global list with the exact intersector and finds no hit has no triangle the
+// intersector accepts: a proven miss of the reference walk.  A lane that finds
+// one keeps it as a candidate; it stands only after fast_verify replays the
+// reference's BIH decisions along the leaf's root path (bih_render.hip).
+//
+// Per triangle the footprint also goes into its primary-ray record (k_tri_prim
+// leaves words 13-15 free): r[13] = leaf index, r[14] = x0 | (x1 - x0) << 16,
+// r[15] = y0 | (y1 - y0) << 16 (global pixels), so that the render loop skips
+// a triangle for the lanes outside its footprint without touching MT.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+
+#include "bih_internal.h"
+#include "bih_bound.h"
+
+namespace bih {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ bool alive(const float *prim, uint32_t k) {
+    const uint32_t b = __float_as_uint(prim[16ull * k + 12]);
+    return b - 1u < 0x7f7fffffu;                 // 0 < tnum < +inf (tri_alive)
+}
+
+// r[13] = leaf of each Morton-ordered triangle (the leaf fast_verify checks)
+__global__ void __launch_bounds__(kThreads) k_bin_leaf(const int32_t *__restrict__ first,
+                                                       const uint32_t *__restrict__ cnt, uint32_t U,
+                                                       float *__restrict__ prim) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= U) return;
+    const uint32_t b = (uint32_t)first[k], c = cnt[k];
+    for (uint32_t i = b; i < b + c; ++i) prim[16ull * i + 13] = __uint_as_float(k);
+}
+
+__device__ __forceinline__ double dot3(const double *a, const double *b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
+// by0 | by1 << 16; empty = bx0 > bx1) and the pixel rectangle in r[14..15];
+// the global list takes the rest.
+__global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, uint32_t n,
+                                                     BinCamera c, uint2 *__restrict__ brect,
+                                                     uint32_t *__restrict__ gcount,
+                                                     uint32_t *__restrict__ glist) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    float *r = prim + 16ull * i;
+    const uint2 none = make_uint2(1u, 0u);
+    if (!alive(prim, i)) {
+        brect[i] = none;
+        r[14] = __uint_as_float(1u);   // empty pixel range
+        r[15] = __uint_as_float(1u);
+        return;
+    }
+    float rr[13];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) rr[k] = r[k];
+    float a, b, cc;
+    const bool ok = miss_bary(rr, c.dmax, a, b, cc);
+    int side = 0;                      // 1: all in front, -1: all behind, 0: neither / no bound
+    double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+    if (ok) {
+        const double cu[3] = {-(double)a, 1.0 + (double)b + (double)cc, -(double)a};
+        const double cv[3] = {-(double)b, -(double)b, 1.0 + (double)a + (double)cc};
+        int front = 0, back = 0;
+        for (int j = 0; j < 3; ++j) {
+            double X[3];
+            for (int ax = 0; ax < 3; ++ax)
+                X[ax] = (cu[j] * (double)rr[ax] + cv[j] * (double)rr[3 + ax]) - (double)rr[6 + ax];
+            const double depth = dot3(X, c.n);
+            const double mag = sqrt(dot3(X, X)) * c.nlen;
+            if (depth > 1e-9 * mag) {
+                ++front;
+                // X = lambda (A + u h + v vert), lambda = depth / (A.n)
+                const double inv = c.an / depth;
+                const double u = dot3(X, c.hu) * inv - c.ahu;
+                const double v = dot3(X, c.vv) * inv - c.avv;
+                umin = fmin(umin, u);
+                umax = fmax(umax, u);
+                vmin = fmin(vmin, v);
+                vmax = fmax(vmax, v);
+            } else if (depth < -1e-9 * mag) {
+                ++back;
+            }
+        }
+        if (front == 3) {
+            side = 1;
+        } else if (back == 3) {
+            // exact t* = tnum* / det* with det* > 0 (miss_bary's den); tnum_c
+            // errs by at most 5e |e2|.Q (q_c = cross(s, e1): 2e Q, the dot
+            // 3e): above 8e |e2|.Q its sign is exact, t* > 0, and the hit
+            // point would have positive depth -- none lies behind
+            const double as[3] = {fabs((double)rr[6]), fabs((double)rr[7]), fabs((double)rr[8])};
+            const double ae1[3] = {fabs((double)rr[0]), fabs((double)rr[1]), fabs((double)rr[2])};
+            const double Q[3] = {as[1] * ae1[2] + ae1[1] * as[2], as[2] * ae1[0] + ae1[2] * as[0],
+                                 as[0] * ae1[1] + ae1[0] * as[1]};
+            const double et = 8.0 * 0x1p-24 * (fabs((double)rr[3]) * Q[0] +
+                                               fabs((double)rr[4]) * Q[1] +
+                                               fabs((double)rr[5]) * Q[2]);
+            if ((double)rr[12] > et) side = -1;
+        }
+    }
+    if (side == -1) {
+        brect[i] = none;
+        r[14] = __uint_as_float(1u);
+        r[15] = __uint_as_float(1u);
+        return;
+    }
+    if (side == 0) {                   // every packet tests it
+        brect[i] = none;
+        r[14] = __uint_as_float(0xffff0000u);
+        r[15] = __uint_as_float(0xffff0000u);
+        glist[atomicAdd(gcount, 1u)] = i;
+        return;
+    }
+    // pixel x holds the samples u in (x / W, (x + 1) / W]: pixels
+    // [floor(W umin - 1/2) - 1, floor(W umax + 1/2)], clipped to the image
+    const double W = (double)c.w, H = (double)c.h;
+    const double fx0 = floor(fmax(fmin(umin * W - 0.5, 1e9), -1e9)) - 1.0;
+    const double fx1 = floor(fmax(fmin(umax * W + 0.5, 1e9), -1e9));
+    const double fy0 = floor(fmax(fmin(vmin * H - 0.5, 1e9), -1e9)) - 1.0;
+    const double fy1 = floor(fmax(fmin(vmax * H + 0.5, 1e9), -1e9));
+    if (!(fx1 >= 0.0 && fy1 >= 0.0 && fx0 <= W - 1.0 && fy0 <= H - 1.0)) {
+        brect[i] = none;               // off the image
+        r[14] = __uint_as_float(1u);
+        r[15] = __uint_as_float(1u);
+        return;
+    }
+    const uint32_t x0 = (uint32_t)fmax(fx0, 0.0), x1 = (uint32_t)fmin(fx1, W - 1.0);
+    const uint32_t y0 = (uint32_t)fmax(fy0, 0.0), y1 = (uint32_t)fmin(fy1, H - 1.0);
+    r[14] = __uint_as_float(x0 | ((x1 - x0) << 16));
+    r[15] = __uint_as_float(y0 | ((y1 - y0) << 16));
+    brect[i] = make_uint2((x0 / c.tw) | ((x1 / c.tw) << 16), (y0 / c.th) | ((y1 / c.th) << 16));
+}
+
+__global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect, uint32_t n,
+                                                        uint32_t bins_x, uint32_t *__restrict__ cnt) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint2 q = brect[i];
+    const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+    if (bx0 > bx1) return;
+    for (uint32_t by = by0; by <= by1; ++by)
+        for (uint32_t bx = bx0; bx <= bx1; ++bx) atomicAdd(cnt + by * bins_x + bx, 1u);
+}
+
+__global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect, uint32_t n,
+                                                       uint32_t bins_x, const uint32_t *__restrict__ off,
+                                                       uint32_t *__restrict__ fill,
+                                                       uint32_t *__restrict__ list) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint2 q = brect[i];
+    const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+    if (bx0 > bx1) return;
+    for (uint32_t by = by0; by <= by1; ++by)
+        for (uint32_t bx = bx0; bx <= bx1; ++bx) {
+            const uint32_t b = by * bins_x + bx;
+            list[off[b] + atomicAdd(fill + b, 1u)] = i;
+        }
+}
+
+}  // namespace
+
+bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
+                uint32_t th, BinCamera *out) {
+    const double O[3] = {cam[0], cam[1], cam[2]};
+    double A[3], hh[3], vv[3];
+    for (int k = 0; k < 3; ++k) {
+        A[k] = (double)cam[3 + k] - O[k];
+        hh[k] = cam[6 + k];
+        vv[k] = cam[9 + k];
+    }
+    auto cross = [](const double *a, const double *b, double *o) {
+        o[0] = a[1] * b[2] - a[2] * b[1];
+        o[1] = a[2] * b[0] - a[0] * b[2];
+        o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    auto dot = [](const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    double n[3];
+    cross(hh, vv, n);
+    const double nl = sqrt(dot(n, n)), al = sqrt(dot(A, A));
+    if (!(nl > 0.0) || !(al > 0.0) || !std::isfinite(nl) || !std::isfinite(al)) return false;
+    double an = dot(A, n);
+    if (an < 0.0) {
+        for (double &x : n) x = -x;
+        an = -an;
+    }
+    // every ray direction must point clearly into the front half-space (D.n
+    // = A.n for every (u, v); the f32 D errs by ~1e-6 |D|)
+    if (!(an > 1e-3 * nl * al)) return false;
+    double vn[3], nh[3];
+    cross(vv, n, vn);
+    cross(n, hh, nh);
+    const double hvn = dot(hh, vn), vnh = dot(vv, nh);
+    if (!(fabs(hvn) > 0.0) || !(fabs(vnh) > 0.0)) return false;
+    BinCamera c;
+    for (int k = 0; k < 3; ++k) {
+        c.n[k] = n[k];
+        c.hu[k] = vn[k] / hvn;
+        c.vv[k] = nh[k] / vnh;
+        c.dmax[k] = dmax[k];
+    }
+    c.nlen = nl;
+    c.an = an;
+    c.ahu = dot(A, c.hu);
+    c.avv = dot(A, c.vv);
+    c.w = w;
+    c.h = h;
+    c.tw = tw;
+    c.th = th;
+    *out = c;
+    return true;
+}
+
+int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+                          uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const uint32_t nb = b.bins_x * b.bins_y;
+    hipError_t e = hipMemsetAsync(b.gcount, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    if (U > 0)
+        hipLaunchKernelGGL(k_bin_leaf, dim3((U + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           first_idx, dup_cnt, U, prim);
+    if (n > 0) {
+        const dim3 g((n + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, b.brect, b.gcount, b.glist);
+        hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x, b.cnt);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    // off[nb] = the total (list length)
+    return scan_exclusive(b.cnt, b.off, nb, b.partials, b.off + nb, stream);
+}
+
+int launch_bin_fill(uint32_t n, const BinBuffers &b, uint32_t *list, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const uint32_t nb = b.bins_x * b.bins_y;
+    hipError_t e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    if (n > 0)
+        hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           b.brect, n, b.bins_x, b.off, b.cnt, list);
+    return (int)hipGetLastError();
+}
+
+}  // namespace bih

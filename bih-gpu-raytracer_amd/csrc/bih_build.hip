@@ -586,6 +586,13 @@ static hipError_t dalloc(T **p, size_t count, size_t &bytes) {
     return hipMalloc((void **)p, b);
 }
 
+// exclusive scan for the other translation units (frustum bins)
+int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
+                   uint32_t *total_dev, void *stream) {
+    return (int)exclusive_scan(in, out, n, partials, total_dev, (hipStream_t)stream);
+}
+size_t scan_partials_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
 void free_tree_device(DeviceTree &t) {
     void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
                     t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,

@@ -69,6 +69,16 @@ struct bih_tree {
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
     uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
+    // frustum bins (bih_bins.hip) of the camera the records were built for,
+    // for one image size and tile shape (bins_key = {w, h, spp})
+    char *bins_mem = nullptr;        // brect, cnt, off, gcount, glist, partials
+    size_t bins_mem_cap = 0;         // bytes
+    uint32_t *bin_list = nullptr;
+    size_t bin_list_cap = 0;         // u32
+    bih::BinBuffers bins;
+    bool bins_valid = false;         // built for prim_origin and bins_key
+    bool bins_usable = false;        // built and within the limits (else the kernel skips them)
+    uint32_t bins_key[3] = {0, 0, 0};
 };
 
 namespace {
@@ -182,6 +192,7 @@ int finish_build(bih_tree *tr) {
     // the per-pixel RNG state does not depend on the geometry: a rebuild (the
     // reference rebuilds every frame) keeps the frame sequence going
     tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
+    tr->bins_valid = false;
     if (e) return map_hip(e);
     // renders issued on other streams order after the (re)build; tr->stream
     // waited for every render above, so this also follows the last advance
@@ -352,6 +363,8 @@ void bih_free(bih_tree *tr) {
     if (tr->spill) (void)hipFree(tr->spill);
     if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
     if (tr->prim) (void)hipFree(tr->prim);
+    if (tr->bins_mem) (void)hipFree(tr->bins_mem);
+    if (tr->bin_list) (void)hipFree(tr->bin_list);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
         if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
@@ -382,7 +395,7 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // per-slot accumulators, the host-path framebuffer, the per-camera
     // records, and the per-slot tile queues, spill areas and chunk orders
     info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 +
-                         tr->prim_cap +
+                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 4 +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap) * 4;
     info->build_ms = tr->build_ms;
@@ -483,6 +496,92 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
     return BIH_OK;
 }
 
+// Frustum bins are on unless BIH_BINS=0 (A-B); they never change a pixel.
+static bool bins_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("BIH_BINS");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+// Packet tile of spp samples per pixel (TileShape in bih_render.hip).
+static void tile_shape(uint32_t spp, uint32_t *tw, uint32_t *th) {
+    const int L = __builtin_ctz(spp);
+    const uint32_t lp = 6 - L;
+    *tw = 1u << ((lp + 1) / 2);
+    *th = 1u << (lp / 2);
+}
+
+// (Re)builds the frustum bins for `cam` and a w x h image on `st`, after the
+// primary-ray records; every render that read the old ones has finished
+// (the caller waited for them).  Synchronises `st` once to size the lists.
+static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], uint32_t w,
+                      uint32_t h, uint32_t spp, hipStream_t st) {
+    tr->bins_valid = true;
+    tr->bins_usable = false;
+    tr->bins_key[0] = w;
+    tr->bins_key[1] = h;
+    tr->bins_key[2] = spp;
+    const uint32_t n = tr->t.n, U = tr->t.u;
+    uint32_t tw = 0, th = 0;
+    tile_shape(spp, &tw, &th);
+    bih::BinCamera bc;
+    if (w > 0xffffu || h > 0xffffu || !bih::bin_camera(reinterpret_cast<const float *>(cam), dmax, w, h,
+                                                        tw, th, &bc))
+        return BIH_OK;   // no bins: the kernel runs the shortcut passes instead
+    bih::BinBuffers b;
+    b.bins_x = (w + tw - 1) / tw;
+    b.bins_y = (h + th - 1) / th;
+    const size_t nb = (size_t)b.bins_x * b.bins_y;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t s_brect = al((size_t)n * 8), s_cnt = al(nb * 4), s_off = al((nb + 1) * 4),
+                 s_g = al(4), s_glist = al((size_t)n * 4 + 4),
+                 s_part = al(bih::scan_partials_words((uint32_t)nb) * 4);
+    const size_t need = s_brect + s_cnt + s_off + s_g + s_glist + s_part;
+    if (tr->bins_mem_cap < need) {
+        hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
+        if (e != hipSuccess) return map_hip((int)e);
+        if (tr->bins_mem) (void)hipFree(tr->bins_mem);
+        tr->bins_mem = nullptr;
+        tr->bins_mem_cap = 0;
+        e = hipMalloc((void **)&tr->bins_mem, need);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->bins_mem_cap = need;
+    }
+    char *p = tr->bins_mem;
+    b.brect = reinterpret_cast<uint2 *>(p); p += s_brect;
+    b.cnt = reinterpret_cast<uint32_t *>(p); p += s_cnt;
+    b.off = reinterpret_cast<uint32_t *>(p); p += s_off;
+    b.gcount = reinterpret_cast<uint32_t *>(p); p += s_g;
+    b.glist = reinterpret_cast<uint32_t *>(p); p += s_glist;
+    b.partials = reinterpret_cast<uint32_t *>(p);
+    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.first_idx, tr->t.dup_cnt, U, bc, b, st);
+    if (le) return map_hip(le);
+    uint32_t tot[2] = {0, 0};
+    hipError_t e = hipMemcpyAsync(tot, b.off + nb, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(tot + 1, b.gcount, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return map_hip((int)e);
+    // every packet tests the whole global list: beyond a few thousand
+    // triangles the shortcut passes are the better proof
+    if (tot[1] > 4096) return BIH_OK;
+    if (tr->bin_list_cap < (size_t)tot[0] + 1) {
+        if (tr->bin_list) (void)hipFree(tr->bin_list);
+        tr->bin_list = nullptr;
+        tr->bin_list_cap = 0;
+        const size_t cap = (size_t)tot[0] + tot[0] / 8 + 1024;
+        e = hipMalloc((void **)&tr->bin_list, cap * 4);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->bin_list_cap = cap;
+    }
+    le = bih::launch_bin_fill(n, b, tr->bin_list, st);
+    if (le) return map_hip(le);
+    tr->bins = b;
+    tr->bins_usable = true;
+    return BIH_OK;
+}
+
 int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
                       uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
                       uint32_t *d_out, uint32_t *d_ray_stats, void *stream) {
@@ -572,6 +671,20 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             if (le) return map_hip(le);
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
+            tr->bins_valid = false;
+        }
+        const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
+        if (bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0 &&
+            (!tr->bins_valid || !bins_key_ok)) {
+            if (tr->bins_valid) {
+                // rewritten in place (the records' words 13-15 too)
+                rc = wait_renders(tr, st);
+                if (rc) return rc;
+            }
+            float dmax[3];
+            (void)bih_camera_ray_bound(cam, dmax);
+            rc = build_bins(tr, cam, dmax, w, h, spp, st);
+            if (rc) return rc;
         }
     }
     // the next render (on any stream) orders after the advance above and after
@@ -606,6 +719,19 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
                                                  bih::fast_offset(tr->t.n, n_int));
         if (fast_enabled() > 1) a.fast2 = a.fast + 16ull * (n_int + 1);
+    }
+    if (tr->bins_usable && tr->bins_valid && tr->bins_key[0] == w && tr->bins_key[1] == h &&
+        tr->bins_key[2] == spp && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && tr->prim) {
+        uint32_t tw = 0, th = 0;
+        tile_shape(spp, &tw, &th);
+        // a packet's rows are one bin row when tiles and bands align
+        if (rows.row0 % th == 0 && rows.band_h % th == 0) {
+            a.bin_off = tr->bins.off;
+            a.bin_list = tr->bin_list;
+            a.bin_glist = tr->bins.glist;
+            a.bin_gcount = tr->bins.gcount;
+            a.bins_x = tr->bins.bins_x;
+        }
     }
     a.rng_in = rng_buf(tr, cur);
     a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;

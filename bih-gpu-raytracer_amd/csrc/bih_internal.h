@@ -82,6 +82,35 @@ struct RenderArgs {
     uint32_t *chunk_cost = nullptr;         // packet kernel: per-chunk cycle accumulator (zeroed)
     const float *fast = nullptr;            // any-hit shortcut boxes (k_fast_fit); null: exact walk only
     const float *fast2 = nullptr;           // miss-proof boxes (miss_box); null: no miss proof
+    // frustum bins (bih_bins.hip) of this camera and image: per TW x TH tile
+    // of the full image the triangles whose footprint touches it
+    // (bin_list[bin_off[b] .. bin_off[b+1])), and the global list
+    // (bin_glist[0 .. *bin_gcount)); null: no bins (rows not tile-aligned)
+    const uint32_t *bin_off = nullptr;
+    const uint32_t *bin_list = nullptr;
+    const uint32_t *bin_glist = nullptr;
+    const uint32_t *bin_gcount = nullptr;
+    uint32_t bins_x = 0;
+};
+
+// Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
+// A = lower_left - O), and the (u, v) of a camera-relative point X:
+// u = (X.hu) an / (X.n) - ahu, v = (X.vv) an / (X.n) - avv.
+struct BinCamera {
+    double n[3], hu[3], vv[3];
+    double nlen, an, ahu, avv;
+    float dmax[3];
+    uint32_t w, h, tw, th;
+};
+// Device buffers of the frustum bins.
+struct BinBuffers {
+    uint32_t bins_x = 0, bins_y = 0;
+    uint2 *brect = nullptr;       // [n] bin rectangle per triangle
+    uint32_t *cnt = nullptr;      // [nb] counts / fill cursors
+    uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
+    uint32_t *gcount = nullptr;   // [1] global list length
+    uint32_t *glist = nullptr;    // [n] global list
+    uint32_t *partials = nullptr; // scan scratch
 };
 
 // Device buffers of one tree.
@@ -144,6 +173,19 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
                 uint32_t m, const float origin[3], const float dmax[3], float *prim,
                 void *stream);
 bool render_uses_prim(uint32_t spp);
+
+// frustum bins (bih_bins.hip): camera setup (false: degenerate camera, no
+// bins), footprints + per-tile counts + offsets (needs the primary-ray
+// records; writes their words 13-15), then the lists
+bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
+                uint32_t th, BinCamera *out);
+int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+                          uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
+int launch_bin_fill(uint32_t n, const BinBuffers &b, uint32_t *list, void *stream);
+// exclusive scan of n u32 (bih_build.hip); *total_dev = the sum
+int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
+                   uint32_t *total_dev, void *stream);
+size_t scan_partials_words(uint32_t n);
 
 // host XORWOW helpers (xorwow_host.cpp)
 void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);

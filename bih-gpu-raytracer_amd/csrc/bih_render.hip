@@ -35,6 +35,7 @@
 #include <mutex>
 
 #include "bih_internal.h"
+#include "bih_bound.h"
 #include "bih_packet_asm.h"
 
 namespace bih {
@@ -1607,6 +1608,68 @@ __device__ __forceinline__ bool fast_verify(const uint4 *__restrict__ rec, uint3
     return false;
 }
 
+// Exact MT of prim_hits with the division-free pre-test of the asm walk
+// (BIH_MT, tests/test_mt_prefilter.py): lanes whose u numerator is certain to
+// fail are dropped before the division.  Same f32 expressions, same result.
+__device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, float dx, float dy,
+                                                           float dz, unsigned long long m) {
+    const float px = dy * r[5] - r[4] * dz;          // pvec = cross(D, e2)
+    const float py = dz * r[3] - r[5] * dx;
+    const float pz = dx * r[4] - r[3] * dy;
+    const float det = (r[0] * px + r[1] * py) + r[2] * pz;
+    m &= __ballot(!(det <= kDetEps));                // det < 0.000001 (double); NaN passes
+    if (!m) return 0ull;
+    const float un = (r[6] * px + r[7] * py) + r[8] * pz;
+    m &= __ballot(!(un < -(det * 0x1p-20f) || un > det * (1.0f + 0x1p-20f)));
+    if (!m) return 0ull;
+    const float inv = 1.0f / det;
+    const float u = un * inv;
+    m &= __ballot(!(u < 0.0f || u > 1.0f));
+    if (!m) return 0ull;
+    const float v = ((dx * r[9] + dy * r[10]) + dz * r[11]) * inv;
+    const float t = r[12] * inv;
+    return m & __ballot(!(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX);
+}
+
+// Frustum-bin walk (bih_bins.hip): the packet tests the triangles of its
+// tile's list and then of the global list with the exact intersector, each
+// only for the lanes inside the triangle's pixel footprint (r[14..15]), until
+// every lane of `live` has a hit.  A lane with a hit keeps the triangle's
+// leaf (r[13]) in `cand`; returns the lanes with a candidate.  A lane of
+// `live` without one has tested every triangle whose footprint covers its
+// pixel, i.e. every triangle the exact intersector could accept for its ray:
+// a proven miss.
+#ifndef BIH_BINS
+#define BIH_BINS 1
+#endif
+__device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, const cprim_t *prims,
+                                                      uint32_t bin, uint32_t x, uint32_t y, float dx,
+                                                      float dy, float dz, unsigned long long live,
+                                                      uint32_t lane, uint32_t &cand) {
+    const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
+    const cu32_t *list = (const cu32_t *)(const void *)a.bin_list;
+    uint32_t e = off[bin], end = off[bin + 1];
+    unsigned long long rem = live;
+    const unsigned long long me = lane_bit(lane);
+    for (int part = 0; part < 2; ++part) {
+        for (; e < end && rem; ++e) {
+            const sf32x16 r = prim_rec(prims, list[e]);
+            const uint32_t rx = __float_as_uint(r[14]), ry = __float_as_uint(r[15]);
+            const unsigned long long in =
+                rem & __ballot(x - (rx & 0xffffu) <= (rx >> 16) && y - (ry & 0xffffu) <= (ry >> 16));
+            if (!in) continue;
+            const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
+            if (h & me) cand = __float_as_uint(r[13]);
+            rem &= ~h;
+        }
+        if (!rem) break;
+        list = (const cu32_t *)(const void *)a.bin_glist;
+        e = 0;
+        end = *(const cu32_t *)(const void *)a.bin_gcount;
+    }
+    return live & ~rem;
+}
+
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
 // loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
 // offsets are 32-bit in the loop: used for scenes of < 2^26 triangles.
@@ -1652,10 +1715,10 @@ k_render_packet_asm(const RenderArgs a) {
         const bool valid = x < a.w && lr < a.nrows;
         const uint64_t lp = (uint64_t)lr * a.w + x;
         float dx = 0.f, dy = 0.f, dz = 1.f;
+        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
         if (valid) {
             float ru = 0.f, rv = 0.f;
             ray_jitter<SPP>(a, lp, s, ru, rv);
-            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
             camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
         }
         // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
@@ -1679,6 +1742,22 @@ k_render_packet_asm(const RenderArgs a) {
 #if BIH_FAST_COUNTERS
         uint64_t fc_walk0 = __builtin_amdgcn_s_memtime();
 #endif
+        if (BIH_BINS && ANYHIT && !STATS && a.bin_off && live && sc.U > 1) {
+            // frustum bins: candidates from the tile's triangle list, proven
+            // misses for the lanes without one; a candidate the reference's
+            // walk provably reaches (fast_verify) is a hit.  Only lanes with
+            // an unverified candidate go on to the passes below.
+            const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+            const uint32_t y0 = global_row(ty * TH, a.row0, a.band_h, a.band_step);
+            uint32_t cand = 0;
+            const unsigned long long found =
+                bin_walk(a, prims, (y0 / TH) * a.bins_x + tx, x, y, dx, dy, dz, live, lane, cand);
+            const bool ok = ((found >> lane) & 1ull) &&
+                            fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
+            const unsigned long long ver = __ballot(ok);
+            shortcut |= ver;
+            live &= found & ~ver;
+        }
         if (ANYHIT && !STATS && a.fast && live && sc.U > 1) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
             // provably reaches are done; the others take the exact walk below
@@ -2048,49 +2127,17 @@ __device__ __forceinline__ void fbox_get(float *slot, float lo[3], float hi[3]) 
 }
 
 // Miss-proof box of one alive triangle (camera-relative), from its primary-ray
-// record r = {e1, e2, s = O - v0, q = cross(s, e1), tnum} and dmax[] >= |D|
-// per component for every primary ray of the camera.  Claim: if the exact
-// intersector (RayTriangleIntersection, CUDAKernels.cu:17-50, as the kernels
-// evaluate it: f32, no contraction) returns a hit for direction D, the line
-// O + t D passes through this box.  Proof sketch: the exact line meets the
-// plane of the triangle {v0' + u e1 + v e2} (v0' = O - s, the f32 values MT
-// uses) at barycentrics u* = s.p/det*, v* = D.q/det*, p = D x e2.  The f32
-// evaluation errs by at most (unit roundoff e = 2^-24, first order):
-//   |p_c - p| <= 2e P,  P = (|dy||e2z| + |e2y||dz|, ...)   (abs cross product)
-//   |un_c - s.p|   <= 5e |s|.P     =: Eu
-//   |det_c - e1.p| <= 5e |e1|.P    =: Ed
-//   |vn_c - D.q|   <= 5e |D|.Q     =: Ev,  Q = abs cross(|s|, |e1|) (q_c's own
-//                                           rounding included)
-// A hit has det_c > 1e-6 (kDetEps), u_c in [0, 1], v_c >= 0, u_c + v_c <= 1,
-// so with den = 0.99e-6 - Ed > 0:  u* >= -(4e + Eu/den) =: -a,
-// v* >= -(4e + Ev/den) =: -b,  u* + v* <= 1 + 8e + 1.01 (Eu + Ev + 2 Ed)/den =: 1 + c.
-// The point lies in the triangle of barycentric corners (-a, -b), (1+b+c, -b),
-// (-a, 1+a+c); the box is that triangle's AABB padded by 1e-5 + 1e-6|x| (far
-// more than the slab test's own rounding).  The constants are taken 6e (BIH_MISS_E),
-// not 5e: margin for the second-order terms and the f32 evaluation of the bound.
-// A non-finite bound or den <= 0.5e-6 gives the unbounded box.
-#ifndef BIH_MISS_E
-#define BIH_MISS_E 6   // error constant of miss_box in units of 2^-24 (the analysis gives 5)
-#endif
+// record r and dmax[] (miss_bary, bih_bound.h): the AABB of the inflated
+// triangle of barycentric corners (-a, -b), (1+b+c, -b), (-a, 1+a+c), padded
+// by 1e-5 + 1e-6|x| (far more than the slab test's own rounding).  If the
+// exact intersector returns a hit for direction D, the line O + t D passes
+// through this box.  No bound gives the unbounded box.
 __device__ __forceinline__ void miss_box(const float *r, const float *dmax, float lo[3],
                                          float hi[3]) {
-    const float E = (float)BIH_MISS_E * 0x1p-24f;
     const float e1[3] = {r[0], r[1], r[2]}, e2[3] = {r[3], r[4], r[5]};
     const float sv[3] = {r[6], r[7], r[8]};
-    const float ae1[3] = {fabsf(e1[0]), fabsf(e1[1]), fabsf(e1[2])};
-    const float ae2[3] = {fabsf(e2[0]), fabsf(e2[1]), fabsf(e2[2])};
-    const float as[3] = {fabsf(sv[0]), fabsf(sv[1]), fabsf(sv[2])};
-    const float P[3] = {dmax[1] * ae2[2] + ae2[1] * dmax[2], dmax[2] * ae2[0] + ae2[2] * dmax[0],
-                        dmax[0] * ae2[1] + ae2[0] * dmax[1]};
-    const float Q[3] = {as[1] * ae1[2] + ae1[1] * as[2], as[2] * ae1[0] + ae1[2] * as[0],
-                        as[0] * ae1[1] + ae1[0] * as[1]};
-    const float Eu = E * (as[0] * P[0] + as[1] * P[1] + as[2] * P[2]);
-    const float Ed = E * (ae1[0] * P[0] + ae1[1] * P[1] + ae1[2] * P[2]);
-    const float Ev = E * (dmax[0] * Q[0] + dmax[1] * Q[1] + dmax[2] * Q[2]);
-    const float den = 0.99e-6f - Ed;
-    const float a = 4.0f * E + Eu / den, bb = 4.0f * E + Ev / den;
-    const float c = 8.0f * E + 1.01f * (Eu + Ev + 2.0f * Ed) / den;
-    bool ok = den > 0.5e-6f && a < 1e30f && bb < 1e30f && c < 1e30f;
+    float a, bb, c;
+    bool ok = miss_bary(r, dmax, a, bb, c);
     const float cu[3] = {-a, 1.0f + bb + c, -a}, cv[3] = {-bb, -bb, 1.0f + a + c};
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
