@@ -31,10 +31,24 @@
 // one keeps it as a candidate; it stands only after fast_verify replays the
 // reference's BIH decisions along the leaf's root path (bih_render.hip).
 //
-// Per triangle the footprint also goes into its primary-ray record (k_tri_prim
-// leaves words 13-15 free): r[13] = leaf index, r[14] = x0 | (x1 - x0) << 16,
-// r[15] = y0 | (y1 - y0) << 16 (global pixels), so that the render loop skips
-// a triangle for the lanes outside its footprint without touching MT.
+// List entries are 64-byte records {edge pre-test (9 f32), triangle, leaf}:
+//   edge pre-test: MT accepting direction D implies (miss_bary) the exact
+//     line's barycentrics u* >= -a, v* >= -b, u* + v* <= 1 + c, i.e. with
+//     det* > 0: D.Gu >= 0, D.Gv >= 0, D.Gw >= 0 for Gu = Nu + a Nd,
+//     Gv = Q + b Nd, Gw = (1 + c) Nd - Nu - Q, Nu = e2 x s, Nd = e2 x e1,
+//     Q = s x e1 (exact, from the f32 record).  The kernel's f32 D is
+//     A + u h + v vert + delta (A = lower_left - O, u and v the f32 values it
+//     forms, |delta_i| <= 4e (|llc_i| + |h_i| + |vert_i| + |O_i|)), so
+//     K0 + Ku u + Kv v >= -M with K0 = A.G, Ku = h.G, Kv = vert.G and
+//     M >= |delta|.|G|; the record holds (K0 + M rounded up, Ku, Kv) per
+//     edge with M also covering the f32 rounding of the K's and of the
+//     kernel's fmaf evaluation (x4 margin).  A lane failing one edge cannot
+//     be accepted by MT: the packet skips the triangle for it;
+//   leaf: the leaf holding the triangle (the one fast_verify checks).
+// Per leaf the root path goes into a per-camera table of 32 8-byte steps
+// {clip - O[axis] of the side taken, axis | side << 2}, end = 8 (16: path too
+// deep, never verified), so that the check loads it without a dependent
+// chain.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
@@ -66,11 +80,58 @@ __device__ __forceinline__ double dot3(const double *a, const double *b) {
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
 }
 
+__device__ __forceinline__ void cross3(const double *a, const double *b, double *o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// f32 >= x (x finite): rounded up
+__device__ __forceinline__ float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// The edge pre-test of one triangle (header comment): 3 x {K0 + M, Ku, Kv}.
+__device__ __forceinline__ void edge_pretest(const float *rr, float a, float b, float cc,
+                                             const BinCamera &c, float *out) {
+    double e1[3], e2[3], sv[3];
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = rr[k];
+        e2[k] = rr[3 + k];
+        sv[k] = rr[6 + k];
+    }
+    double Nu[3], Nd[3], Q[3], G[3][3];
+    cross3(e2, sv, Nu);
+    cross3(e2, e1, Nd);
+    cross3(sv, e1, Q);
+    for (int k = 0; k < 3; ++k) {
+        G[0][k] = Nu[k] + (double)a * Nd[k];
+        G[1][k] = Q[k] + (double)b * Nd[k];
+        G[2][k] = (1.0 + (double)cc) * Nd[k] - Nu[k] - Q[k];
+    }
+    const double e = 0x1p-24;
+    for (int j = 0; j < 3; ++j) {
+        const double K0 = dot3(c.A, G[j]), Ku = dot3(c.hh, G[j]), Kv = dot3(c.vert, G[j]);
+        const double dg = fabs(G[j][0]) * c.delta[0] + fabs(G[j][1]) * c.delta[1] +
+                          fabs(G[j][2]) * c.delta[2];
+        // |delta|.|G| (the f64 G errs by ~1e-16 relative), the K roundings
+        // (e each) and the fmaf evaluation (2e of |K0'| + |Ku| + |Kv|, u, v
+        // in [0, 1]); x4
+        const double M = 4.0 * (dg + 8.0 * e * (fabs(K0) + fabs(Ku) + fabs(Kv)) + 1e-30);
+        out[3 * j] = f32_up(K0 + M + 8.0 * e * M);
+        out[3 * j + 1] = (float)Ku;
+        out[3 * j + 2] = (float)Kv;
+    }
+}
+
 // Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
-// by0 | by1 << 16; empty = bx0 > bx1) and the pixel rectangle in r[14..15];
-// the global list takes the rest.
+// by0 | by1 << 16; empty = bx0 > bx1), the pixel rectangle in r[14..15] and
+// its list entry binrec[i]; the global list takes the rest.
 __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, uint32_t n,
                                                      BinCamera c, uint2 *__restrict__ brect,
+                                                     float *__restrict__ binrec,
                                                      uint32_t *__restrict__ gcount,
                                                      uint32_t *__restrict__ glist) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
@@ -137,6 +198,24 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
         r[15] = __uint_as_float(1u);
         return;
     }
+    // the list entry: edge pre-test (or the always-passing one), triangle, leaf
+    {
+        float rec[16];
+        if (ok) {
+            edge_pretest(rr, a, b, cc, c, rec);
+        } else {
+            for (int j = 0; j < 3; ++j) {
+                rec[3 * j] = INFINITY;
+                rec[3 * j + 1] = 0.0f;
+                rec[3 * j + 2] = 0.0f;
+            }
+        }
+        rec[9] = __uint_as_float(i);
+        rec[10] = r[13];
+        for (int k = 11; k < 16; ++k) rec[k] = 0.0f;
+        float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
+        for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+    }
     if (side == 0) {                   // every packet tests it
         brect[i] = none;
         r[14] = __uint_as_float(0xffff0000u);
@@ -175,20 +254,68 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
         for (uint32_t bx = bx0; bx <= bx1; ++bx) atomicAdd(cnt + by * bins_x + bx, 1u);
 }
 
+// A thread per triangle copies its 64-byte entry into each of its tiles' slots.
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect, uint32_t n,
                                                        uint32_t bins_x, const uint32_t *__restrict__ off,
                                                        uint32_t *__restrict__ fill,
-                                                       uint32_t *__restrict__ list) {
+                                                       const float4 *__restrict__ binrec,
+                                                       float4 *__restrict__ list) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
     const uint2 q = brect[i];
     const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
     if (bx0 > bx1) return;
+    const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2],
+                 r3 = binrec[4ull * i + 3];
     for (uint32_t by = by0; by <= by1; ++by)
         for (uint32_t bx = bx0; bx <= bx1; ++bx) {
             const uint32_t b = by * bins_x + bx;
-            list[off[b] + atomicAdd(fill + b, 1u)] = i;
+            float4 *o = list + 4ull * (off[b] + atomicAdd(fill + b, 1u));
+            o[0] = r0;
+            o[1] = r1;
+            o[2] = r2;
+            o[3] = r3;
         }
+}
+
+// The global list's entries (the same 64-byte records).
+__global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restrict__ gcount,
+                                                        const uint32_t *__restrict__ glist,
+                                                        const float4 *__restrict__ binrec,
+                                                        float4 *__restrict__ gent) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= *gcount) return;
+    const uint32_t i = glist[j];
+    for (int k = 0; k < 4; ++k) gent[4ull * j + k] = binrec[4ull * i + k];
+}
+
+// Root path of leaf k as 32 steps root-first (header comment).
+__global__ void __launch_bounds__(kThreads) k_bin_paths(const uint4 *__restrict__ node_prim,
+                                                        const int32_t *__restrict__ leaf_parent,
+                                                        const int32_t *__restrict__ parent,
+                                                        uint32_t U, uint2 *__restrict__ path) {
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= U) return;
+    uint2 *out = path + 32ull * k;
+    int depth = 0;
+    for (int32_t p = leaf_parent[k]; p >= 0 && depth <= 32; p = parent[p]) ++depth;
+    if (depth > 31) {
+        out[0] = make_uint2(0u, 8u | 16u);   // never verified: the exact walk decides
+        return;
+    }
+    uint32_t cidx = k;
+    bool cleaf = true;
+    int j = depth - 1;
+    for (int32_t p = leaf_parent[k]; p >= 0; p = parent[p], --j) {
+        const uint4 r = node_prim[p];
+        const uint32_t split = r.z >> 8, axis = r.z & 0xffu;
+        const bool leafL = (r.w >> 26) & 1u;
+        const uint32_t side = (cidx == split && cleaf == leafL) ? 0u : 1u;
+        out[j] = make_uint2(side ? r.y : r.x, axis | (side << 2));
+        cidx = (uint32_t)p;
+        cleaf = false;
+    }
+    out[depth] = make_uint2(0u, 8u);
 }
 
 }  // namespace
@@ -232,6 +359,14 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
         c.vv[k] = nh[k] / vnh;
         c.dmax[k] = dmax[k];
     }
+    for (int k = 0; k < 3; ++k) {
+        c.A[k] = A[k];
+        c.hh[k] = hh[k];
+        c.vert[k] = vv[k];
+        // |f32 D - exact D(u, v)| per component (header comment): 4e, taken 8e
+        c.delta[k] = 8.0 * 0x1p-24 * (fabs((double)cam[3 + k]) + fabs(hh[k]) + fabs(vv[k]) +
+                                      fabs(O[k]));
+    }
     c.nlen = nl;
     c.an = an;
     c.ahu = dot(A, c.hu);
@@ -245,18 +380,23 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
 }
 
 int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+                          const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
     hipError_t e = hipMemsetAsync(b.gcount, 0, sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
-    if (U > 0)
-        hipLaunchKernelGGL(k_bin_leaf, dim3((U + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           first_idx, dup_cnt, U, prim);
+    if (U > 0) {
+        const dim3 g((U + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_bin_leaf, g, dim3(kThreads), 0, st, first_idx, dup_cnt, U, prim);
+        hipLaunchKernelGGL(k_bin_paths, g, dim3(kThreads), 0, st, node_prim, leaf_parent, parent, U,
+                           b.path);
+    }
     if (n > 0) {
         const dim3 g((n + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, b.brect, b.gcount, b.glist);
+        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, b.brect, b.binrec, b.gcount,
+                           b.glist);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x, b.cnt);
     }
     e = hipGetLastError();
@@ -265,14 +405,20 @@ int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, con
     return scan_exclusive(b.cnt, b.off, nb, b.partials, b.off + nb, stream);
 }
 
-int launch_bin_fill(uint32_t n, const BinBuffers &b, uint32_t *list, void *stream) {
+int launch_bin_fill(uint32_t n, uint32_t gcount, const BinBuffers &b, float *list, float *gent,
+                    void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
     hipError_t e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, n, b.bins_x, b.off, b.cnt, list);
+                           b.brect, n, b.bins_x, b.off, b.cnt,
+                           reinterpret_cast<const float4 *>(b.binrec), reinterpret_cast<float4 *>(list));
+    if (gcount > 0)
+        hipLaunchKernelGGL(k_bin_gfill, dim3((gcount + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           b.gcount, b.glist, reinterpret_cast<const float4 *>(b.binrec),
+                           reinterpret_cast<float4 *>(gent));
     return (int)hipGetLastError();
 }
 

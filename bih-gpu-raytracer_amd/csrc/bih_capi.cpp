@@ -71,14 +71,16 @@ struct bih_tree {
     uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
     // frustum bins (bih_bins.hip) of the camera the records were built for,
     // for one image size and tile shape (bins_key = {w, h, spp})
-    char *bins_mem = nullptr;        // brect, cnt, off, gcount, glist, partials
+    char *bins_mem = nullptr;        // brect, cnt, off, gcount, glist, partials, binrec, path, gent
     size_t bins_mem_cap = 0;         // bytes
-    uint32_t *bin_list = nullptr;
-    size_t bin_list_cap = 0;         // u32
+    float *bin_list = nullptr;       // 64-byte entries
+    size_t bin_list_cap = 0;         // entries
     bih::BinBuffers bins;
     bool bins_valid = false;         // built for prim_origin and bins_key
     bool bins_usable = false;        // built and within the limits (else the kernel skips them)
     uint32_t bins_key[3] = {0, 0, 0};
+    float *bin_gent = nullptr;       // global list entries (in bins_mem)
+    uint32_t bin_gn = 0;             // global list length
 };
 
 namespace {
@@ -395,7 +397,7 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // per-slot accumulators, the host-path framebuffer, the per-camera
     // records, and the per-slot tile queues, spill areas and chunk orders
     info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 +
-                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 4 +
+                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 64 +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap) * 4;
     info->build_ms = tr->build_ms;
@@ -537,8 +539,10 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t s_brect = al((size_t)n * 8), s_cnt = al(nb * 4), s_off = al((nb + 1) * 4),
                  s_g = al(4), s_glist = al((size_t)n * 4 + 4),
-                 s_part = al(bih::scan_partials_words((uint32_t)nb) * 4);
-    const size_t need = s_brect + s_cnt + s_off + s_g + s_glist + s_part;
+                 s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
+                 s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
+                 s_gent = al((size_t)4097 * 64);
+    const size_t need = s_brect + s_cnt + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent;
     if (tr->bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -555,8 +559,13 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.off = reinterpret_cast<uint32_t *>(p); p += s_off;
     b.gcount = reinterpret_cast<uint32_t *>(p); p += s_g;
     b.glist = reinterpret_cast<uint32_t *>(p); p += s_glist;
-    b.partials = reinterpret_cast<uint32_t *>(p);
-    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.first_idx, tr->t.dup_cnt, U, bc, b, st);
+    b.partials = reinterpret_cast<uint32_t *>(p); p += s_part;
+    b.binrec = reinterpret_cast<float *>(p); p += s_rec;
+    b.path = reinterpret_cast<uint2 *>(p); p += s_path;
+    float *gent = reinterpret_cast<float *>(p);
+    const uint4 *node_prim = reinterpret_cast<const uint4 *>(tr->prim + 16ull * n);
+    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
+                                        tr->t.parent, node_prim, U, bc, b, st);
     if (le) return map_hip(le);
     uint32_t tot[2] = {0, 0};
     hipError_t e = hipMemcpyAsync(tot, b.off + nb, 4, hipMemcpyDeviceToHost, st);
@@ -571,13 +580,15 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
         tr->bin_list = nullptr;
         tr->bin_list_cap = 0;
         const size_t cap = (size_t)tot[0] + tot[0] / 8 + 1024;
-        e = hipMalloc((void **)&tr->bin_list, cap * 4);
+        e = hipMalloc((void **)&tr->bin_list, cap * 64);
         if (e != hipSuccess) return map_hip((int)e);
         tr->bin_list_cap = cap;
     }
-    le = bih::launch_bin_fill(n, b, tr->bin_list, st);
+    le = bih::launch_bin_fill(n, tot[1], b, tr->bin_list, gent, st);
     if (le) return map_hip(le);
     tr->bins = b;
+    tr->bin_gent = gent;
+    tr->bin_gn = tot[1];
     tr->bins_usable = true;
     return BIH_OK;
 }
@@ -693,8 +704,28 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
     bih::RenderArgs a;
-    rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
-    if (rc) return rc;
+    bool use_bins = false;
+    if (tr->bins_usable && tr->bins_valid && tr->bins_key[0] == w && tr->bins_key[1] == h &&
+        tr->bins_key[2] == spp && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && tr->prim) {
+        uint32_t tw = 0, th = 0;
+        tile_shape(spp, &tw, &th);
+        // a packet's rows are one bin row when tiles and bands align
+        use_bins = rows.row0 % th == 0 && rows.band_h % th == 0;
+    }
+    if (use_bins) {
+        a.bin_off = tr->bins.off;
+        a.bin_list = tr->bin_list;
+        a.bin_glist = tr->bin_gent;
+        a.bin_gcount = tr->bins.gcount;
+        a.bin_path = tr->bins.path;
+        a.bins_x = tr->bins.bins_x;
+        a.bin_gn = tr->bin_gn;
+    } else {
+        // the cost order pays off for the long BIH walks; with the bins the
+        // packets are short and the order's own launch costs more (A/B)
+        rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
+        if (rc) return rc;
+    }
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;
@@ -719,19 +750,6 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
                                                  bih::fast_offset(tr->t.n, n_int));
         if (fast_enabled() > 1) a.fast2 = a.fast + 16ull * (n_int + 1);
-    }
-    if (tr->bins_usable && tr->bins_valid && tr->bins_key[0] == w && tr->bins_key[1] == h &&
-        tr->bins_key[2] == spp && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && tr->prim) {
-        uint32_t tw = 0, th = 0;
-        tile_shape(spp, &tw, &th);
-        // a packet's rows are one bin row when tiles and bands align
-        if (rows.row0 % th == 0 && rows.band_h % th == 0) {
-            a.bin_off = tr->bins.off;
-            a.bin_list = tr->bin_list;
-            a.bin_glist = tr->bins.glist;
-            a.bin_gcount = tr->bins.gcount;
-            a.bins_x = tr->bins.bins_x;
-        }
     }
     a.rng_in = rng_buf(tr, cur);
     a.pixacc = tr->rng + (size_t)5 * kRngBufs * tr->rng_cap + (size_t)slot * tr->rng_cap;
@@ -831,6 +849,11 @@ int bih_sync(const bih_tree *tr, void *stream) {
                     " exact %llu\n",
                     c[16], c[17], c[18], c[19], c[20], c[21], c[22], c[23], c[24], c[25], c[26],
                     c[28], c[29], cy[0], cy[3], cy[1], cy[2]);
+            const unsigned long long *cb = reinterpret_cast<const unsigned long long *>(c + 48);
+            fprintf(stderr,
+                    "bin-counters packets %u lanes %u entries %u mt %u found %u verified %u"
+                    " unverified %u packets-with-miss %u | cycles walk %llu verify %llu\n",
+                    c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], cb[0], cb[1]);
         }
     }
 #endif

@@ -87,10 +87,12 @@ struct RenderArgs {
     // (bin_list[bin_off[b] .. bin_off[b+1])), and the global list
     // (bin_glist[0 .. *bin_gcount)); null: no bins (rows not tile-aligned)
     const uint32_t *bin_off = nullptr;
-    const uint32_t *bin_list = nullptr;
-    const uint32_t *bin_glist = nullptr;
+    const float *bin_list = nullptr;        // 64-byte entries (bih_bins.hip)
+    const float *bin_glist = nullptr;       // global list entries
     const uint32_t *bin_gcount = nullptr;
+    const uint2 *bin_path = nullptr;        // [U][32] root path steps per leaf
     uint32_t bins_x = 0;
+    uint32_t bin_gn = 0;                    // == *bin_gcount (host copy)
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
@@ -98,6 +100,7 @@ struct RenderArgs {
 // u = (X.hu) an / (X.n) - ahu, v = (X.vv) an / (X.n) - avv.
 struct BinCamera {
     double n[3], hu[3], vv[3];
+    double A[3], hh[3], vert[3], delta[3];   // A = lower_left - O, h, vert, |f32 D - D| bound
     double nlen, an, ahu, avv;
     float dmax[3];
     uint32_t w, h, tw, th;
@@ -109,8 +112,10 @@ struct BinBuffers {
     uint32_t *cnt = nullptr;      // [nb] counts / fill cursors
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
     uint32_t *gcount = nullptr;   // [1] global list length
-    uint32_t *glist = nullptr;    // [n] global list
+    uint32_t *glist = nullptr;    // [n] global list (triangles)
     uint32_t *partials = nullptr; // scan scratch
+    float *binrec = nullptr;      // [n][16] list entry of each triangle
+    uint2 *path = nullptr;        // [U][32] root path steps per leaf
 };
 
 // Device buffers of one tree.
@@ -180,8 +185,11 @@ bool render_uses_prim(uint32_t spp);
 bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
                 uint32_t th, BinCamera *out);
 int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+                          const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
-int launch_bin_fill(uint32_t n, const BinBuffers &b, uint32_t *list, void *stream);
+// lists of 64-byte entries (list: per-tile, gent: the global list's)
+int launch_bin_fill(uint32_t n, uint32_t gcount, const BinBuffers &b, float *list, float *gent,
+                    void *stream);
 // exclusive scan of n u32 (bih_build.hip); *total_dev = the sum
 int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                    uint32_t *total_dev, void *stream);

@@ -1632,42 +1632,158 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 }
 
 // Frustum-bin walk (bih_bins.hip): the packet tests the triangles of its
-// tile's list and then of the global list with the exact intersector, each
-// only for the lanes inside the triangle's pixel footprint (r[14..15]), until
-// every lane of `live` has a hit.  A lane with a hit keeps the triangle's
-// leaf (r[13]) in `cand`; returns the lanes with a candidate.  A lane of
-// `live` without one has tested every triangle whose footprint covers its
-// pixel, i.e. every triangle the exact intersector could accept for its ray:
-// a proven miss.
+// tile's list and then of the global list with the exact intersector until
+// every lane of `live` has a hit.  Each 64-byte entry starts with the
+// triangle's edge pre-test (three affine functions of the lane's f32 (u, v),
+// each >= 0 whenever MT can accept): a lane failing one skips the triangle,
+// and a triangle no remaining lane passes costs no MT.  A lane with a hit
+// keeps the entry's leaf in `cand`; returns the lanes with a candidate.  A
+// lane of `live` without one has tested every triangle the exact intersector
+// could accept for its ray: a proven miss.
 #ifndef BIH_BINS
 #define BIH_BINS 1
 #endif
+// The list is streamed in chunks of 64 entries: lane j loads entry e + j
+// (its first 48 bytes, coalesced vector loads), the next chunk is requested
+// before the current one is consumed, and each entry reaches the scalar unit
+// by v_readlane -- one memory round trip per 64 entries instead of one per
+// entry.
+#ifndef BIH_SKIP_TRACE
+#define BIH_SKIP_TRACE 0
+#endif
+#ifndef BIH_NO_VERIFY
+#define BIH_NO_VERIFY 0
+#endif
+#ifndef BIH_BIN_PREFETCH_AT
+#define BIH_BIN_PREFETCH_AT 16
+#endif
+__device__ __forceinline__ float lane_f(float v, uint32_t j) {
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), j));
+}
+__device__ __forceinline__ void bin_chunk_load(const float4 *ents, uint32_t e, uint32_t end,
+                                               uint32_t lane, float4 &c0, float4 &c1, float4 &c2) {
+    const uint32_t k = e + lane;
+    if (k < end) {
+        const float4 *p = ents + 4ull * k;
+        c0 = p[0];
+        c1 = p[1];
+        c2 = p[2];
+    }
+}
 __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, const cprim_t *prims,
-                                                      uint32_t bin, uint32_t x, uint32_t y, float dx,
+                                                      uint32_t bin, float uf, float vf, float dx,
                                                       float dy, float dz, unsigned long long live,
-                                                      uint32_t lane, uint32_t &cand) {
+                                                      uint32_t lane, uint32_t &cand,
+                                                      uint32_t &fc_ent, uint32_t &fc_mt) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
-    const cu32_t *list = (const cu32_t *)(const void *)a.bin_list;
+    const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
     unsigned long long rem = live;
     const unsigned long long me = lane_bit(lane);
     for (int part = 0; part < 2; ++part) {
-        for (; e < end && rem; ++e) {
-            const sf32x16 r = prim_rec(prims, list[e]);
-            const uint32_t rx = __float_as_uint(r[14]), ry = __float_as_uint(r[15]);
-            const unsigned long long in =
-                rem & __ballot(x - (rx & 0xffffu) <= (rx >> 16) && y - (ry & 0xffffu) <= (ry >> 16));
-            if (!in) continue;
-            const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
-            if (h & me) cand = __float_as_uint(r[13]);
-            rem &= ~h;
+        float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+        if (e < end) bin_chunk_load(ents, e, end, lane, c0, c1, c2);
+        while (e < end && rem) {
+            const float4 d0 = c0, d1 = c1, d2 = c2;
+            const uint32_t n = end - e < 64u ? end - e : 64u;
+            // the next chunk is requested once this one is a quarter done
+            // with lanes left: a packet that ends early leaves no load in
+            // flight for the verification's loads to queue behind (vmcnt
+            // retires in order)
+            for (uint32_t j = 0; j < n && rem; ++j) {
+                if (j == BIH_BIN_PREFETCH_AT && e + 64u < end)
+                    bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
+                const float f0 = __builtin_fmaf(lane_f(d0.z, j), vf,
+                                                __builtin_fmaf(lane_f(d0.y, j), uf, lane_f(d0.x, j)));
+                const float f1 = __builtin_fmaf(lane_f(d1.y, j), vf,
+                                                __builtin_fmaf(lane_f(d1.x, j), uf, lane_f(d0.w, j)));
+                const float f2 = __builtin_fmaf(lane_f(d2.x, j), vf,
+                                                __builtin_fmaf(lane_f(d1.w, j), uf, lane_f(d1.z, j)));
+                const unsigned long long in =
+                    rem & __ballot(!(f0 < 0.0f) && !(f1 < 0.0f) && !(f2 < 0.0f));
+                BIH_FC(++fc_ent);
+                if (!in) continue;
+                BIH_FC(++fc_mt);
+                const sf32x16 r = prim_rec(prims, __builtin_amdgcn_readlane(__float_as_uint(d2.y), j));
+                const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
+                if (h & me) cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
+                rem &= ~h;
+            }
+            if (n <= BIH_BIN_PREFETCH_AT && e + 64u < end)   // (cannot happen: n < 64 is the last chunk)
+                bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
+            e += 64u;
         }
         if (!rem) break;
-        list = (const cu32_t *)(const void *)a.bin_glist;
+        ents = reinterpret_cast<const float4 *>(a.bin_glist);
         e = 0;
-        end = *(const cu32_t *)(const void *)a.bin_gcount;
+        end = a.bin_gn;
     }
     return live & ~rem;
+}
+
+// fast_verify over the leaf's root path from the per-camera path table
+// (bih_bins.hip: 32 steps {clip - O[axis] of the side taken, axis | side << 2}
+// root-first, end 8, 16 = never verified): the same decisions and intervals,
+// with every load's address known up front (no dependent chain).
+__device__ __forceinline__ bool path_step(uint32_t val, uint32_t meta, float ix, float iy, float iz,
+                                          float &lo, float &hi, bool &done, bool &ok) {
+    if (meta & 8u) {
+        done = true;
+        ok = (meta & 16u) == 0u;
+        return false;
+    }
+    const float inv = sel3(meta & 3u, ix, iy, iz);
+    const bool neg = 0.0f > inv;
+    const float t = __uint_as_float(val) * inv;
+    bool g;
+    float nlo, nhi;
+    if (!(meta & 4u)) {                       // left child
+        const float sL = neg ? hi : lo;
+        g = (t > sL) != neg;
+        nlo = neg ? t : lo;
+        nhi = neg ? hi : t;
+    } else {                                  // right child
+        const float sR = neg ? lo : hi;
+        g = (!(t > sR)) != neg;
+        nlo = neg ? lo : t;
+        nhi = neg ? t : hi;
+    }
+    if (!g) {
+        done = true;
+        ok = false;
+        return false;
+    }
+    lo = nlo;
+    hi = nhi;
+    return true;
+}
+// The first 24 steps are requested at once (one round trip for most
+// leaves), the last 8 only by lanes whose path is longer.
+__device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint32_t k, float ix,
+                                            float iy, float iz, float lo, float hi) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(path + 32ull * k);
+    bool done = false, ok = false;
+    {
+        uint4 q[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) q[j] = p[j];
+#pragma unroll
+        for (int j = 0; j < 24; ++j) {
+            const uint4 w = q[j >> 1];
+            if (!path_step((j & 1) ? w.z : w.x, (j & 1) ? w.w : w.y, ix, iy, iz, lo, hi, done, ok))
+                return ok;
+        }
+    }
+    uint4 q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = p[12 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint4 w = q[j >> 1];
+        if (!path_step((j & 1) ? w.z : w.x, (j & 1) ? w.w : w.y, ix, iy, iz, lo, hi, done, ok))
+            return ok;
+    }
+    return false;
 }
 
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
@@ -1714,12 +1830,26 @@ k_render_packet_asm(const RenderArgs a) {
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
         const uint64_t lp = (uint64_t)lr * a.w + x;
-        float dx = 0.f, dy = 0.f, dz = 1.f;
-        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+        uint32_t bin = 0;
+        if (BIH_BINS && ANYHIT && !STATS && a.bin_off) {
+            const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+            bin = (global_row(ty * TH, a.row0, a.band_h, a.band_step) / TH) * a.bins_x + tx;
+            const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
+            if (a.bin_gn == 0 && off[bin] == off[bin + 1]) {
+                // no triangle's footprint touches the tile: every sample is a
+                // proven miss (Color's background), whatever its jitter
+                if (valid && s == SPP - 1) a.out[lp] = pixel_from_hits(0u, SPP);
+                continue;
+            }
+        }
+        float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
         if (valid) {
             float ru = 0.f, rv = 0.f;
             ray_jitter<SPP>(a, lp, s, ru, rv);
-            camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            uf = ((float)x + ru) / fw;
+            vf = ((float)y + rv) / fh;
+            camera_dir(a, uf, vf, dx, dy, dz);
         }
         // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
         const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
@@ -1737,7 +1867,12 @@ k_render_packet_asm(const RenderArgs a) {
         if (tzmin > tMin) tMin = tzmin;
         if (tzmax < tMax) tMax = tzmax;
         uint32_t c_nodes = 0, c_leaves = 0, c_tris = 0;
+#if BIH_SKIP_TRACE   // timing experiments only: the kernel without any traversal
+        unsigned long long live = 0ull;
+        (void)in_box;
+#else
         unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+#endif
         unsigned long long hits = 0ull, shortcut = 0ull;
 #if BIH_FAST_COUNTERS
         uint64_t fc_walk0 = __builtin_amdgcn_s_memtime();
@@ -1747,16 +1882,41 @@ k_render_packet_asm(const RenderArgs a) {
             // misses for the lanes without one; a candidate the reference's
             // walk provably reaches (fast_verify) is a hit.  Only lanes with
             // an unverified candidate go on to the passes below.
-            const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-            const uint32_t y0 = global_row(ty * TH, a.row0, a.band_h, a.band_step);
-            uint32_t cand = 0;
-            const unsigned long long found =
-                bin_walk(a, prims, (y0 / TH) * a.bins_x + tx, x, y, dx, dy, dz, live, lane, cand);
+            uint32_t cand = 0, fc_ent = 0, fc_mt = 0;
+            (void)fc_ent, (void)fc_mt;
+            BIH_FC(const uint64_t fb0 = __builtin_amdgcn_s_memtime());
+            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx,
+                                                      dy, dz, live, lane, cand, fc_ent, fc_mt);
+            BIH_FC(const uint64_t fb1 = __builtin_amdgcn_s_memtime());
+#if BIH_NO_VERIFY   // timing experiments only (takes every candidate as verified)
+            const bool ok = ((found >> lane) & 1ull);
+#else
             const bool ok = ((found >> lane) & 1ull) &&
-                            fast_verify(a.node_prim, cand, ix, iy, iz, tMin, tMax);
+                            path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
+#endif
             const unsigned long long ver = __ballot(ok);
+#if BIH_FAST_COUNTERS
+            const uint64_t fb2 = __builtin_amdgcn_s_memtime();
+            if (lane == 0) {
+                unsigned long long *cy = reinterpret_cast<unsigned long long *>(a.work + 48);
+                atomicAdd(a.work + 40, 1u);
+                atomicAdd(a.work + 41, (uint32_t)__popcll(live));
+                atomicAdd(a.work + 42, fc_ent);
+                atomicAdd(a.work + 43, fc_mt);
+                atomicAdd(a.work + 44, (uint32_t)__popcll(found));
+                atomicAdd(a.work + 45, (uint32_t)__popcll(ver));
+                atomicAdd(a.work + 46, (uint32_t)__popcll(found & ~ver));
+                atomicAdd(a.work + 47, found != live ? 1u : 0u);
+                atomicAdd(cy, (unsigned long long)(fb1 - fb0));
+                atomicAdd(cy + 1, (unsigned long long)(fb2 - fb1));
+            }
+#endif
             shortcut |= ver;
-            live &= found & ~ver;
+            // wave-uniform (the counters' lane-0 branch above hides that from
+            // the compiler, which then keeps live in VGPRs)
+            const unsigned long long nl = live & found & ~ver;
+            live = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(nl >> 32)) << 32) |
+                   __builtin_amdgcn_readfirstlane((uint32_t)nl);
         }
         if (ANYHIT && !STATS && a.fast && live && sc.U > 1) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
@@ -1959,15 +2119,16 @@ k_render_packet_asm(const RenderArgs a) {
 // bands (TileQueue::band_begin), chunks by descending cost (the cycles their
 // longest packet took in an earlier frame of the same geometry), ties by index, so
 // that the slow chunks start first and the frame does not end on one long
-// packet (longest-processing-time-first).  One block per band; the rank of
-// chunk i is the number of band chunks that sort before it.  Bands of more
+// packet (longest-processing-time-first).  One block per band sorts the
+// band's keys (~cost << 32 | index: descending cost, ascending index; padded
+// to a power of two with all-ones keys) bitonically in LDS.  Bands of more
 // than kOrderMax chunks keep the identity order.  Only the order of the work
 // changes, never a pixel.
 constexpr uint32_t kOrderMax = 4096;
 __global__ void __launch_bounds__(kThreads) k_chunk_order(const uint32_t *__restrict__ cost,
                                                           uint32_t chunks_x, uint32_t nchunks,
                                                           uint32_t *__restrict__ order) {
-    __shared__ uint32_t c[kOrderMax];
+    __shared__ unsigned long long key[kOrderMax];
     const uint32_t rows = nchunks / chunks_x, b = blockIdx.x;
     const uint32_t b0 = (uint32_t)(((uint64_t)rows * b) / kRegions) * chunks_x;
     const uint32_t b1 = (uint32_t)(((uint64_t)rows * (b + 1)) / kRegions) * chunks_x;
@@ -1976,17 +2137,27 @@ __global__ void __launch_bounds__(kThreads) k_chunk_order(const uint32_t *__rest
         for (uint32_t i = threadIdx.x; i < n; i += kThreads) order[b0 + i] = b0 + i;
         return;
     }
-    for (uint32_t i = threadIdx.x; i < n; i += kThreads) c[i] = cost[b0 + i];
+    uint32_t np = 1;
+    while (np < n) np <<= 1;
+    for (uint32_t i = threadIdx.x; i < np; i += kThreads)
+        key[i] = i < n ? ((unsigned long long)(~cost[b0 + i]) << 32) | i : ~0ull;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
-        const uint32_t ci = c[i];
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < n; ++j) {
-            const uint32_t cj = c[j];
-            r += (cj > ci || (cj == ci && j < i)) ? 1u : 0u;
+    for (uint32_t k = 2; k <= np; k <<= 1)
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t i = threadIdx.x; i < np; i += kThreads) {
+                const uint32_t l = i ^ jj;
+                if (l > i) {
+                    const unsigned long long x = key[i], y = key[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        key[i] = y;
+                        key[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
         }
-        order[b0 + r] = b0 + i;
-    }
+    for (uint32_t i = threadIdx.x; i < n; i += kThreads) order[b0 + i] = b0 + (uint32_t)key[i];
 }
 
 // A primary ray from O can hit triangle k only if its tnum = dot(e2, q) (the
