@@ -152,27 +152,54 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
     int side = 0;                      // 1: all in front, -1: all behind, 0: neither / no bound
     double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
     if (ok) {
-        const double cu[3] = {-(double)a, 1.0 + (double)b + (double)cc, -(double)a};
-        const double cv[3] = {-(double)b, -(double)b, 1.0 + (double)a + (double)cc};
+        // corners of the inflated triangle: depth and image (u, v)
         int front = 0, back = 0;
-        for (int j = 0; j < 3; ++j) {
-            double X[3];
-            for (int ax = 0; ax < 3; ++ax)
-                X[ax] = (cu[j] * (double)rr[ax] + cv[j] * (double)rr[3 + ax]) - (double)rr[6 + ax];
-            const double depth = dot3(X, c.n);
-            const double mag = sqrt(dot3(X, X)) * c.nlen;
-            if (depth > 1e-9 * mag) {
-                ++front;
-                // X = lambda (A + u h + v vert), lambda = depth / (A.n)
-                const double inv = c.an / depth;
-                const double u = dot3(X, c.hu) * inv - c.ahu;
-                const double v = dot3(X, c.vv) * inv - c.avv;
-                umin = fmin(umin, u);
-                umax = fmax(umax, u);
-                vmin = fmin(vmin, v);
-                vmax = fmax(vmax, v);
-            } else if (depth < -1e-9 * mag) {
-                ++back;
+        double max_depth = 0.0;
+        auto corners = [&](float a_, float b_, float c_) {
+            const double cu[3] = {-(double)a_, 1.0 + (double)b_ + (double)c_, -(double)a_};
+            const double cv[3] = {-(double)b_, -(double)b_, 1.0 + (double)a_ + (double)c_};
+            front = back = 0;
+            max_depth = 0.0;
+            umin = vmin = INFINITY;
+            umax = vmax = -INFINITY;
+            for (int j = 0; j < 3; ++j) {
+                double X[3];
+                for (int ax = 0; ax < 3; ++ax)
+                    X[ax] = (cu[j] * (double)rr[ax] + cv[j] * (double)rr[3 + ax]) - (double)rr[6 + ax];
+                const double depth = dot3(X, c.n);
+                const double mag = sqrt(dot3(X, X)) * c.nlen;
+                if (depth > 1e-9 * mag) {
+                    ++front;
+                    max_depth = fmax(max_depth, depth);
+                    // X = lambda (A + u h + v vert), lambda = depth / (A.n)
+                    const double inv = c.an / depth;
+                    const double u = dot3(X, c.hu) * inv - c.ahu;
+                    const double v = dot3(X, c.vv) * inv - c.avv;
+                    umin = fmin(umin, u);
+                    umax = fmax(umax, u);
+                    vmin = fmin(vmin, v);
+                    vmax = fmax(vmax, v);
+                } else if (depth < -1e-9 * mag) {
+                    ++back;
+                }
+            }
+        };
+        corners(a, b, cc);
+        if (front == 3) {
+            // the inflated triangle lies in front of the camera: the exact det
+            // of an accepted ray has a geometric lower bound (det_lower_bound),
+            // usually far above 1e-6 -- a much tighter inflation, a smaller
+            // footprint and a sharper pre-test (the refined triangle lies
+            // inside the first, so it is still in front)
+            const double L = det_lower_bound(rr, c.dn_lb, max_depth);
+            if (L > 0.0) {
+                float a2, b2, c2;
+                if (miss_bary(rr, c.dmax, a2, b2, c2, (float)L) && a2 <= a && b2 <= b && c2 <= cc) {
+                    a = a2;
+                    b = b2;
+                    cc = c2;
+                    corners(a, b, cc);
+                }
             }
         }
         if (front == 3) {
@@ -243,21 +270,64 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
     brect[i] = make_uint2((x0 / c.tw) | ((x1 / c.tw) << 16), (y0 / c.th) | ((y1 / c.th) << 16));
 }
 
+// Tile (bx, by) against a triangle's edge pre-test (k0..k8 = 3 x {K0', Ku,
+// Kv}, the kernel evaluates fmaf(Kv, v, fmaf(Ku, u, K0'))): 0 = no sample of
+// the tile passes all three edges (the triangle stays off the tile's list),
+// 2 = every sample passes (listed first: it most likely hits every lane),
+// 1 = otherwise.  A sample of pixel x has u = fl(fl(x + r) / W), r in (0, 1]:
+// u in [x / W, (x + 1) / W] up to 2 roundings (|u| <= 1; padded 2^-20).  Over
+// the tile's (u, v) rectangle the affine function ranges over [lo, hi]
+// (f64, exact enough); the kernel's two fmaf roundings err by at most
+// 2e (|K0'| + |Ku| + |Kv|), taken 4e (sl).  NaN / inf coefficients never
+// exclude a tile.
+__device__ __forceinline__ int tile_class(const float4 r0, const float4 r1, const float4 r2,
+                                          uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
+                                          uint32_t tw, uint32_t th) {
+    const double pad = 0x1p-20;
+    const uint32_t xe = (bx + 1) * tw < w ? (bx + 1) * tw : w;
+    const uint32_t ye = (by + 1) * th < h ? (by + 1) * th : h;
+    const double u0 = (double)(bx * tw) / w - pad, u1 = (double)xe / w + pad;
+    const double v0 = (double)(by * th) / h - pad, v1 = (double)ye / h + pad;
+    const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const double K0 = k[3 * j], Ku = k[3 * j + 1], Kv = k[3 * j + 2];
+        const double sl = 0x1p-22 * (fabs(K0) + fabs(Ku) + fabs(Kv));
+        const double hi = K0 + fmax(Ku * u0, Ku * u1) + fmax(Kv * v0, Kv * v1);
+        const double lo = K0 + fmin(Ku * u0, Ku * u1) + fmin(Kv * v0, Kv * v1);
+        if (hi < -sl) return 0;
+        if (!(lo > sl)) all = false;
+    }
+    return all ? 2 : 1;
+}
+
 __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect, uint32_t n,
-                                                        uint32_t bins_x, uint32_t *__restrict__ cnt) {
+                                                        uint32_t bins_x, const float4 *__restrict__ binrec,
+                                                        uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
+                                                        uint32_t *__restrict__ cnt) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
     const uint2 q = brect[i];
     const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
     if (bx0 > bx1) return;
+    const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
     for (uint32_t by = by0; by <= by1; ++by)
-        for (uint32_t bx = bx0; bx <= bx1; ++bx) atomicAdd(cnt + by * bins_x + bx, 1u);
+        for (uint32_t bx = bx0; bx <= bx1; ++bx)
+            if (tile_class(r0, r1, r2, bx, by, w, h, tw, th)) atomicAdd(cnt + by * bins_x + bx, 1u);
 }
 
-// A thread per triangle copies its 64-byte entry into each of its tiles' slots.
+// A thread per triangle copies its 64-byte entry into each of its tiles'
+// lists: every-sample entries from the front (fill), the others from the
+// back (fill2), so a packet meets the triangles that cover its whole tile
+// first.  The order within each part follows the atomics (it can change
+// which candidate a lane verifies, never a pixel).
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect, uint32_t n,
-                                                       uint32_t bins_x, const uint32_t *__restrict__ off,
+                                                       uint32_t bins_x, uint32_t w, uint32_t h,
+                                                       uint32_t tw, uint32_t th,
+                                                       const uint32_t *__restrict__ off,
                                                        uint32_t *__restrict__ fill,
+                                                       uint32_t *__restrict__ fill2,
                                                        const float4 *__restrict__ binrec,
                                                        float4 *__restrict__ list) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
@@ -269,8 +339,12 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                  r3 = binrec[4ull * i + 3];
     for (uint32_t by = by0; by <= by1; ++by)
         for (uint32_t bx = bx0; bx <= bx1; ++bx) {
+            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+            if (!cls) continue;
             const uint32_t b = by * bins_x + bx;
-            float4 *o = list + 4ull * (off[b] + atomicAdd(fill + b, 1u));
+            const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
+                                          : off[b + 1] - 1u - atomicAdd(fill2 + b, 1u);
+            float4 *o = list + 4ull * pos;
             o[0] = r0;
             o[1] = r1;
             o[2] = r2;
@@ -369,6 +443,8 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
     }
     c.nlen = nl;
     c.an = an;
+    // D.n = A.n exactly for D(u, v); the f32 D errs by delta per component
+    c.dn_lb = an - 2.0 * (c.delta[0] * fabs(n[0]) + c.delta[1] * fabs(n[1]) + c.delta[2] * fabs(n[2]));
     c.ahu = dot(A, c.hu);
     c.avv = dot(A, c.vv);
     c.w = w;
@@ -397,7 +473,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, con
         const dim3 g((n + kThreads - 1) / kThreads);
         hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, b.brect, b.binrec, b.gcount,
                            b.glist);
-        hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x, b.cnt);
+        hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x,
+                           reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
@@ -405,15 +482,16 @@ int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, con
     return scan_exclusive(b.cnt, b.off, nb, b.partials, b.off + nb, stream);
 }
 
-int launch_bin_fill(uint32_t n, uint32_t gcount, const BinBuffers &b, float *list, float *gent,
-                    void *stream) {
+int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBuffers &b, float *list,
+                    float *gent, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
     hipError_t e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(b.cnt2, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, n, b.bins_x, b.off, b.cnt,
+                           b.brect, n, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt, b.cnt2,
                            reinterpret_cast<const float4 *>(b.binrec), reinterpret_cast<float4 *>(list));
     if (gcount > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((gcount + kThreads - 1) / kThreads), dim3(kThreads), 0, st,

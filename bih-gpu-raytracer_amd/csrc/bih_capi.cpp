@@ -537,12 +537,12 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.bins_y = (h + th - 1) / th;
     const size_t nb = (size_t)b.bins_x * b.bins_y;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t s_brect = al((size_t)n * 8), s_cnt = al(nb * 4), s_off = al((nb + 1) * 4),
+    const size_t s_brect = al((size_t)n * 8), s_cnt = al(nb * 4), s_cnt2 = al(nb * 4), s_off = al((nb + 1) * 4),
                  s_g = al(4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
                  s_gent = al((size_t)4097 * 64);
-    const size_t need = s_brect + s_cnt + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent;
+    const size_t need = s_brect + s_cnt + s_cnt2 + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent;
     if (tr->bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -556,6 +556,7 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     char *p = tr->bins_mem;
     b.brect = reinterpret_cast<uint2 *>(p); p += s_brect;
     b.cnt = reinterpret_cast<uint32_t *>(p); p += s_cnt;
+    b.cnt2 = reinterpret_cast<uint32_t *>(p); p += s_cnt2;
     b.off = reinterpret_cast<uint32_t *>(p); p += s_off;
     b.gcount = reinterpret_cast<uint32_t *>(p); p += s_g;
     b.glist = reinterpret_cast<uint32_t *>(p); p += s_glist;
@@ -584,7 +585,7 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
         if (e != hipSuccess) return map_hip((int)e);
         tr->bin_list_cap = cap;
     }
-    le = bih::launch_bin_fill(n, tot[1], b, tr->bin_list, gent, st);
+    le = bih::launch_bin_fill(n, tot[1], bc, b, tr->bin_list, gent, st);
     if (le) return map_hip(le);
     tr->bins = b;
     tr->bin_gent = gent;

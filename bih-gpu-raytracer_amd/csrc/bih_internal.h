@@ -102,6 +102,7 @@ struct BinCamera {
     double n[3], hu[3], vv[3];
     double A[3], hh[3], vert[3], delta[3];   // A = lower_left - O, h, vert, |f32 D - D| bound
     double nlen, an, ahu, avv;
+    double dn_lb;                             // <= D.n of every f32 primary ray (det_lower_bound)
     float dmax[3];
     uint32_t w, h, tw, th;
 };
@@ -109,7 +110,8 @@ struct BinCamera {
 struct BinBuffers {
     uint32_t bins_x = 0, bins_y = 0;
     uint2 *brect = nullptr;       // [n] bin rectangle per triangle
-    uint32_t *cnt = nullptr;      // [nb] counts / fill cursors
+    uint32_t *cnt = nullptr;      // [nb] counts / fill cursors (front)
+    uint32_t *cnt2 = nullptr;     // [nb] fill cursors (back)
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
     uint32_t *gcount = nullptr;   // [1] global list length
     uint32_t *glist = nullptr;    // [n] global list (triangles)
@@ -188,8 +190,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, con
                           const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
 // lists of 64-byte entries (list: per-tile, gent: the global list's)
-int launch_bin_fill(uint32_t n, uint32_t gcount, const BinBuffers &b, float *list, float *gent,
-                    void *stream);
+int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBuffers &b, float *list,
+                    float *gent, void *stream);
 // exclusive scan of n u32 (bih_build.hip); *total_dev = the sum
 int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                    uint32_t *total_dev, void *stream);

@@ -8,6 +8,7 @@ kernel forms and D its f32 camera_dir.  A numpy restatement of the pre-test
 near-edge-on triangles and a soup for the reference camera and cameras far
 from the origin, at the library's own dmax (bih_camera_ray_bound)."""
 import numpy as np
+import pytest
 
 from test_miss_box import F, _barycentric_bounds, _camera_dir, _mt, _offset_cameras, _tri_prim
 
@@ -134,3 +135,201 @@ def test_edge_pretest_soup_reference_camera(bihrt_mod):
     vq = np.clip(Y[:, 1] / vv[1], 0, 1).astype(F)
     h, m, dr = _check(cam, dmax, v[:, 0], v[:, 1], v[:, 2], u, vq)
     assert h > 20_000 and dr > 0.5 * m, (h, m, dr)
+
+
+def _bin_camera(cam):
+    """bin_camera's n (A.n > 0), A.n and dn_lb (bih_bins.hip)."""
+    cam = np.asarray(cam, np.float64)
+    O, llc, h, vert = cam[:3], cam[3:6], cam[6:9], cam[9:12]
+    A = llc - O
+    n = np.cross(h, vert)
+    if A @ n < 0:
+        n = -n
+    delta = 8.0 * E * (np.abs(llc) + np.abs(h) + np.abs(vert) + np.abs(O))
+    an = A @ n
+    return n, an, an - 2.0 * (delta @ np.abs(n))
+
+
+def _refined_bounds(e1, e2, s, tn, dmax, cam):
+    """k_bin_fp's refinement: coarse a, b, c; when every corner of the
+    inflated triangle lies in front, det >= 0.99 (tnum_c - 8e |e2|.Q) dn_lb /
+    max depth (det_lower_bound, bih_bound.h), and a, b, c are recomputed with
+    that den (miss_bary's den_lb).  Returns a, b, c, the mask where the
+    refinement applied."""
+    n, an, dn_lb = _bin_camera(cam)
+    a, b, c = _barycentric_bounds(e1, e2, s, dmax)
+    e164, e264, s64 = (x.astype(np.float64) for x in (e1, e2, s))
+    cu = [-a.astype(np.float64), 1.0 + b.astype(np.float64) + c.astype(np.float64), -a.astype(np.float64)]
+    cv = [-b.astype(np.float64), -b.astype(np.float64), 1.0 + a.astype(np.float64) + c.astype(np.float64)]
+    front = np.ones(len(a), bool)
+    maxd = np.zeros(len(a))
+    for j in range(3):
+        X = cu[j][:, None] * e164 + cv[j][:, None] * e264 - s64
+        d = X @ n
+        front &= d > 1e-9 * np.linalg.norm(X, axis=1) * np.linalg.norm(n)
+        maxd = np.maximum(maxd, d)
+    as_, ae1 = np.abs(s64), np.abs(e164)
+    Q = np.stack([as_[:, 1] * ae1[:, 2] + ae1[:, 1] * as_[:, 2],
+                  as_[:, 2] * ae1[:, 0] + ae1[:, 2] * as_[:, 0],
+                  as_[:, 0] * ae1[:, 1] + ae1[:, 0] * as_[:, 1]], 1)
+    et = 8.0 * E * np.einsum("ij,ij->i", np.abs(e264), Q)
+    tlb = tn.astype(np.float64) - et
+    with np.errstate(all="ignore"):
+        L = 0.99 * tlb * dn_lb / maxd
+    use = front & (tlb > 0) & (maxd > 0) & (L < 1e30)
+    Em = F(6.0 * 2.0 ** -24)
+    ae1f, ae2f, asf = np.abs(e1), np.abs(e2), np.abs(s)
+    P = np.stack([dmax[:, 1] * ae2f[:, 2] + ae2f[:, 1] * dmax[:, 2],
+                  dmax[:, 2] * ae2f[:, 0] + ae2f[:, 2] * dmax[:, 0],
+                  dmax[:, 0] * ae2f[:, 1] + ae2f[:, 0] * dmax[:, 1]], 1).astype(F)
+    Qf = np.stack([asf[:, 1] * ae1f[:, 2] + ae1f[:, 1] * asf[:, 2],
+                   asf[:, 2] * ae1f[:, 0] + ae1f[:, 2] * asf[:, 0],
+                   asf[:, 0] * ae1f[:, 1] + ae1f[:, 0] * asf[:, 1]], 1).astype(F)
+    dot = lambda x, y: (x[:, 0] * y[:, 0] + x[:, 1] * y[:, 1]) + x[:, 2] * y[:, 2]
+    Eu, Ed, Ev = Em * dot(asf, P), Em * dot(ae1f, P), Em * dot(dmax, Qf)
+    den0 = F(0.99e-6) - Ed
+    Lf = np.where(use, L, 0).astype(F)
+    den = np.maximum(den0, Lf)
+    a2 = F(4) * Em + Eu / den
+    b2 = F(4) * Em + Ev / den
+    c2 = F(8) * Em + F(1.01) * (Eu + Ev + F(2) * Ed) / den
+    take = use & (a2 <= a) & (b2 <= b) & (c2 <= c)
+    return np.where(take, a2, a), np.where(take, b2, b), np.where(take, c2, c), take
+
+
+def _check_refined(cam, dmax, v0, v1, v2, u, v):
+    """Accepted rays: exact-line barycentrics inside the refined inflated
+    triangle and the refined pre-test passed.  Returns (accepted, accepted
+    under a refined bound, largest excursion / refined bound)."""
+    O = np.asarray(cam[:3], F)
+    D = _camera_dir(cam, u, v)
+    v0, v1, v2 = (np.asarray(x, F) for x in (v0, v1, v2))
+    e1, e2 = (v1 - v0).astype(F), (v2 - v0).astype(F)
+    s, q, tn = _tri_prim(v0, e1, e2, O)
+    with np.errstate(all="ignore"):
+        hit, _ = _mt(e1, e2, s, q, tn, D)
+        dm = np.broadcast_to(np.asarray(dmax, F), D.shape)
+        a0, b0, c0 = _barycentric_bounds(e1, e2, s, dm)
+        ok = ((F(0.99e-6) - _ed(e1, e2, dm)) > F(0.5e-6)) & (a0 < F(1e30)) & (b0 < F(1e30)) & \
+            (c0 < F(1e30)) & (tn > 0)
+        a, b, c, ref = _refined_bounds(e1, e2, s, tn, dm, cam)
+        co = _pretest_coeffs(e1, e2, s, a, b, c, cam)
+        passed = np.ones(len(u), bool)
+        for K0, Ku, Kv in co:
+            f = _fmaf(Kv, v, _fmaf(Ku, u, K0))
+            passed &= ~(f < 0)
+        s64, e164, e264, D64 = (x.astype(np.float64) for x in (s, e1, e2, D))
+        p = np.cross(D64, e264)
+        det64 = np.einsum("ij,ij->i", e164, p)
+        uu = np.einsum("ij,ij->i", s64, p) / det64
+        vv = np.einsum("ij,ij->i", D64, np.cross(s64, e164)) / det64
+    h = hit & ok
+    a, b, c = (x.astype(np.float64) for x in (a, b, c))
+    assert np.all(uu[h] >= -a[h]) and np.all(vv[h] >= -b[h]) and np.all(uu[h] + vv[h] <= 1 + c[h])
+    assert not np.any(h & ~passed), int((h & ~passed).sum())
+    hr = h & ref
+    ratio = np.max(np.concatenate([(-uu[hr]) / a[hr], (-vv[hr]) / b[hr], (uu[hr] + vv[hr] - 1) / c[hr],
+                                   [0.0]]))
+    return int(h.sum()), int(hr.sum()), ratio
+
+
+def test_refined_bound_keeps_every_accepted_ray(bihrt_mod):
+    """det_lower_bound (bih_bound.h): the tighter inflation still contains the
+    exact-line barycentrics of every accepted ray and the pre-test built from
+    it keeps them -- near-edge-on triangles (det down to 1e-6), offset cameras."""
+    rng = np.random.default_rng(33)
+    acc = refd = 0
+    worst = 0.0
+    for cam in _offset_cameras()[:3]:
+        dmax = bihrt_mod.camera_ray_bound(bihrt_mod.Camera.from_list(cam.tolist()))
+        for edge_on in (True, False):
+            h, r, w = _check_refined(cam, dmax, *_scene_on_rays(cam, 150_000, rng, edge_on))
+            acc, refd, worst = acc + h, refd + r, max(worst, w)
+    assert acc > 50_000 and refd > 0.5 * acc, (acc, refd)
+    assert worst > 0.005, worst        # accepted rays do approach the refined bound
+
+
+def test_refined_bound_soup_reference_camera(bihrt_mod):
+    """The bench's soup shape: the refinement applies to nearly every
+    triangle and shrinks the inflation by orders of magnitude."""
+    rng = np.random.default_rng(8)
+    cam = np.asarray(bihrt_mod.camera_reference(1920, 1080).as_list(), F)
+    dmax = bihrt_mod.camera_ray_bound(bihrt_mod.Camera.from_list(cam.tolist()))
+    n = 300_000
+    c = np.stack([rng.uniform(0, 2.6667, n), rng.uniform(-1, 1, n), rng.uniform(0, 2, n)], 1)
+    v = c[:, None, :] + rng.uniform(-0.02, 0.02, (n, 3, 3))
+    w = rng.uniform(-0.01, 1.01, (n, 2))
+    X = v[:, 0] + w[:, :1] * (v[:, 1] - v[:, 0]) + w[:, 1:] * (v[:, 2] - v[:, 0])
+    O, llc, hh, vv = (cam[3 * k:3 * k + 3].astype(np.float64) for k in range(4))
+    d = X - O
+    lam = (llc - O)[2] / d[:, 2]
+    Y = d * lam[:, None] - (llc - O)
+    u = np.clip(Y[:, 0] / hh[0], 0, 1).astype(F)
+    vq = np.clip(Y[:, 1] / vv[1], 0, 1).astype(F)
+    h, r, _ = _check_refined(cam, dmax, v[:, 0], v[:, 1], v[:, 2], u, vq)
+    assert h > 50_000 and r > 0.95 * h, (h, r)
+
+
+def _tile_class(K, bx, by, w, h, tw, th):
+    """tile_class (bih_bins.hip) on f32 coefficient triples K = [(K0, Ku, Kv)] x 3."""
+    pad = 2.0 ** -20
+    xe = np.minimum((bx + 1) * tw, w)
+    ye = np.minimum((by + 1) * th, h)
+    u0, u1 = bx * tw / w - pad, xe / w + pad
+    v0, v1 = by * th / h - pad, ye / h + pad
+    out = np.full(len(bx), 2)
+    for K0, Ku, Kv in K:
+        K0, Ku, Kv = (x.astype(np.float64) for x in (K0, Ku, Kv))
+        sl = 2.0 ** -22 * (np.abs(K0) + np.abs(Ku) + np.abs(Kv))
+        hi = K0 + np.maximum(Ku * u0, Ku * u1) + np.maximum(Kv * v0, Kv * v1)
+        lo = K0 + np.minimum(Ku * u0, Ku * u1) + np.minimum(Kv * v0, Kv * v1)
+        with np.errstate(invalid="ignore"):
+            out = np.where(hi < -sl, 0, np.where(~(lo > sl), np.minimum(out, 1), out))
+    return out
+
+
+@pytest.mark.parametrize("size", [0.02, 0.3])
+def test_tile_class_keeps_passing_samples(bihrt_mod, size):
+    """A tile is dropped from a triangle's list only when no sample of it can
+    pass the pre-test; a tile classed 'every sample passes' has every sample
+    pass.  Samples at the kernel's f32 (x + r) / W, r in (0, 1].  Bench-size
+    triangles (~5 px) and large ones (~80 px, tiles inside them)."""
+    rng = np.random.default_rng(12)
+    W, H, tw, th = 1920, 1080, 4, 4
+    cam = np.asarray(bihrt_mod.camera_reference(W, H).as_list(), F)
+    dmax = bihrt_mod.camera_ray_bound(bihrt_mod.Camera.from_list(cam.tolist()))
+    n = 200_000
+    c = np.stack([rng.uniform(0, 2.6667, n), rng.uniform(-1, 1, n), rng.uniform(0, 2, n)], 1)
+    v = (c[:, None, :] + rng.uniform(-size, size, (n, 3, 3))).astype(F)
+    O = cam[:3]
+    e1, e2 = (v[:, 1] - v[:, 0]).astype(F), (v[:, 2] - v[:, 0]).astype(F)
+    s, q, tn = _tri_prim(v[:, 0], e1, e2, O)
+    dm = np.broadcast_to(np.asarray(dmax, F), e1.shape)
+    with np.errstate(all="ignore"):
+        a, b, cc, _ = _refined_bounds(e1, e2, s, tn, dm, cam)
+        K = _pretest_coeffs(e1, e2, s, a, b, cc, cam)
+    # a sample pixel near each triangle's projection, random jitter
+    Xc = v.mean(1).astype(np.float64)
+    llc, hh, vv = (cam[3 * k:3 * k + 3].astype(np.float64) for k in (1, 2, 3))
+    d = Xc - O
+    lam = (llc - O)[2] / d[:, 2]
+    Y = d * lam[:, None] - (llc - O)
+    sp = int(400 * size)
+    px = np.clip((Y[:, 0] / hh[0] * W).astype(np.int64) + rng.integers(-sp, sp + 1, n), 0, W - 1)
+    py = np.clip((Y[:, 1] / vv[1] * H).astype(np.int64) + rng.integers(-sp, sp + 1, n), 0, H - 1)
+    r1 = np.maximum(rng.random(n).astype(F), F(2.0 ** -32))
+    r2 = np.maximum(rng.random(n).astype(F), F(2.0 ** -32))
+    u = ((px.astype(F) + r1).astype(F) / F(W)).astype(F)
+    vq = ((py.astype(F) + r2).astype(F) / F(H)).astype(F)
+    passed = np.ones(n, bool)
+    with np.errstate(all="ignore"):
+        for K0, Ku, Kv in K:
+            passed &= ~(_fmaf(Kv, vq, _fmaf(Ku, u, K0)) < 0)
+    cls = _tile_class(K, px // tw, py // th, W, H, tw, th)
+    assert not np.any(passed & (cls == 0)), int((passed & (cls == 0)).sum())
+    assert np.all(passed[cls == 2])
+    # the test has teeth: many tiles are dropped (and, for the large
+    # triangles, many are fully covered)
+    assert (cls == 0).sum() > 0.1 * n, np.bincount(cls)
+    if size > 0.1:
+        assert (cls == 2).sum() > 1000, np.bincount(cls)
