@@ -126,11 +126,155 @@ __device__ __forceinline__ void edge_pretest(const float *rr, float a, float b, 
     }
 }
 
+
+// Which of the reference walk's decisions on the way to this triangle's
+// leaf can go differently from the exact hit point's, for some ray the
+// intersector accepts?  The answer replaces the root-path check
+// (path_verify) with at most two comparisons carried in the list entry.
+//
+// The walk's decisions (path_step, root first) each compare two computed
+// plane parameters t_p = fl(val_p * fl(1 / D[a_p])), val_p the
+// camera-relative plane as the kernels hold it (f32): t_p = tau_p (1 + d),
+// |d| <= 2.0001e, tau_p = val_p / D[a_p] exact.  A plane is an entry (the ray
+// enters the child's region there) or an exit by the sign of D[a] -- that of
+// X[a] over the whole inflated triangle when min|X[a]| > 0 (X = P - O,
+// camera-relative hit point).  A node's entry plane is compared with the
+// current hi, which is the t of the last exit plane above it (nhi = t,
+// never a min) or the slab test's tMax; an exit plane with lo, the last
+// entry plane's t or tMin.
+//
+// The exact line meets the triangle's plane at X inside the inflated
+// triangle (corners X_j), at t* = X[a] / D[a] for every axis a.  Plane p
+// has signed gap g_p(X) = val - X[a] ("X[a] <= val" side) or X[a] - val, so
+// in t-units the separation minus rounding is (g_p - 2.0001e |val_p|) / |D[a]|
+// and, divided by t*, >= h_p(X) / |X[a]| with h_p = g_p - 4e |val_p| (linear
+// in X) >= L_p(X) = min(h_p / min|X[a]|, h_p / max|X[a]|) over the hull
+// (-inf when the hull reaches X[a] = 0 and h_p < 0).  A comparison of p and
+// k comes out as for the exact hit point (the child is visited) when
+// L_p(X) + L_k(X) > 0; L_p + L_k is concave (sums of minima of linear
+// functions), so it suffices at the three corners.  Against the slab test's
+// tMin / tMax the smallest L over the faces that can be entries / exits is
+// taken.  The leaf's parent plane is the triangle's own extreme coordinate
+// and pokes through by the inflation near one vertex; its partner is
+// usually far from that vertex.
+//
+// Plan (rec[11] = meta, rec[12..15] = vals, rec[10] bit 31 = no check):
+//   n = meta & 3: 0 = every decision proven, 1-2 = that many critical
+//   comparisons c, 3 = full root-path check (more than two, a plane of
+//   either kind, val = 0 where 0 * inf = NaN, or a path deeper than 64);
+//   comparison c: bits 2+6c: axis of k (2), k is an exit (1), axis of the
+//   partner p (2), p is the slab's tMin / tMax (1); vals: val_k, val_p.
+//   The kernel evaluates g = t_k > t_p (k exit) or !(t_k > t_p) (k entry),
+//   as path_step does.
+struct PlanL {
+    double L[3];
+};
+__device__ __forceinline__ PlanL plane_l(const double (*X)[3], int ax, double val, bool le, double amin,
+                                         double amax) {
+    PlanL o;
+    const double r = 4.0 * 0x1p-24 * fabs(val);
+    for (int j = 0; j < 3; ++j) {
+        const double h = (le ? val - X[j][ax] : X[j][ax] - val) - r;
+        double m;
+        if (h >= 0.0) m = amax > 0.0 ? h / amax : INFINITY;
+        else m = amin > 0.0 ? h / amin : -INFINITY;
+        o.L[j] = (m == m) ? m : -INFINITY;
+    }
+    return o;
+}
+__device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const TreeHeader *hdr,
+                                  const float *o, const uint4 *node_prim, const int32_t *leaf_parent,
+                                  const int32_t *parent, float *vals) {
+    constexpr uint32_t kFull = 3u;
+    double amin[3], amax[3];
+    int sgn[3];
+    for (int ax = 0; ax < 3; ++ax) {
+        const double lo = fmin(fmin(X[0][ax], X[1][ax]), X[2][ax]);
+        const double hi = fmax(fmax(X[0][ax], X[1][ax]), X[2][ax]);
+        amin[ax] = lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0);
+        amax[ax] = fmax(fabs(lo), fabs(hi));
+        sgn[ax] = lo > 0.0 ? 1 : (hi < 0.0 ? -1 : 0);
+    }
+    // slab faces: the smallest L over the faces that can be entries / exits
+    PlanL slabE, slabX;
+    for (int j = 0; j < 3; ++j) slabE.L[j] = slabX.L[j] = INFINITY;
+    for (int ax = 0; ax < 3; ++ax)
+        for (int f = 0; f < 2; ++f) {
+            const bool le = f == 1;   // hi face: region X[a] <= hi - O
+            const float v = le ? hdr->scene_hi[ax] - o[ax] : hdr->scene_lo[ax] - o[ax];
+            if (v == 0.0f || !(v == v)) return kFull;
+            const PlanL l = plane_l(X, ax, (double)v, le, amin[ax], amax[ax]);
+            const bool can_exit = sgn[ax] == 0 || (le == (sgn[ax] > 0));
+            const bool can_entry = sgn[ax] == 0 || !(le == (sgn[ax] > 0));
+            for (int j = 0; j < 3; ++j) {
+                if (can_entry) slabE.L[j] = fmin(slabE.L[j], l.L[j]);
+                if (can_exit) slabX.L[j] = fmin(slabX.L[j], l.L[j]);
+            }
+        }
+    // the root path, leaf first
+    float pv[64];
+    uint8_t pa[64];
+    bool pl[64];
+    int n = 0;
+    {
+        uint32_t cidx = leaf;
+        bool cleaf = true;
+        for (int32_t p = leaf_parent[leaf]; p >= 0; p = parent[p]) {
+            if (n == 64) return kFull;
+            const uint4 r = node_prim[p];
+            const uint32_t split = r.z >> 8, ax = r.z & 0xffu;
+            if (ax > 2u) return kFull;
+            const bool leafL = (r.w >> 26) & 1u;
+            const bool left = cidx == split && cleaf == leafL;
+            pv[n] = __uint_as_float(left ? r.x : r.y);
+            pa[n] = (uint8_t)ax;
+            pl[n] = left;
+            ++n;
+            cidx = (uint32_t)p;
+            cleaf = false;
+        }
+    }
+    // root first: each plane against the last plane of the other kind
+    PlanL lastE = slabE, lastX = slabX;
+    int lastEi = -1, lastXi = -1;             // -1: the slab endpoint
+    uint32_t meta = 0, nc = 0;
+    for (int i = n - 1; i >= 0; --i) {
+        const int ax = pa[i];
+        if (sgn[ax] == 0 || pv[i] == 0.0f || !(pv[i] == pv[i])) return kFull;
+        const bool le = pl[i];
+        const bool is_exit = le == (sgn[ax] > 0);
+        const PlanL l = plane_l(X, ax, (double)pv[i], le, amin[ax], amax[ax]);
+        const PlanL &q = is_exit ? lastE : lastX;
+        const int qi = is_exit ? lastEi : lastXi;
+        bool ok = true;
+        for (int j = 0; j < 3; ++j) ok = ok && (l.L[j] + q.L[j] > 0.0);
+        if (!ok) {
+            if (nc == 2) return kFull;
+            meta |= ((uint32_t)ax | (is_exit ? 4u : 0u) | ((qi >= 0 ? (uint32_t)pa[qi] : 0u) << 3) |
+                     (qi < 0 ? 32u : 0u)) << (2 + 6 * nc);
+            vals[2 * nc] = pv[i];
+            vals[2 * nc + 1] = qi >= 0 ? pv[qi] : 0.0f;
+            ++nc;
+        }
+        if (is_exit) {
+            lastX = l;
+            lastXi = i;
+        } else {
+            lastE = l;
+            lastEi = i;
+        }
+    }
+    return meta | nc;
+}
+
 // Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
 // by0 | by1 << 16; empty = bx0 > bx1), the pixel rectangle in r[14..15] and
 // its list entry binrec[i]; the global list takes the rest.
 __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, uint32_t n,
-                                                     BinCamera c, uint2 *__restrict__ brect,
+                                                     BinCamera c, const TreeHeader *__restrict__ hdr,
+                                                     const uint4 *__restrict__ node_prim,
+                                                     const int32_t *__restrict__ leaf_parent,
+                                                     const int32_t *__restrict__ parent, uint2 *__restrict__ brect,
                                                      float *__restrict__ binrec,
                                                      uint32_t *__restrict__ gcount,
                                                      uint32_t *__restrict__ glist) {
@@ -150,11 +294,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
     float a, b, cc;
     const bool ok = miss_bary(rr, c.dmax, a, b, cc);
     int side = 0;                      // 1: all in front, -1: all behind, 0: neither / no bound
+    uint32_t plan = 3u;                // triangle_plan: 3 = full root-path check
+    float plan_vals[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
     if (ok) {
         // corners of the inflated triangle: depth and image (u, v)
         int front = 0, back = 0;
         double max_depth = 0.0;
+        double cx[3][3];               // corners X_j (camera-relative)
         auto corners = [&](float a_, float b_, float c_) {
             const double cu[3] = {-(double)a_, 1.0 + (double)b_ + (double)c_, -(double)a_};
             const double cv[3] = {-(double)b_, -(double)b_, 1.0 + (double)a_ + (double)c_};
@@ -163,7 +310,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
             umin = vmin = INFINITY;
             umax = vmax = -INFINITY;
             for (int j = 0; j < 3; ++j) {
-                double X[3];
+                double *X = cx[j];
                 for (int ax = 0; ax < 3; ++ax)
                     X[ax] = (cu[j] * (double)rr[ax] + cv[j] * (double)rr[3 + ax]) - (double)rr[6 + ax];
                 const double depth = dot3(X, c.n);
@@ -204,6 +351,8 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
         }
         if (front == 3) {
             side = 1;
+            plan = triangle_plan(cx, __float_as_uint(r[13]), hdr, c.o, node_prim, leaf_parent, parent,
+                                 plan_vals);
         } else if (back == 3) {
             // exact t* = tnum* / det* with det* > 0 (miss_bary's den); tnum_c
             // errs by at most 5e |e2|.Q (q_c = cross(s, e1): 2e Q, the dot
@@ -238,8 +387,9 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
             }
         }
         rec[9] = __uint_as_float(i);
-        rec[10] = r[13];
-        for (int k = 11; k < 16; ++k) rec[k] = 0.0f;
+        rec[10] = __uint_as_float(__float_as_uint(r[13]) | (plan == 0u ? 0x80000000u : 0u));
+        rec[11] = __uint_as_float(plan);
+        for (int k = 0; k < 4; ++k) rec[12 + k] = plan_vals[k];
         float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
         for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
     }
@@ -443,6 +593,7 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
     }
     c.nlen = nl;
     c.an = an;
+    for (int k = 0; k < 3; ++k) c.o[k] = cam[k];
     // D.n = A.n exactly for D(u, v); the f32 D errs by delta per component
     c.dn_lb = an - 2.0 * (c.delta[0] * fabs(n[0]) + c.delta[1] * fabs(n[1]) + c.delta[2] * fabs(n[2]));
     c.ahu = dot(A, c.hu);
@@ -455,7 +606,8 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
     return true;
 }
 
-int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const int32_t *first_idx,
+                          const uint32_t *dup_cnt,
                           const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
@@ -471,7 +623,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, con
     }
     if (n > 0) {
         const dim3 g((n + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, b.brect, b.binrec, b.gcount,
+        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, leaf_parent,
+                           parent, b.brect, b.binrec, b.gcount,
                            b.glist);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt);

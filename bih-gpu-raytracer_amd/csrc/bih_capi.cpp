@@ -565,7 +565,7 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.path = reinterpret_cast<uint2 *>(p); p += s_path;
     float *gent = reinterpret_cast<float *>(p);
     const uint4 *node_prim = reinterpret_cast<const uint4 *>(tr->prim + 16ull * n);
-    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
+    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.hdr, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
                                         tr->t.parent, node_prim, U, bc, b, st);
     if (le) return map_hip(le);
     uint32_t tot[2] = {0, 0};
@@ -853,8 +853,9 @@ int bih_sync(const bih_tree *tr, void *stream) {
             const unsigned long long *cb = reinterpret_cast<const unsigned long long *>(c + 48);
             fprintf(stderr,
                     "bin-counters packets %u lanes %u entries %u mt %u found %u verified %u"
-                    " unverified %u packets-with-miss %u | cycles walk %llu verify %llu\n",
-                    c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], cb[0], cb[1]);
+                    " unverified %u packets-with-miss %u planned %u plan-disagrees %u"
+                    " | cycles walk %llu verify %llu\n",
+                    c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], c[39], c[38], cb[0], cb[1]);
         }
     }
 #endif

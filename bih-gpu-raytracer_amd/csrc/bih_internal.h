@@ -104,6 +104,7 @@ struct BinCamera {
     double nlen, an, ahu, avv;
     double dn_lb;                             // <= D.n of every f32 primary ray (det_lower_bound)
     float dmax[3];
+    float o[3];                               // origin (f32, as the kernels hold it)
     uint32_t w, h, tw, th;
 };
 // Device buffers of the frustum bins.
@@ -186,7 +187,8 @@ bool render_uses_prim(uint32_t spp);
 // records; writes their words 13-15), then the lists
 bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
                 uint32_t th, BinCamera *out);
-int launch_bin_footprints(float *prim, uint32_t n, const int32_t *first_idx, const uint32_t *dup_cnt,
+int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const int32_t *first_idx,
+                          const uint32_t *dup_cnt,
                           const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
 // lists of 64-byte entries (list: per-tile, gent: the global list's)

@@ -1673,8 +1673,9 @@ __device__ __forceinline__ void bin_chunk_load(const float4 *ents, uint32_t e, u
 __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, const cprim_t *prims,
                                                       uint32_t bin, float uf, float vf, float dx,
                                                       float dy, float dz, unsigned long long live,
-                                                      uint32_t lane, uint32_t &cand,
-                                                      uint32_t &fc_ent, uint32_t &fc_mt) {
+                                                      uint32_t lane, uint32_t &cand, uint32_t &cmeta,
+                                                      uint32_t &cent, uint32_t &fc_ent,
+                                                      uint32_t &fc_mt) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
     const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
@@ -1706,7 +1707,11 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 BIH_FC(++fc_mt);
                 const sf32x16 r = prim_rec(prims, __builtin_amdgcn_readlane(__float_as_uint(d2.y), j));
                 const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
-                if (h & me) cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
+                if (h & me) {
+                    cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
+                    cmeta = __builtin_amdgcn_readlane(__float_as_uint(d2.w), j);
+                    cent = ((uint32_t)part << 31) | (e + j);
+                }
                 rem &= ~h;
             }
             if (n <= BIH_BIN_PREFETCH_AT && e + 64u < end)   // (cannot happen: n < 64 is the last chunk)
@@ -1784,6 +1789,33 @@ __device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint
             return ok;
     }
     return false;
+}
+
+// The candidate's verification plan (triangle_plan, bih_bins.hip): the
+// entry's leaf carries bit 31 when every decision on its root path is
+// proven; otherwise meta & 3 = 1-2 critical comparisons, each t_k against
+// t_p (another plane on the path, or the slab test's tMin / tMax), whose
+// operands sit in the entry's last 16 bytes; 3 = the full root-path check.
+__device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, uint32_t meta,
+                                            uint32_t cent, float ix, float iy, float iz, float tMin,
+                                            float tMax) {
+    if (cand >> 31) return true;
+    const uint32_t n = meta & 3u;
+    if (n == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
+    const float4 *base = reinterpret_cast<const float4 *>((cent >> 31) ? a.bin_glist : a.bin_list);
+    const float4 v = base[4ull * (cent & 0x7fffffffu) + 3];
+    bool ok = true;
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) {
+        if (c >= n) break;
+        const uint32_t m = meta >> (2 + 6 * c);
+        const float vk = c ? v.z : v.x, vp = c ? v.w : v.y;
+        const float tk = vk * sel3(m & 3u, ix, iy, iz);
+        const bool is_exit = (m & 4u) != 0u;
+        const float tp = (m & 32u) ? (is_exit ? tMin : tMax) : vp * sel3((m >> 3) & 3u, ix, iy, iz);
+        ok = ok && (is_exit ? (tk > tp) : !(tk > tp));
+    }
+    return ok;
 }
 
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
@@ -1882,17 +1914,33 @@ k_render_packet_asm(const RenderArgs a) {
             // misses for the lanes without one; a candidate the reference's
             // walk provably reaches (fast_verify) is a hit.  Only lanes with
             // an unverified candidate go on to the passes below.
-            uint32_t cand = 0, fc_ent = 0, fc_mt = 0;
+            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0;
             (void)fc_ent, (void)fc_mt;
             BIH_FC(const uint64_t fb0 = __builtin_amdgcn_s_memtime());
-            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx,
-                                                      dy, dz, live, lane, cand, fc_ent, fc_mt);
+            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane,
+                                                      cand, cmeta, cent, fc_ent, fc_mt);
             BIH_FC(const uint64_t fb1 = __builtin_amdgcn_s_memtime());
 #if BIH_NO_VERIFY   // timing experiments only (takes every candidate as verified)
             const bool ok = ((found >> lane) & 1ull);
 #else
+            // entries of triangles whose every accepted ray the reference's
+            // walk provably reaches (triangle_robust, bih_bins.hip) carry bit
+            // 31 on the leaf: no root-path check
             const bool ok = ((found >> lane) & 1ull) &&
-                            path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
+                            plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax);
+#endif
+#if BIH_FAST_COUNTERS
+            {   // candidates decided by a plan (no root-path walk) and those
+                // whose plan disagrees with the root-path check (must stay 0)
+                const bool fnd = ((found >> lane) & 1ull) != 0ull;
+                const bool planned = fnd && ((cand >> 31) || (cmeta & 3u) != 3u);
+                const bool pv = fnd && path_verify(a.bin_path, cand & 0x7fffffffu, ix, iy, iz, tMin, tMax);
+                const unsigned long long rb = __ballot(planned), bad = __ballot(planned && (pv != ok));
+                if (lane == 0) {
+                    atomicAdd(a.work + 38, (uint32_t)__popcll(bad));
+                    atomicAdd(a.work + 39, (uint32_t)__popcll(rb));
+                }
+            }
 #endif
             const unsigned long long ver = __ballot(ok);
 #if BIH_FAST_COUNTERS
