@@ -52,6 +52,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "bih_internal.h"
 #include "bih_bound.h"
@@ -542,6 +543,68 @@ __global__ void __launch_bounds__(kThreads) k_bin_paths(const uint4 *__restrict_
     out[depth] = make_uint2(0u, 8u);
 }
 
+
+// Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of
+// its rows, bih_rows), in kRegions bands of tile rows, one per XCD (the
+// render kernel's waves on XCD x draw from band x first, then from the
+// others): per band the tiles with a non-empty list, by descending list
+// length in power-of-two classes (longest processing time first), then the
+// tiles no triangle touches (background).  Built once per camera, image and
+// row set (bih_render.hip draws from it).
+constexpr uint32_t kQBands = 8, kQClasses = 34;   // classes 0..32: clz(length); 33: background
+__device__ __forceinline__ uint32_t queue_bin(uint32_t t, uint32_t tiles_x, uint32_t row0,
+                                              uint32_t band_h, uint32_t band_step, uint32_t th,
+                                              uint32_t bins_x) {
+    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+    const uint32_t lr = ty * th;
+    const uint32_t gy = row0 + (lr / band_h) * band_h * band_step + (lr % band_h);
+    return (gy / th) * bins_x + tx;
+}
+// qw: [0, 272) class counts, [288, 560) class starts, [576, 848) fill
+// cursors, [896, 928) per band {start, live, background, items}
+__global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__restrict__ off, uint32_t gn,
+                                                          uint32_t ntiles, uint32_t tiles_x,
+                                                          uint32_t tiles_y, uint32_t row0,
+                                                          uint32_t band_h, uint32_t band_step,
+                                                          uint32_t th, uint32_t bins_x, uint32_t lpt,
+                                                          uint16_t *__restrict__ cls,
+                                                          uint32_t *__restrict__ qw) {
+    const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint32_t b = queue_bin(t, tiles_x, row0, band_h, band_step, th, bins_x);
+    const uint32_t len = off[b + 1] - off[b] + gn;
+    const uint32_t band = (uint32_t)(((uint64_t)(t / tiles_x) * kQBands) / tiles_y);
+    const uint32_t k = band * kQClasses + (len ? (lpt ? (uint32_t)__clz(len) : 0u) : kQClasses - 1);
+    cls[t] = (uint16_t)k;
+    atomicAdd(qw + k, 1u);
+}
+__global__ void k_queue_scan(uint32_t *__restrict__ qw) {
+    if (threadIdx.x != 0) return;
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b < kQBands; ++b) {
+        const uint32_t start = acc;
+        for (uint32_t k = 0; k < kQClasses; ++k) {
+            qw[288 + b * kQClasses + k] = acc;
+            qw[576 + b * kQClasses + k] = 0;
+            acc += qw[b * kQClasses + k];
+        }
+        const uint32_t bg = qw[b * kQClasses + kQClasses - 1];
+        const uint32_t live = acc - start - bg;
+        qw[896 + 4 * b] = start;
+        qw[896 + 4 * b + 1] = live;
+        qw[896 + 4 * b + 2] = bg;
+        qw[896 + 4 * b + 3] = live + (bg + 63u) / 64u;
+    }
+}
+__global__ void __launch_bounds__(kThreads) k_queue_fill(const uint16_t *__restrict__ cls, uint32_t ntiles,
+                                                         uint32_t *__restrict__ qw,
+                                                         uint32_t *__restrict__ queue) {
+    const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint32_t k = cls[t];
+    queue[qw[288 + k] + atomicAdd(qw + 576 + k, 1u)] = t;
+}
+
 }  // namespace
 
 bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
@@ -650,6 +713,37 @@ int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBu
         hipLaunchKernelGGL(k_bin_gfill, dim3((gcount + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                            b.gcount, b.glist, reinterpret_cast<const float4 *>(b.binrec),
                            reinterpret_cast<float4 *>(gent));
+    return (int)hipGetLastError();
+}
+
+size_t bin_queue_bytes(uint32_t ntiles) { return ((size_t)ntiles * 6 + 1024 * 4 + 255) & ~(size_t)255; }
+
+int launch_bin_queue(const uint32_t *off, uint32_t gn, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
+                     uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
+                     uint32_t **queue, uint32_t **qhdr, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    uint32_t *qw = reinterpret_cast<uint32_t *>(mem);
+    uint32_t *q = qw + 1024;
+    uint16_t *cls = reinterpret_cast<uint16_t *>(q + ntiles);
+    *queue = q;
+    *qhdr = qw + 896;
+    hipError_t e = hipMemsetAsync(qw, 0, 1024 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    const uint32_t tiles_y = tiles_x ? (ntiles + tiles_x - 1) / tiles_x : 0;
+    // BIH_QUEUE_LPT=0: live tiles in tile order (A/B)
+    static const uint32_t lpt = [] {
+        const char *v = getenv("BIH_QUEUE_LPT");
+        return (v && v[0] == '0') ? 0u : 1u;
+    }();
+    if (ntiles > 0) {
+        const dim3 g((ntiles + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_queue_class, g, dim3(kThreads), 0, st, off, gn, ntiles, tiles_x, tiles_y, row0,
+                           band_h, band_step, th, bins_x, lpt, cls, qw);
+    }
+    hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(64), 0, st, qw);
+    if (ntiles > 0)
+        hipLaunchKernelGGL(k_queue_fill, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0, st, cls,
+                           ntiles, qw, q);
     return (int)hipGetLastError();
 }
 

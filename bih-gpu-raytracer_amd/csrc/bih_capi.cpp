@@ -81,6 +81,20 @@ struct bih_tree {
     uint32_t bins_key[3] = {0, 0, 0};
     float *bin_gent = nullptr;       // global list entries (in bins_mem)
     uint32_t bin_gn = 0;             // global list length
+    uint32_t bins_gen = 0;           // incremented by every bins build
+    // the render kernel's tile queue over one launch's rows (launch_bin_queue),
+    // for q_key = {w, h, spp, row0, nrows, band_h, band_step, bins_gen}
+    char *q_mem = nullptr;
+    size_t q_cap = 0;
+    bool q_valid = false;
+    uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t *q_list = nullptr, *q_hdr = nullptr;
+    // per render slot two sets of 8 band heads (32 words apart): a launch
+    // draws from set q_par[slot] and zeroes the other for the slot's next launch
+    uint32_t *q_count = nullptr;
+    uint32_t q_par[kSlots] = {};
+    uint32_t *fb_mem = nullptr;      // per slot: fallback records of k_render_bins (8 words per tile)
+    size_t fbq_cap = 0;              // tiles per slot
 };
 
 namespace {
@@ -367,6 +381,9 @@ void bih_free(bih_tree *tr) {
     if (tr->prim) (void)hipFree(tr->prim);
     if (tr->bins_mem) (void)hipFree(tr->bins_mem);
     if (tr->bin_list) (void)hipFree(tr->bin_list);
+    if (tr->q_mem) (void)hipFree(tr->q_mem);
+    if (tr->q_count) (void)hipFree(tr->q_count);
+    if (tr->fb_mem) (void)hipFree(tr->fb_mem);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
         if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
@@ -522,6 +539,7 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
                       uint32_t h, uint32_t spp, hipStream_t st) {
     tr->bins_valid = true;
     tr->bins_usable = false;
+    ++tr->bins_gen;
     tr->bins_key[0] = w;
     tr->bins_key[1] = h;
     tr->bins_key[2] = spp;
@@ -591,6 +609,65 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     tr->bin_gent = gent;
     tr->bin_gn = tot[1];
     tr->bins_usable = true;
+    return BIH_OK;
+}
+
+// The render kernel's tile queue for this launch's rows (launch_bin_queue):
+// rebuilt when the bins or the rows change, after every render that may
+// still read the old one.
+static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_rows &rows,
+                             int slot, hipStream_t st, bih::RenderArgs &a) {
+    uint32_t tw = 0, th = 0;
+    tile_shape(spp, &tw, &th);
+    const uint32_t tiles_x = (w + tw - 1) / tw;
+    const uint32_t ntiles = tiles_x * ((rows.nrows + th - 1) / th);
+    const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, tr->bins_gen};
+    if (!tr->q_count) {
+        hipError_t e = hipMalloc((void **)&tr->q_count, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemset(tr->q_count, 0, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    if (!tr->q_valid || memcmp(key, tr->q_key, sizeof key) != 0) {
+        int rc = wait_renders(tr, st);
+        if (rc) return rc;
+        const size_t need = bih::bin_queue_bytes(ntiles);
+        if (tr->q_cap < need) {
+            for (int k = 0; k < kSlots; ++k)
+                if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+            if (tr->q_mem) (void)hipFree(tr->q_mem);
+            tr->q_mem = nullptr;
+            tr->q_cap = 0;
+            tr->q_valid = false;
+            hipError_t e = hipMalloc((void **)&tr->q_mem, need);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->q_cap = need;
+        }
+        int le = bih::launch_bin_queue(tr->bins.off, tr->bin_gn, tr->bins.bins_x, tiles_x, ntiles, rows.row0,
+                                       rows.band_h, rows.band_step, th, tr->q_mem, &tr->q_list, &tr->q_hdr,
+                                       st);
+        if (le) return map_hip(le);
+        memcpy(tr->q_key, key, sizeof key);
+        tr->q_valid = true;
+    }
+    if (tr->fbq_cap < ntiles) {
+        for (int k = 0; k < kSlots; ++k)
+            if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+        if (tr->fb_mem) (void)hipFree(tr->fb_mem);
+        tr->fb_mem = nullptr;
+        tr->fbq_cap = 0;
+        hipError_t e = hipMalloc((void **)&tr->fb_mem, (size_t)kSlots * ntiles * 8 * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->fbq_cap = ntiles;
+    }
+    a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
+    a.bin_queue = tr->q_list;
+    a.bin_qhdr = tr->q_hdr;
+    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d);
+    const uint32_t par = tr->q_par[slot];
+    a.bin_heads = tr->q_count + (size_t)(2 * slot + par) * bih::kBinSetWords;
+    a.bin_heads_next = tr->q_count + (size_t)(2 * slot + (par ^ 1u)) * bih::kBinSetWords;
+    tr->q_par[slot] = par ^ 1u;
     return BIH_OK;
 }
 
@@ -699,11 +776,6 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             if (rc) return rc;
         }
     }
-    // the next render (on any stream) orders after the advance above and after
-    // the per-camera records, which it reads as they stand now
-    e = hipEventRecord(tr->ev_rng, st);
-    if (e != hipSuccess) return map_hip((int)e);
-    tr->rng_pending = true;
     bih::RenderArgs a;
     bool use_bins = false;
     if (tr->bins_usable && tr->bins_valid && tr->bins_key[0] == w && tr->bins_key[1] == h &&
@@ -721,12 +793,19 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         a.bin_path = tr->bins.path;
         a.bins_x = tr->bins.bins_x;
         a.bin_gn = tr->bin_gn;
+        rc = prepare_bin_queue(tr, w, h, spp, rows, slot, st, a);
+        if (rc) return rc;
     } else {
         // the cost order pays off for the long BIH walks; with the bins the
         // packets are short and the order's own launch costs more (A/B)
         rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
         if (rc) return rc;
     }
+    // the next render (on any stream) orders after the advance above, the
+    // per-camera records and the tile queue, which it reads as they stand now
+    e = hipEventRecord(tr->ev_rng, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_pending = true;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;

@@ -41,6 +41,7 @@ constexpr int kLdsStack = BIH_LDS_STACK;
 constexpr uint32_t kSlotStrideWords = 32;
 constexpr uint32_t kWorkWords = 64 + kSlotStrideWords * 1024 + 64;   // + histograms (counter builds)
 constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
+constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue state per set
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif
@@ -93,6 +94,15 @@ struct RenderArgs {
     const uint2 *bin_path = nullptr;        // [U][32] root path steps per leaf
     uint32_t bins_x = 0;
     uint32_t bin_gn = 0;                    // == *bin_gcount (host copy)
+    // the launch's tile queue (launch_bin_queue) and this render slot's queue
+    // state (kBinSetWords, zero at launch: band heads, fallback count, per-CU
+    // slots), plus the other set, which this launch zeroes for the slot's next one
+    const uint32_t *bin_queue = nullptr;
+    const uint32_t *bin_qhdr = nullptr;
+    uint32_t *bin_heads = nullptr;
+    uint32_t *bin_heads_next = nullptr;
+    uint32_t *bin_fb = nullptr;             // fallback records of the slot (k_render_bins), 8 words each
+    uint32_t dbg = 0;                       // timing experiments only (BIH_DBG): 1 skip background, 2 skip live
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
@@ -194,6 +204,14 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
 // lists of 64-byte entries (list: per-tile, gent: the global list's)
 int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBuffers &b, float *list,
                     float *gent, void *stream);
+// the render kernel's work queue over one launch's tiles (k_queue_*), in 8
+// bands of tile rows: per band the live tiles by descending list length,
+// then the background tiles; qhdr (device) = per band {start, live,
+// background, items}.  mem: bin_queue_bytes(ntiles)
+size_t bin_queue_bytes(uint32_t ntiles);
+int launch_bin_queue(const uint32_t *off, uint32_t gn, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
+                     uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
+                     uint32_t **queue, uint32_t **qhdr, void *stream);
 // exclusive scan of n u32 (bih_build.hip); *total_dev = the sum
 int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                    uint32_t *total_dev, void *stream);

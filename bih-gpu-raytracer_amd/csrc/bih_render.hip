@@ -1818,6 +1818,235 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
     return ok;
 }
 
+// ---------------------------------------------------------------------------
+// k_render_bins: the any-hit render through the frustum bins alone (no BIH
+// walk in this kernel).  Persistent waves draw items from the launch's tile
+// queue (launch_bin_queue, bih_bins.hip): a wave starts in its XCD's band of
+// tile rows and moves on to the others when that band is drained.  An item is
+// a live tile -- one 64-ray packet: jitter, camera ray, scene slab test,
+// bin_walk over the tile's list, plan_verify of each lane's candidate -- or
+// 64 background tiles (one per lane), which no triangle's footprint touches.
+// A packet whose lanes all end as a verified hit or a proven miss writes its
+// pixels; a packet with a lane left undecided (a candidate the plan or the
+// root-path check rejects, or a single-leaf scene) appends {tile, undecided,
+// hits} to the slot's fallback list, and k_render_fallback finishes it with
+// the exact walk.  Registers stay those of the list walk (no BIH walk state).
+// Queue state (a "head set", kBinSetWords, zero at launch; the launch zeroes
+// the slot's other set for its next launch): 8 band heads and the fallback
+// count, then per-CU slots like TileQueue's -- a wave claims a position of
+// its CU's current batch of kBinBatch consecutive items with one atomicAdd
+// on the CU's own 128-byte line, and the wave that drains a batch refills
+// the slot from a band head.  One device-wide atomic per batch instead of
+// one per item: a single head word saturates near 90 dequeues per us.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hits lo/hi, pad
+constexpr uint32_t kBinBatch = 16;
+constexpr uint32_t kBinSlot0 = 16 * 32;   // words: heads at b * 32, fallback count at 8 * 32
+struct BinQueue {
+    const uint4 *hdr;                  // per band {start, live, bg, items}
+    uint32_t *set;
+    unsigned long long *slot;
+    uint32_t band, left;
+    uint4 hb;                          // header of the band of the item next() returned
+
+    // next item: band (this->hb / band) and index within the band
+    __device__ bool next(uint32_t lane, uint32_t &item) {
+        for (;;) {
+            unsigned long long v = 0;
+            if (lane == 0) v = atomicAdd(slot, 1ull);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+            if (hi == 0xFFFFFFFFu) return false;
+            if (hi != 0 && lo < kBinBatch) {
+                const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch;
+                hb = hdr[b];
+                if (start + lo < hb.w) {
+                    item = start + lo;
+                    band = b;
+                    return true;
+                }
+                continue;                                // past the band's end
+            }
+            if ((hi == 0 && lo == 0) || (hi != 0 && lo == kBinBatch)) {
+                while (left) {
+                    const uint4 h = hdr[band];
+                    uint32_t c = 0;
+                    if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
+                    c = __builtin_amdgcn_readfirstlane(c);
+                    if (c < h.w) {
+                        if (lane == 0)
+                            atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
+                        hb = h;
+                        item = c;
+                        return true;
+                    }
+                    band = (band + 1u) & 7u;
+                    --left;
+                }
+                if (lane == 0) atomicExch(slot, kSlotDone);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(2);                 // another wave is refilling
+        }
+    }
+};
+template <int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_bins(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    // the slot's next launch starts from a zeroed set
+    if (tid == 0 && blockIdx.x < 1024u)
+        *reinterpret_cast<unsigned long long *>(a.bin_heads_next + kBinSlot0 + blockIdx.x * 32) = 0ull;
+    if (tid == 0 && blockIdx.x < 9u) a.bin_heads_next[blockIdx.x * 32] = 0u;
+    const SceneU sc = load_scene(a);
+    const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+    const uint32_t bgpix = pixel_from_hits(0u, SPP);
+    BinQueue q;
+    q.hdr = reinterpret_cast<const uint4 *>(a.bin_qhdr);
+    q.set = a.bin_heads;
+    q.slot = reinterpret_cast<unsigned long long *>(a.bin_heads + kBinSlot0 + cu_key() * 32);
+    q.band = xcc_id();
+    q.left = 8;
+    uint32_t it = 0;
+    while (q.next(lane, it)) {
+        const uint4 hb = q.hb;
+        if (it >= hb.y) {
+            // background: every sample misses (Color's background), whatever its jitter
+            const uint32_t k = (it - hb.y) * 64u + lane;
+            if (k < hb.z && !(a.dbg & 1u)) {
+                const uint32_t t = a.bin_queue[hb.x + hb.y + k];
+                const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+                const uint32_t x0 = tx * TW;
+                for (uint32_t r = 0; r < TH; ++r) {
+                    const uint32_t lr = ty * TH + r;
+                    if (lr >= a.nrows) break;
+                    uint32_t *o = a.out + (uint64_t)lr * a.w + x0;
+                    if (TW == 4 && x0 + 4 <= a.w && ((uintptr_t)o & 15u) == 0) {
+                        *reinterpret_cast<uint4 *>(o) = make_uint4(bgpix, bgpix, bgpix, bgpix);
+                    } else {
+                        for (uint32_t c = 0; c < TW && x0 + c < a.w; ++c) o[c] = bgpix;
+                    }
+                }
+            }
+            continue;
+        }
+        if (a.dbg & 2u) continue;
+        const uint32_t tile = a.bin_queue[hb.x + it];
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+        const uint32_t bin = (global_row(ty * TH, a.row0, a.band_h, a.band_step) / TH) * a.bins_x + tx;
+        float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
+        if (valid) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            uf = ((float)x + ru) / fw;       // CUDAKernels.cu:414-415
+            vf = ((float)y + rv) / fh;
+            camera_dir(a, uf, vf, dx, dy, dz);
+        }
+        // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
+        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+        const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+        float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+        const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+        const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+        bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
+        if (tymin > tMin) tMin = tymin;
+        if (tymax < tMax) tMax = tymax;
+        const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+        const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+        in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+        if (tzmin > tMin) tMin = tzmin;
+        if (tzmax < tMax) tMax = tzmax;
+        const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+        unsigned long long hits = 0ull, undecided = 0ull;
+        if (live && sc.U > 1) {
+            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0;
+            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
+                                                      cmeta, cent, fc_ent, fc_mt);
+            const bool ok = ((found >> lane) & 1ull) && plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax);
+            hits = __ballot(ok);
+            undecided = live & found & ~hits;
+        } else if (live) {
+            undecided = live;              // one leaf (U == 1): the exact walk decides
+        }
+        if (undecided) {
+            uint32_t r = 0;
+            if (lane == 0) r = atomicAdd(a.bin_heads + 8 * 32, 1u);
+            r = __builtin_amdgcn_readfirstlane(r);
+            if (lane < 5) {
+                const uint32_t v[5] = {tile, (uint32_t)undecided, (uint32_t)(undecided >> 32), (uint32_t)hits,
+                                       (uint32_t)(hits >> 32)};
+                a.bin_fb[(uint64_t)r * kFbWords + lane] = v[lane];
+            }
+            continue;
+        }
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+        }
+    }
+}
+
+// The packets k_render_bins left undecided: the undecided lanes take the
+// exact any-hit walk (Walker: TraverseTree as the reference runs it, per
+// lane, LDS stack), then the tile's pixels are written.  Launched after every
+// k_render_bins on the same stream; with no fallback record it only reads
+// the count.
+template <int LOG2SPP>
+__global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a) {
+    constexpr uint32_t SPP = 1u << LOG2SPP;
+    constexpr uint32_t TW = TileShape<LOG2SPP>::TW;
+    __shared__ uint32_t s_node[kLdsStack * kThreads];
+    __shared__ float s_min[kLdsStack * kThreads];
+    __shared__ float s_max[kLdsStack * kThreads];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t n = *(volatile const uint32_t *)(a.bin_heads + 8 * 32);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (kThreads / 64) + (tid >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kThreads / 64);
+    if (gwave >= n) return;
+    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
+                      (uint64_t)blockIdx.x * kThreads + tid};
+    const SceneU sc = load_scene(a);
+    const uint32_t tiles_x = (a.w + TW - 1) / TW;
+    const float fw = (float)a.w, fh = (float)a.h;
+    const uint32_t pix = lane >> LOG2SPP;
+    for (uint64_t r = gwave; r < n; r += nwaves) {
+        const uint32_t *rec = a.bin_fb + r * kFbWords;
+        const uint32_t tile = rec[0];
+        const unsigned long long und = ((unsigned long long)rec[2] << 32) | rec[1];
+        unsigned long long hits = ((unsigned long long)rec[4] << 32) | rec[3];
+        uint32_t x, lr, s;
+        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
+        const bool valid = x < a.w && lr < a.nrows;
+        const uint64_t lp = (uint64_t)lr * a.w + x;
+        const bool mine = valid && ((und >> lane) & 1ull);
+        float dx = 0.f, dy = 0.f, dz = 1.f;
+        if (mine) {
+            float ru = 0.f, rv = 0.f;
+            ray_jitter<SPP>(a, lp, s, ru, rv);
+            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+            camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
+        }
+        Walker<true, false> w;
+        w.start(sc, mine, dx, dy, dz);
+        while (w.alive) w.step(sc, st);
+        hits |= __ballot(mine && w.hit);
+        if (valid && s == SPP - 1) {
+            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+        }
+    }
+}
+
 // k_render_packet_asm: k_render_packet2 with the walk as one hand-scheduled
 // loop (bih_packet_asm.h); ray setup and writeback stay in HIP.  Triangle
 // offsets are 32-bit in the loop: used for scenes of < 2^26 triangles.
@@ -2706,12 +2935,57 @@ int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks
     return (int)hipGetLastError();
 }
 
+// Resident blocks of k_render_bins on `device` (its own occupancy: the list
+// walk needs fewer registers than the BIH walks).
+uint32_t bins_grid_blocks(int device) {
+    static std::mutex mu;
+    static uint32_t cache[64] = {0};
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0 || device >= 64) return 0;
+    if (!cache[device]) {
+        int cus = 0, per = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void *>(k_render_bins<2>), kThreads, 0);
+        if (cus <= 0) cus = 256;
+        if (per <= 0) per = 1;
+        if (const char *e = getenv("BIH_BINS_BLOCKS_PER_CU")) {
+            const int v = atoi(e);
+            if (v > 0 && v <= 32) per = v;
+        }
+        cache[device] = (uint32_t)(cus * per);
+    }
+    return cache[device];
+}
+
+template <int L>
+static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t blocks, uint32_t fb_blocks) {
+    hipLaunchKernelGGL(k_render_bins<L>, dim3(blocks), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(k_render_fallback<L>, dim3(fb_blocks), dim3(kThreads), 0, st, a);
+    return hipGetLastError();
+}
+
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     const uint32_t spp = a.spp;
     int dev = 0;
     (void)hipGetDevice(&dev);
     const uint32_t grid = wave_grid_blocks(dev);
+    if (a.bin_queue && spp <= 64 && (spp & (spp - 1)) == 0) {
+        // frustum bins: the list-walk kernel, then the exact walk for what it
+        // left undecided (the fallback grid stays within the spill area)
+        const uint32_t fb = grid < 64u ? grid : 64u;
+        const uint32_t gb = bins_grid_blocks(dev);
+        switch (__builtin_ctz(spp)) {
+        case 0: return (int)launch_bins<0>(a, st, gb, fb);
+        case 1: return (int)launch_bins<1>(a, st, gb, fb);
+        case 2: return (int)launch_bins<2>(a, st, gb, fb);
+        case 3: return (int)launch_bins<3>(a, st, gb, fb);
+        case 4: return (int)launch_bins<4>(a, st, gb, fb);
+        case 5: return (int)launch_bins<5>(a, st, gb, fb);
+        default: return (int)launch_bins<6>(a, st, gb, fb);
+        }
+    }
     if (spp <= 64 && (spp & (spp - 1)) == 0) {
         static const Variant var = variant_from_env();
         const int L = __builtin_ctz(spp);
@@ -2721,11 +2995,9 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         if (tiles == 0) return 0;
         uint32_t blocks = (uint32_t)((tiles + 3) / 4);
         if (blocks > grid) blocks = grid;
-#if BIH_PACKET_COUNTERS
+        // the tile queue of the per-CU slots starts from zero; the bins' item
+        // queue resets itself (counter builds also count into a.work)
         hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
-#else
-        hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
-#endif
         if (e != hipSuccess) return (int)e;
         switch (L) {
         case 0: e = launch_persistent<0>(var, a, traverse, st, blocks); break;
