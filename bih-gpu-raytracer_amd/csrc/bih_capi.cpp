@@ -663,7 +663,10 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
     a.bin_queue = tr->q_list;
     a.bin_qhdr = tr->q_hdr;
-    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d);
+    // timing experiments (BIH_DBG bits 1-2) and the fallback test mode
+    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d) & 3u;
+    if (const char *d = getenv("BIH_BINS_FORCE_FALLBACK"))
+        if (d[0] == '1') a.dbg |= 4u;
     const uint32_t par = tr->q_par[slot];
     a.bin_heads = tr->q_count + (size_t)(2 * slot + par) * bih::kBinSetWords;
     a.bin_heads_next = tr->q_count + (size_t)(2 * slot + (par ^ 1u)) * bih::kBinSetWords;

@@ -1975,6 +1975,31 @@ __global__ void __launch_bounds__(kThreads) k_render_bins(const RenderArgs a) {
             const bool ok = ((found >> lane) & 1ull) && plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax);
             hits = __ballot(ok);
             undecided = live & found & ~hits;
+#if BIH_FAST_COUNTERS
+            {   // bin counters (bih_sync prints them): candidates decided by a
+                // plan, and plans that disagree with the root-path check (0)
+                const bool fnd = ((found >> lane) & 1ull) != 0ull;
+                const bool planned = fnd && ((cand >> 31) || (cmeta & 3u) != 3u);
+                const bool pv = fnd && path_verify(a.bin_path, cand & 0x7fffffffu, ix, iy, iz, tMin, tMax);
+                const unsigned long long rb = __ballot(planned), bad = __ballot(planned && (pv != ok));
+                if (lane == 0) {
+                    atomicAdd(a.work + 38, (uint32_t)__popcll(bad));
+                    atomicAdd(a.work + 39, (uint32_t)__popcll(rb));
+                    atomicAdd(a.work + 40, 1u);
+                    atomicAdd(a.work + 41, (uint32_t)__popcll(live));
+                    atomicAdd(a.work + 42, fc_ent);
+                    atomicAdd(a.work + 43, fc_mt);
+                    atomicAdd(a.work + 44, (uint32_t)__popcll(found));
+                    atomicAdd(a.work + 45, (uint32_t)__popcll(hits));
+                    atomicAdd(a.work + 46, (uint32_t)__popcll(undecided));
+                    atomicAdd(a.work + 47, found != live ? 1u : 0u);
+                }
+            }
+#endif
+            if (a.dbg & 4u) {              // tests: every live lane to the fallback
+                hits = 0ull;
+                undecided = live;
+            }
         } else if (live) {
             undecided = live;              // one leaf (U == 1): the exact walk decides
         }
@@ -2091,18 +2116,6 @@ k_render_packet_asm(const RenderArgs a) {
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
         const uint64_t lp = (uint64_t)lr * a.w + x;
-        uint32_t bin = 0;
-        if (BIH_BINS && ANYHIT && !STATS && a.bin_off) {
-            const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-            bin = (global_row(ty * TH, a.row0, a.band_h, a.band_step) / TH) * a.bins_x + tx;
-            const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
-            if (a.bin_gn == 0 && off[bin] == off[bin + 1]) {
-                // no triangle's footprint touches the tile: every sample is a
-                // proven miss (Color's background), whatever its jitter
-                if (valid && s == SPP - 1) a.out[lp] = pixel_from_hits(0u, SPP);
-                continue;
-            }
-        }
         float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
         if (valid) {
             float ru = 0.f, rv = 0.f;
@@ -2138,63 +2151,6 @@ k_render_packet_asm(const RenderArgs a) {
 #if BIH_FAST_COUNTERS
         uint64_t fc_walk0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (BIH_BINS && ANYHIT && !STATS && a.bin_off && live && sc.U > 1) {
-            // frustum bins: candidates from the tile's triangle list, proven
-            // misses for the lanes without one; a candidate the reference's
-            // walk provably reaches (fast_verify) is a hit.  Only lanes with
-            // an unverified candidate go on to the passes below.
-            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0;
-            (void)fc_ent, (void)fc_mt;
-            BIH_FC(const uint64_t fb0 = __builtin_amdgcn_s_memtime());
-            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane,
-                                                      cand, cmeta, cent, fc_ent, fc_mt);
-            BIH_FC(const uint64_t fb1 = __builtin_amdgcn_s_memtime());
-#if BIH_NO_VERIFY   // timing experiments only (takes every candidate as verified)
-            const bool ok = ((found >> lane) & 1ull);
-#else
-            // entries of triangles whose every accepted ray the reference's
-            // walk provably reaches (triangle_robust, bih_bins.hip) carry bit
-            // 31 on the leaf: no root-path check
-            const bool ok = ((found >> lane) & 1ull) &&
-                            plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax);
-#endif
-#if BIH_FAST_COUNTERS
-            {   // candidates decided by a plan (no root-path walk) and those
-                // whose plan disagrees with the root-path check (must stay 0)
-                const bool fnd = ((found >> lane) & 1ull) != 0ull;
-                const bool planned = fnd && ((cand >> 31) || (cmeta & 3u) != 3u);
-                const bool pv = fnd && path_verify(a.bin_path, cand & 0x7fffffffu, ix, iy, iz, tMin, tMax);
-                const unsigned long long rb = __ballot(planned), bad = __ballot(planned && (pv != ok));
-                if (lane == 0) {
-                    atomicAdd(a.work + 38, (uint32_t)__popcll(bad));
-                    atomicAdd(a.work + 39, (uint32_t)__popcll(rb));
-                }
-            }
-#endif
-            const unsigned long long ver = __ballot(ok);
-#if BIH_FAST_COUNTERS
-            const uint64_t fb2 = __builtin_amdgcn_s_memtime();
-            if (lane == 0) {
-                unsigned long long *cy = reinterpret_cast<unsigned long long *>(a.work + 48);
-                atomicAdd(a.work + 40, 1u);
-                atomicAdd(a.work + 41, (uint32_t)__popcll(live));
-                atomicAdd(a.work + 42, fc_ent);
-                atomicAdd(a.work + 43, fc_mt);
-                atomicAdd(a.work + 44, (uint32_t)__popcll(found));
-                atomicAdd(a.work + 45, (uint32_t)__popcll(ver));
-                atomicAdd(a.work + 46, (uint32_t)__popcll(found & ~ver));
-                atomicAdd(a.work + 47, found != live ? 1u : 0u);
-                atomicAdd(cy, (unsigned long long)(fb1 - fb0));
-                atomicAdd(cy + 1, (unsigned long long)(fb2 - fb1));
-            }
-#endif
-            shortcut |= ver;
-            // wave-uniform (the counters' lane-0 branch above hides that from
-            // the compiler, which then keeps live in VGPRs)
-            const unsigned long long nl = live & found & ~ver;
-            live = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(nl >> 32)) << 32) |
-                   __builtin_amdgcn_readfirstlane((uint32_t)nl);
-        }
         if (ANYHIT && !STATS && a.fast && live && sc.U > 1) {
             // any-hit shortcut: lanes whose shortcut hit the reference's walk
             // provably reaches are done; the others take the exact walk below
@@ -2976,6 +2932,10 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         // left undecided (the fallback grid stays within the spill area)
         const uint32_t fb = grid < 64u ? grid : 64u;
         const uint32_t gb = bins_grid_blocks(dev);
+        if (BIH_FAST_COUNTERS) {
+            const hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
+            if (e != hipSuccess) return (int)e;
+        }
         switch (__builtin_ctz(spp)) {
         case 0: return (int)launch_bins<0>(a, st, gb, fb);
         case 1: return (int)launch_bins<1>(a, st, gb, fb);

@@ -340,6 +340,36 @@ def test_anyhit_shortcut_matches_exact_walk(scene, gpu, bihrt_mod):
         assert np.array_equal(a, b), (scene, frame, int((a != b).sum()))
 
 
+@pytest.mark.parametrize("scene", ["soup200k", "grazing_dense", "cornell"])
+def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
+    """k_render_fallback (the exact walk for packets the frustum-bin kernel
+    leaves undecided) on every live packet: BIH_BINS_FORCE_FALLBACK=1 sends
+    each one there; every pixel equals the exact walk's, on one stream and
+    with frames in flight on three."""
+    import torch
+    S = bihrt_mod.scenes
+    tris = {"soup200k": lambda: S.soup(200_000, seed=11),
+            "grazing_dense": lambda: np.concatenate([_grazing_scene(60_000, 2),
+                                                     S.soup(60_000, seed=12)])}.get(
+        scene, lambda: SCENES[scene])()
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 480, 270
+    ref = [_device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_REFERENCE) for f in range(4)]
+    monkeypatch.setenv("BIH_BINS_FORCE_FALLBACK", "1")
+    for f in (0, 3):
+        a = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_ANYHIT)
+        assert np.array_equal(a, ref[f]), (scene, f, int((a != ref[f]).sum()))
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.full((h * w,), -1, dtype=torch.int32, device="cuda") for _ in range(4)]
+    for f in range(4):
+        r.render_device(outs[f].data_ptr(), f, stream=streams[f % 3].cuda_stream)
+    torch.cuda.synchronize()
+    for f in range(4):
+        a = outs[f].cpu().numpy().view(np.uint32).reshape(h, w)
+        assert np.array_equal(a, ref[f]), (scene, "in flight", f, int((a != ref[f]).sum()))
+
+
 def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod):
     """Config C5's scene and size on one GPU (10M-triangle soup, 3840x2160,
     4 spp): the any-hit shortcut and the exact walk agree on every pixel of
