@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--traffic", type=int, default=1,
                     help="N=1: measure HBM traffic per launch with rocprofv3 PMC passes "
                          "(child processes, before this process touches the GPU)")
+    ap.add_argument("--kernel-samples", type=int, default=20,
+                    help="isolated launches timed with the library's kernel events (roofline launch_ms)")
     ap.add_argument("--no-reference-leg", action="store_true")
     ap.add_argument("--no-rebuild-leg", action="store_true",
                     help="skip the leg that rebuilds the BIH every frame (as the reference does)")
@@ -180,7 +182,7 @@ def main():
         return el, sum(kms) / len(kms), fps
 
     mode = args.mode if world > 1 else "weak"
-    rows, _, _ = plan(mode)
+    rows, frame_of, _ = plan(mode)
     rays_per_frame = W * H * SPP
     elapsed, kernel_ms, fps = timed(mode, trav, 0)
     value = fps * rays_per_frame * args.steps / elapsed
@@ -226,6 +228,17 @@ def main():
                        "note": "step = bih_rebuild + render"
                                + (" + gather" if mode == "strong" and world > 1 else "")}
 
+    # the dominant kernel's launch duration: HIP events the library records
+    # on the render stream right around the render kernel (bih_last_render_ms),
+    # over isolated launches (each frame synchronised before the next) -- the
+    # figure rocprofv3's kernel trace reports for the same kernel
+    kms_iso = []
+    for k in range(args.kernel_samples):
+        step(mode, rows, k, frame_of(5000, k), trav, nf=1)
+        torch.cuda.synchronize()
+        kms_iso.append(r.last_render_ms())
+    kernel_launch_ms = sum(kms_iso) / len(kms_iso) if kms_iso else None
+
     # per-ray work counters of one frame (untimed): exact integers, equal to
     # the oracle's (tests/test_gpu_parity.py::test_per_ray_counters_match_oracle)
     stat_frame = args.warmup
@@ -245,7 +258,7 @@ def main():
     # events also count the time it queues behind the other stream's frame,
     # so the isolated launches of the one-in-flight leg give the duration
     # (what rocprofv3 reports for `--headline-only --in-flight 1`)
-    launch_ms = serial_leg["kernel_ms"] if serial_leg else kernel_ms
+    launch_ms = kernel_launch_ms if kernel_launch_ms else (serial_leg["kernel_ms"] if serial_leg else kernel_ms)
     work_gbs = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9
     achieved = traffic["bytes_per_launch"] / (launch_ms * 1e-3) / 1e9 if traffic else None
 
@@ -293,12 +306,14 @@ def main():
                 "achieved_source": "measured bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) / "
                                    "launch_ms" if achieved is not None else "traffic not measured",
                 "launch_ms": launch_ms,
-                "launch_ms_source": "one_in_flight leg (isolated launches)" if serial_leg
-                                    else "headline leg",
+                "launch_ms_source": (f"HIP events around the render kernel on its stream "
+                                     f"(bih_last_render_ms), mean of {len(kms_iso)} isolated launches")
+                                    if kernel_launch_ms else "headline leg",
                 "limiter": "scalar-unit issue and memory latency of the packet walk, not HBM "
                            "(DESIGN.md section 4: SQ counters)",
-                "kernel": "k_render_packet_asm (" + ("any-hit: shortcut passes + exact walk for the rest"
-                                                     if trav == 0 else "reference walk") + ")",
+                "kernel": (traffic or {}).get("kernel") or
+                          ("k_render_bins (any-hit: frustum-bin list walk; k_render_fallback finishes "
+                           "undecided packets)" if trav == 0 else "k_render_packet_asm (reference walk)"),
             },
             "work_equivalent": {
                 "bytes_per_ray": b_ray,
@@ -414,19 +429,25 @@ def measure_traffic(args):
             return None
         if p.returncode != 0:
             return None
-        vals = []
+        # the dominant render kernel: k_render_bins (any-hit with frustum
+        # bins), else the BIH packet kernel
+        vals = {}
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
-                if "k_render" in row["Kernel_Name"]:
-                    vals.append(float(row["Counter_Value"]))
-        if not vals:
+                name = row["Kernel_Name"]
+                for key in ("k_render_bins", "k_render_packet_asm"):
+                    if key in name:
+                        vals.setdefault(key, []).append(float(row["Counter_Value"]))
+        key = "k_render_bins" if "k_render_bins" in vals else "k_render_packet_asm"
+        if not vals.get(key):
             return None
-        res[ctr] = sum(vals) / len(vals)
+        kernel_name = key
+        res[ctr] = sum(vals[key]) / len(vals[key])
     shutil.rmtree(tmp, ignore_errors=True)
     fetch = 2.0 * res["FETCH_SIZE"] * 1024.0
     write = res["WRITE_SIZE"] * 1024.0
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024"}
+            "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024", "kernel": kernel_name}
 
 
 if __name__ == "__main__":

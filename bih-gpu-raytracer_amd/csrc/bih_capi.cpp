@@ -32,7 +32,9 @@ constexpr int kRngBufs = kSlots + 1;
 struct bih_tree {
     bih::DeviceTree t;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {};
+    // ev0/ev1: the render kernel's start and end (bih_last_render_ms); evd:
+    // everything the render issued is done (ordering of slot reuse, rebuilds)
+    hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {}, evd[kSlots] = {};
     bool used[kSlots] = {};
     int slot = 0;                    // slot of the next render
     int last_slot = -1;              // slot of the last render
@@ -129,7 +131,7 @@ int check_device(int device) {
 int wait_renders(bih_tree *tr, hipStream_t st) {
     for (int k = 0; k < kSlots; ++k)
         if (tr->used[k]) {
-            hipError_t e = hipStreamWaitEvent(st, tr->ev1[k], 0);
+            hipError_t e = hipStreamWaitEvent(st, tr->evd[k], 0);
             if (e != hipSuccess) return map_hip((int)e);
         }
     return BIH_OK;
@@ -170,7 +172,7 @@ int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &
     if (tr->chunk_cap < n) {
         // every render that may still use the old buffers has finished
         for (int k = 0; k < kSlots; ++k)
-            if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+            if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
         if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
         tr->chunk_buf = nullptr;
         tr->chunk_cap = 0;
@@ -232,6 +234,7 @@ int create_tree(int device, void *stream, bih_tree **out) {
     for (int k = 0; k < kSlots && e == hipSuccess; ++k) {
         e = hipEventCreate(&tr->ev0[k]);
         if (e == hipSuccess) e = hipEventCreate(&tr->ev1[k]);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->evd[k], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
     if (e == hipSuccess && bih::upload_rng_tables(device) != 0) e = hipErrorUnknown;
@@ -371,7 +374,7 @@ void bih_free(bih_tree *tr) {
     DeviceGuard g(tr->t.device);
     if (tr->stream) (void)hipStreamSynchronize(tr->stream);
     for (int k = 0; k < kSlots; ++k)
-        if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+        if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
     bih::free_tree_device(tr->t);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
@@ -386,6 +389,7 @@ void bih_free(bih_tree *tr) {
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
+        if (tr->evd[k]) (void)hipEventDestroy(tr->evd[k]);
         if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
@@ -469,7 +473,7 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
     if (P > tr->rng_cap) {
         for (int k = 0; k < kSlots; ++k)
             if (tr->used[k]) {
-                hipError_t e = hipEventSynchronize(tr->ev1[k]);   // in-flight readers
+                hipError_t e = hipEventSynchronize(tr->evd[k]);   // in-flight readers
                 if (e != hipSuccess) return map_hip((int)e);
             }
         if (tr->rng) (void)hipFree(tr->rng);
@@ -634,7 +638,7 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
         const size_t need = bih::bin_queue_bytes(ntiles);
         if (tr->q_cap < need) {
             for (int k = 0; k < kSlots; ++k)
-                if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
             if (tr->q_mem) (void)hipFree(tr->q_mem);
             tr->q_mem = nullptr;
             tr->q_cap = 0;
@@ -652,7 +656,7 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
     }
     if (tr->fbq_cap < ntiles) {
         for (int k = 0; k < kSlots; ++k)
-            if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+            if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
         if (tr->fb_mem) (void)hipFree(tr->fb_mem);
         tr->fb_mem = nullptr;
         tr->fbq_cap = 0;
@@ -707,7 +711,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     // separate streams overlap, each filling the one before's tail.
     const int slot = tr->slot;
     if (tr->used[slot]) {
-        hipError_t e = hipStreamWaitEvent(st, tr->ev1[slot], 0);
+        hipError_t e = hipStreamWaitEvent(st, tr->evd[slot], 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
     if (tr->rng_pending) {
@@ -738,7 +742,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         }
         if (grow) {
             for (int k = 0; k < kSlots; ++k)
-                if (tr->used[k]) (void)hipEventSynchronize(tr->ev1[k]);
+                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
             if (tr->prim) (void)hipFree(tr->prim);
             tr->prim = nullptr;
             tr->prim_cap = 0;
@@ -840,11 +844,9 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.ray_stats = d_ray_stats;
     a.work = tr->work + (size_t)slot * bih::kWorkWords;
     a.spill = tr->spill + (size_t)slot * tr->spill_per_slot;
-    e = hipEventRecord(tr->ev0[slot], st);
-    if (e != hipSuccess) return map_hip((int)e);
-    rc = bih::launch_render(a, traverse, st);
+    rc = bih::launch_render(a, traverse, st, tr->ev0[slot], tr->ev1[slot]);
     if (rc) return map_hip(rc);
-    e = hipEventRecord(tr->ev1[slot], st);
+    e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
     tr->last_slot = slot;
@@ -970,7 +972,7 @@ int bih_last_render_ms(const bih_tree *tr, double *ms) {
     if (!tr || !ms || tr->last_slot < 0) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     const int k = tr->last_slot;
-    hipError_t e = hipEventSynchronize(tr->ev1[k]);
+    hipError_t e = hipEventSynchronize(tr->evd[k]);
     if (e != hipSuccess) return map_hip((int)e);
     float f = 0.f;
     e = hipEventElapsedTime(&f, tr->ev0[k], tr->ev1[k]);

@@ -170,7 +170,10 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
 int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
                        void *stream);
-int launch_render(const RenderArgs &a, uint32_t traverse, void *stream);
+// ev_k0 / ev_k1 (hipEvent_t or null): recorded right before and after the
+// main render kernel (bih_last_render_ms)
+int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev_k0 = nullptr,
+                  void *ev_k1 = nullptr);
 uint32_t wave_grid_blocks(int device);     // persistent grid of the render kernels
 size_t spill_words(uint32_t blocks);
 // chunks of the packet kernel's tile queue for a w x nrows launch (0: no packet kernel)

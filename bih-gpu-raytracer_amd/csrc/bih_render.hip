@@ -2915,14 +2915,20 @@ uint32_t bins_grid_blocks(int device) {
 }
 
 template <int L>
-static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t blocks, uint32_t fb_blocks) {
+static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t blocks, uint32_t fb_blocks,
+                              hipEvent_t k0, hipEvent_t k1) {
+    hipError_t e = k0 ? hipEventRecord(k0, st) : hipSuccess;
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render_bins<L>, dim3(blocks), dim3(kThreads), 0, st, a);
+    e = k1 ? hipEventRecord(k1, st) : hipSuccess;
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render_fallback<L>, dim3(fb_blocks), dim3(kThreads), 0, st, a);
     return hipGetLastError();
 }
 
-int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
+int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev_k0, void *ev_k1) {
     hipStream_t st = (hipStream_t)stream;
+    const hipEvent_t k0 = (hipEvent_t)ev_k0, k1 = (hipEvent_t)ev_k1;
     const uint32_t spp = a.spp;
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -2937,13 +2943,13 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
             if (e != hipSuccess) return (int)e;
         }
         switch (__builtin_ctz(spp)) {
-        case 0: return (int)launch_bins<0>(a, st, gb, fb);
-        case 1: return (int)launch_bins<1>(a, st, gb, fb);
-        case 2: return (int)launch_bins<2>(a, st, gb, fb);
-        case 3: return (int)launch_bins<3>(a, st, gb, fb);
-        case 4: return (int)launch_bins<4>(a, st, gb, fb);
-        case 5: return (int)launch_bins<5>(a, st, gb, fb);
-        default: return (int)launch_bins<6>(a, st, gb, fb);
+        case 0: return (int)launch_bins<0>(a, st, gb, fb, k0, k1);
+        case 1: return (int)launch_bins<1>(a, st, gb, fb, k0, k1);
+        case 2: return (int)launch_bins<2>(a, st, gb, fb, k0, k1);
+        case 3: return (int)launch_bins<3>(a, st, gb, fb, k0, k1);
+        case 4: return (int)launch_bins<4>(a, st, gb, fb, k0, k1);
+        case 5: return (int)launch_bins<5>(a, st, gb, fb, k0, k1);
+        default: return (int)launch_bins<6>(a, st, gb, fb, k0, k1);
         }
     }
     if (spp <= 64 && (spp & (spp - 1)) == 0) {
@@ -2958,6 +2964,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         // the tile queue of the per-CU slots starts from zero; the bins' item
         // queue resets itself (counter builds also count into a.work)
         hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
+        if (e == hipSuccess && k0) e = hipEventRecord(k0, st);
         if (e != hipSuccess) return (int)e;
         switch (L) {
         case 0: e = launch_persistent<0>(var, a, traverse, st, blocks); break;
@@ -2968,6 +2975,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         case 5: e = launch_persistent<5>(var, a, traverse, st, blocks); break;
         default: e = launch_persistent<6>(var, a, traverse, st, blocks); break;
         }
+        if (e == hipSuccess && k1) e = hipEventRecord(k1, st);
         return (int)e;
     }
     // any other spp: one lane per pixel, grid-stride, grid capped at the spill area
@@ -2976,6 +2984,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
     uint32_t blocks = (tiles + 3) / 4;
     if (blocks > grid) blocks = grid;
     const bool stats = a.ray_stats != nullptr;
+    if (k0) (void)hipEventRecord(k0, st);
     if (traverse == 0) {
         if (stats) hipLaunchKernelGGL((k_render_pixel<true, true>), dim3(blocks), dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((k_render_pixel<true, false>), dim3(blocks), dim3(kThreads), 0, st, a);
@@ -2983,6 +2992,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream) {
         if (stats) hipLaunchKernelGGL((k_render_pixel<false, true>), dim3(blocks), dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((k_render_pixel<false, false>), dim3(blocks), dim3(kThreads), 0, st, a);
     }
+    if (k1) (void)hipEventRecord(k1, st);
     return (int)hipGetLastError();
 }
 
