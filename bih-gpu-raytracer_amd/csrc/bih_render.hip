@@ -1657,6 +1657,9 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #ifndef BIH_BIN_PREFETCH_AT
 #define BIH_BIN_PREFETCH_AT 16
 #endif
+#ifndef BIH_BIN_PREFETCH
+#define BIH_BIN_PREFETCH 1
+#endif
 __device__ __forceinline__ float lane_f(float v, uint32_t j) {
     return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), j));
 }
@@ -1682,18 +1685,24 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
     unsigned long long rem = live;
     const unsigned long long me = lane_bit(lane);
     for (int part = 0; part < 2; ++part) {
+#if BIH_BIN_PREFETCH
         float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
         if (e < end) bin_chunk_load(ents, e, end, lane, c0, c1, c2);
+#endif
         while (e < end && rem) {
-            const float4 d0 = c0, d1 = c1, d2 = c2;
-            const uint32_t n = end - e < 64u ? end - e : 64u;
+#if BIH_BIN_PREFETCH
             // the next chunk is requested once this one is a quarter done
-            // with lanes left: a packet that ends early leaves no load in
-            // flight for the verification's loads to queue behind (vmcnt
-            // retires in order)
+            const float4 d0 = c0, d1 = c1, d2 = c2;
+#else
+            float4 d0 = make_float4(0.f, 0.f, 0.f, 0.f), d1 = d0, d2 = d0;
+            bin_chunk_load(ents, e, end, lane, d0, d1, d2);
+#endif
+            const uint32_t n = end - e < 64u ? end - e : 64u;
             for (uint32_t j = 0; j < n && rem; ++j) {
+#if BIH_BIN_PREFETCH
                 if (j == BIH_BIN_PREFETCH_AT && e + 64u < end)
                     bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
+#endif
                 const float f0 = __builtin_fmaf(lane_f(d0.z, j), vf,
                                                 __builtin_fmaf(lane_f(d0.y, j), uf, lane_f(d0.x, j)));
                 const float f1 = __builtin_fmaf(lane_f(d1.y, j), vf,
@@ -1714,8 +1723,6 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 }
                 rem &= ~h;
             }
-            if (n <= BIH_BIN_PREFETCH_AT && e + 64u < end)   // (cannot happen: n < 64 is the last chunk)
-                bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
             e += 64u;
         }
         if (!rem) break;
@@ -1839,6 +1846,14 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 // the slot from a band head.  One device-wide atomic per batch instead of
 // one per item: a single head word saturates near 90 dequeues per us.
 // ---------------------------------------------------------------------------
+#ifndef BIH_BINS_WAVES_PER_EU
+#define BIH_BINS_WAVES_PER_EU 0   // 0: the compiler's choice
+#endif
+#if BIH_BINS_WAVES_PER_EU
+#define BIH_BINS_OCC __attribute__((amdgpu_waves_per_eu(BIH_BINS_WAVES_PER_EU, BIH_BINS_WAVES_PER_EU)))
+#else
+#define BIH_BINS_OCC
+#endif
 constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hits lo/hi, pad
 constexpr uint32_t kBinBatch = 16;
 constexpr uint32_t kBinSlot0 = 16 * 32;   // words: heads at b * 32, fallback count at 8 * 32
@@ -1891,7 +1906,7 @@ struct BinQueue {
     }
 };
 template <int LOG2SPP>
-__global__ void __launch_bounds__(kThreads) k_render_bins(const RenderArgs a) {
+__global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const RenderArgs a) {
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1968,11 +1983,12 @@ __global__ void __launch_bounds__(kThreads) k_render_bins(const RenderArgs a) {
         if (tzmax < tMax) tMax = tzmax;
         const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
         unsigned long long hits = 0ull, undecided = 0ull;
-        if (live && sc.U > 1) {
+        if (live && sc.U > 1 && !(a.dbg & 8u)) {
             uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0;
             const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
                                                       cmeta, cent, fc_ent, fc_mt);
-            const bool ok = ((found >> lane) & 1ull) && plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax);
+            const bool ok = ((found >> lane) & 1ull) &&
+                            ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
             hits = __ballot(ok);
             undecided = live & found & ~hits;
 #if BIH_FAST_COUNTERS
