@@ -262,6 +262,13 @@ def main():
     work_gbs = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9
     achieved = traffic["bytes_per_launch"] / (launch_ms * 1e-3) / 1e9 if traffic else None
 
+    bst = arrays.bins_stats()
+    bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
+            "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
+            "entry_bytes": 64,
+            "note": "frustum bins of the bench camera (bih_bins_get_stats): per 4x4-pixel tile the "
+                    "triangles whose edge pre-test a sample of the tile can pass"}
+
     cpu = None
     parity_rows = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -329,6 +336,7 @@ def main():
                         "prices work the kernel does not do: it is not a bandwidth",
             },
             "traffic_detail": traffic,
+            "bins": bins,
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
             "with_rebuild": rebuild_leg,

@@ -76,6 +76,13 @@ class GPUArrayManager:
         check(load().bih_tree_get_info(self._tree, C.byref(inf)), "bih_tree_get_info")
         return inf
 
+    def bins_stats(self):
+        """Frustum bins of the current camera and image (bih_bins_get_stats)."""
+        from ._lib import BinsStats
+        st = BinsStats()
+        check(load().bih_bins_get_stats(self._tree, C.byref(st)), "bih_bins_get_stats")
+        return st
+
     def export(self, which: int, dtype) -> np.ndarray:
         n = C.c_size_t(0)
         check(load().bih_tree_export(self._tree, which, None, C.byref(n)), "bih_tree_export")

@@ -65,6 +65,11 @@ class Rows(C.Structure):
                 ("band_step", C.c_uint32)]
 
 
+class BinsStats(C.Structure):
+    _fields_ = [("usable", C.c_uint32), ("tiles_x", C.c_uint32), ("tiles_y", C.c_uint32),
+                ("list_entries", C.c_uint64), ("global_entries", C.c_uint32)]
+
+
 class TreeInfo(C.Structure):
     _fields_ = [("n_tris", C.c_uint32), ("n_unique", C.c_uint32), ("scene_lo", C.c_float * 3),
                 ("scene_hi", C.c_float * 3), ("device", C.c_int), ("device_bytes", C.c_uint64),
@@ -121,9 +126,10 @@ def load():
                                     C.POINTER(Rows), u32, vp, vp, vp]
     L.bih_sync.argtypes = [vp, vp]
     L.bih_last_render_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.bih_bins_get_stats.argtypes = [vp, C.POINTER(BinsStats)]
     for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
-                 "bih_render_device", "bih_sync", "bih_last_render_ms"):
+                 "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_bins_get_stats"):
         getattr(L, name).restype = i32
     _lib = L
     return L

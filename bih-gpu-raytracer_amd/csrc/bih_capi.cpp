@@ -84,6 +84,7 @@ struct bih_tree {
     float *bin_gent = nullptr;       // global list entries (in bins_mem)
     uint32_t bin_gn = 0;             // global list length
     uint32_t bins_gen = 0;           // incremented by every bins build
+    uint64_t bin_entries = 0;        // list entries over all tiles
     // the render kernel's tile queue over one launch's rows (launch_bin_queue),
     // for q_key = {w, h, spp, row0, nrows, band_h, band_step, bins_gen}
     char *q_mem = nullptr;
@@ -612,6 +613,7 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     tr->bins = b;
     tr->bin_gent = gent;
     tr->bin_gn = tot[1];
+    tr->bin_entries = tot[0];
     tr->bins_usable = true;
     return BIH_OK;
 }
@@ -978,6 +980,17 @@ int bih_last_render_ms(const bih_tree *tr, double *ms) {
     e = hipEventElapsedTime(&f, tr->ev0[k], tr->ev1[k]);
     if (e != hipSuccess) return map_hip((int)e);
     *ms = f;
+    return BIH_OK;
+}
+
+int bih_bins_get_stats(const bih_tree *tr, bih_bins_stats *out) {
+    if (!tr || !out) return BIH_ERR_INVALID;
+    memset(out, 0, sizeof *out);
+    out->usable = tr->bins_usable && tr->bins_valid ? 1u : 0u;
+    out->tiles_x = tr->bins.bins_x;
+    out->tiles_y = tr->bins.bins_y;
+    out->list_entries = tr->bin_entries;
+    out->global_entries = tr->bin_gn;
     return BIH_OK;
 }
 

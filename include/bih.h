@@ -169,9 +169,21 @@ int bih_render_device(const bih_tree *tree, const bih_camera *camera, uint32_t w
                       uint32_t traverse, uint32_t *d_out, uint32_t *d_ray_stats, void *stream);
 int bih_sync(const bih_tree *tree, void *stream);
 
-/* Device time (ms, HIP events on the render stream) of the last render
- * kernel launched through this tree. */
+/* Device time (ms, HIP events on the render stream, recorded right before
+ * and after the main render kernel) of the last render launched through this
+ * tree. */
 int bih_last_render_ms(const bih_tree *tree, double *ms);
+
+/* The frustum bins of the tree's current camera and image (any-hit renders):
+ * usable = 1 when renders walk them; list entries over all tiles, entries of
+ * the global list, tiles (TW x TH pixels, one 64-ray packet each). */
+typedef struct bih_bins_stats {
+    uint32_t usable;
+    uint32_t tiles_x, tiles_y;
+    uint64_t list_entries;
+    uint32_t global_entries;
+} bih_bins_stats;
+int bih_bins_get_stats(const bih_tree *tree, bih_bins_stats *out);
 
 #ifdef __cplusplus
 }
