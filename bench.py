@@ -217,6 +217,37 @@ def main():
                     "ms_per_step": 1e3 * el4 / args.steps, "kernel_ms": kms4,
                     "parallelism": parallelism(other_mode, args.band, world)}
 
+    # a camera that moves every frame: the per-camera structures (primary-ray
+    # records, frustum bins, tile queue) are rebuilt inside every step
+    moving_leg = None
+    if not args.no_rebuild_leg:
+        from bihrt import Camera
+        base_cam = cam.as_list()
+        cams = []
+        for k in range(8):
+            c = list(base_cam)
+            d = (0.002 * k, 0.001 * k, -0.003 * k)
+            for j in range(3):
+                c[j] += d[j]
+                c[3 + j] += d[j]
+            cams.append(Camera.from_list(c))
+        rows_m, frame_of_m, fps_m = plan(mode)
+        for k in range(args.warmup):
+            r.camera = cams[k % len(cams)]
+            step(mode, rows_m, k, frame_of_m(6000, k), trav)
+        sync_all()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            r.camera = cams[(args.warmup + k) % len(cams)]
+            step(mode, rows_m, args.warmup + k, frame_of_m(6000, args.warmup + k), trav)
+        sync_all()
+        el6 = max_over_ranks(time.perf_counter() - t0)
+        r.camera = cam
+        moving_leg = {"value": fps_m * rays_per_frame * args.steps / el6, "unit": "rays/s",
+                      "ms_per_step": 1e3 * el6 / args.steps,
+                      "note": "step = render with a camera that moved since the last frame (8 cameras in "
+                              "turn): primary-ray records, frustum bins and tile queue rebuilt per step"}
+
     # the reference rebuilds the BIH every frame (Renderer::Render,
     # Renderer.cpp:415-503): time rebuild + render per step as well
     rebuild_leg = None
@@ -340,6 +371,7 @@ def main():
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
             "with_rebuild": rebuild_leg,
+            "moving_camera": moving_leg,
             "one_in_flight": serial_leg,
             "other_decomposition": side_leg,
         }

@@ -170,15 +170,17 @@ __device__ __forceinline__ void edge_pretest(const float *rr, float a, float b, 
 struct PlanL {
     double L[3];
 };
-__device__ __forceinline__ PlanL plane_l(const double (*X)[3], int ax, double val, bool le, double amin,
-                                         double amax) {
+// ramin / ramax: 1 / min|X[a]|, 1 / max|X[a]| over the hull (0: that bound
+// is 0; the f64 reciprocal's rounding is far below the 4e margins)
+__device__ __forceinline__ PlanL plane_l(const double (*X)[3], int ax, double val, bool le, double ramin,
+                                         double ramax) {
     PlanL o;
     const double r = 4.0 * 0x1p-24 * fabs(val);
     for (int j = 0; j < 3; ++j) {
         const double h = (le ? val - X[j][ax] : X[j][ax] - val) - r;
         double m;
-        if (h >= 0.0) m = amax > 0.0 ? h / amax : INFINITY;
-        else m = amin > 0.0 ? h / amin : -INFINITY;
+        if (h >= 0.0) m = ramax > 0.0 ? h * ramax : INFINITY;
+        else m = ramin > 0.0 ? h * ramin : -INFINITY;
         o.L[j] = (m == m) ? m : -INFINITY;
     }
     return o;
@@ -192,8 +194,10 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
     for (int ax = 0; ax < 3; ++ax) {
         const double lo = fmin(fmin(X[0][ax], X[1][ax]), X[2][ax]);
         const double hi = fmax(fmax(X[0][ax], X[1][ax]), X[2][ax]);
-        amin[ax] = lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0);
-        amax[ax] = fmax(fabs(lo), fabs(hi));
+        const double mn = lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0);
+        const double mx = fmax(fabs(lo), fabs(hi));
+        amin[ax] = mn > 0.0 ? 1.0 / mn : 0.0;   // reciprocals (plane_l)
+        amax[ax] = mx > 0.0 ? 1.0 / mx : 0.0;
         sgn[ax] = lo > 0.0 ? 1 : (hi < 0.0 ? -1 : 0);
     }
     // slab faces: the smallest L over the faces that can be entries / exits
@@ -569,14 +573,23 @@ __global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__rest
                                                           uint32_t th, uint32_t bins_x, uint32_t lpt,
                                                           uint16_t *__restrict__ cls,
                                                           uint32_t *__restrict__ qw) {
+    // class counts aggregated per block in LDS: one global atomic per class
+    // present (a tile row band has a handful), not one per tile
+    __shared__ uint32_t hist[kQBands * kQClasses];
+    for (uint32_t k = threadIdx.x; k < kQBands * kQClasses; k += kThreads) hist[k] = 0;
+    __syncthreads();
     const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
-    if (t >= ntiles) return;
-    const uint32_t b = queue_bin(t, tiles_x, row0, band_h, band_step, th, bins_x);
-    const uint32_t len = off[b + 1] - off[b] + gn;
-    const uint32_t band = (uint32_t)(((uint64_t)(t / tiles_x) * kQBands) / tiles_y);
-    const uint32_t k = band * kQClasses + (len ? (lpt ? (uint32_t)__clz(len) : 0u) : kQClasses - 1);
-    cls[t] = (uint16_t)k;
-    atomicAdd(qw + k, 1u);
+    if (t < ntiles) {
+        const uint32_t b = queue_bin(t, tiles_x, row0, band_h, band_step, th, bins_x);
+        const uint32_t len = off[b + 1] - off[b] + gn;
+        const uint32_t band = (uint32_t)(((uint64_t)(t / tiles_x) * kQBands) / tiles_y);
+        const uint32_t k = band * kQClasses + (len ? (lpt ? (uint32_t)__clz(len) : 0u) : kQClasses - 1);
+        cls[t] = (uint16_t)k;
+        atomicAdd(&hist[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kQBands * kQClasses; k += kThreads)
+        if (hist[k]) atomicAdd(qw + k, hist[k]);
 }
 __global__ void k_queue_scan(uint32_t *__restrict__ qw) {
     if (threadIdx.x != 0) return;
@@ -599,10 +612,22 @@ __global__ void k_queue_scan(uint32_t *__restrict__ qw) {
 __global__ void __launch_bounds__(kThreads) k_queue_fill(const uint16_t *__restrict__ cls, uint32_t ntiles,
                                                          uint32_t *__restrict__ qw,
                                                          uint32_t *__restrict__ queue) {
+    // ranks within the block by LDS atomics, then one global reservation per
+    // class present
+    __shared__ uint32_t hist[kQBands * kQClasses], base[kQBands * kQClasses];
+    for (uint32_t k = threadIdx.x; k < kQBands * kQClasses; k += kThreads) hist[k] = 0;
+    __syncthreads();
     const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
-    if (t >= ntiles) return;
-    const uint32_t k = cls[t];
-    queue[qw[288 + k] + atomicAdd(qw + 576 + k, 1u)] = t;
+    uint32_t k = 0, r = 0;
+    if (t < ntiles) {
+        k = cls[t];
+        r = atomicAdd(&hist[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kQBands * kQClasses; j += kThreads)
+        if (hist[j]) base[j] = qw[288 + j] + atomicAdd(qw + 576 + j, hist[j]);
+    __syncthreads();
+    if (t < ntiles) queue[base[k] + r] = t;
 }
 
 }  // namespace

@@ -70,6 +70,7 @@ struct bih_tree {
     float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
+    bool fast_valid = false;         // the BIH walk's shortcut boxes match the records
     uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
     // frustum bins (bih_bins.hip) of the camera the records were built for,
     // for one image size and tile shape (bins_key = {w, h, spp})
@@ -770,6 +771,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
             tr->bins_valid = false;
+            tr->fast_valid = false;
         }
         const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
         if (bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0 &&
@@ -810,8 +812,24 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
         if (rc) return rc;
     }
+    // the BIH walk's shortcut boxes (any-hit without bins), built on first
+    // use for this camera
+    const bool use_fast = tr->prim && n_int > 0 && fast_enabled() > 0 && !use_bins &&
+                          traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats;
+    if (use_fast && !tr->fast_valid) {
+        rc = wait_renders(tr, st);
+        if (rc) return rc;
+        float dmax[3];
+        (void)bih_camera_ray_bound(cam, dmax);
+        const int le = bih::launch_fast_boxes(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
+                                              tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
+                                              cam->origin, dmax, tr->prim, st);
+        if (le) return map_hip(le);
+        tr->fast_valid = true;
+    }
     // the next render (on any stream) orders after the advance above, the
-    // per-camera records and the tile queue, which it reads as they stand now
+    // per-camera records, the shortcut boxes and the tile queue, which it
+    // reads as they stand now
     e = hipEventRecord(tr->ev_rng, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
@@ -835,7 +853,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
     a.node_cull = a.node_prim ? a.node_prim + (n_int + 1) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
-    if (tr->prim && n_int > 0 && fast_enabled() > 0) {
+    if (use_fast) {
         a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
                                                  bih::fast_offset(tr->t.n, n_int));
         if (fast_enabled() > 1) a.fast2 = a.fast + 16ull * (n_int + 1);

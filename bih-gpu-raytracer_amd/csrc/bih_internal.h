@@ -186,13 +186,17 @@ int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks
 // pad, then the same m + 1 records with unhittable subtrees cut off, then
 // per-leaf and per-node alive bytes, then the any-hit walk's two shortcut
 // box sets (m + 1 records of 16 x 32 bit each, k_fast_fit / k_fast_refs:
-// tight, then miss-proof for |D| <= dmax per component) and m arrival counters
+// tight, then miss-proof for |D| <= dmax per component; launch_fast_boxes)
+// and m arrival counters
 size_t prim_bytes(uint32_t n, uint32_t m);
 size_t fast_offset(uint32_t n, uint32_t m);   // byte offset of the shortcut boxes
 int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
                 const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
                 uint32_t m, const float origin[3], const float dmax[3], float *prim,
                 void *stream);
+int launch_fast_boxes(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
+                      const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
+                      uint32_t m, const float origin[3], const float dmax[3], float *prim, void *stream);
 bool render_uses_prim(uint32_t spp);
 
 // frustum bins (bih_bins.hip): camera setup (false: degenerate camera, no

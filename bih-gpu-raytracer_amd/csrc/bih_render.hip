@@ -2823,6 +2823,19 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
                                node_alive);
         hipLaunchKernelGGL(k_node_prim, gn, dim3(kThreads), 0, st, nodes, m, origin[0], origin[1],
                            origin[2], leaf_alive, node_alive, rec, rec + (m + 1));
+    }
+    return (int)hipGetLastError();
+}
+
+// The any-hit BIH walk's shortcut boxes for the records launch_prim wrote
+// (only renders without frustum bins read them).
+int launch_fast_boxes(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
+                      const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
+                      uint32_t m, const float origin[3], const float dmax[3], float *prim, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    if (m > 0) {
+        const dim3 gl((m + 1 + kThreads - 1) / kThreads), gn((m + kThreads - 1) / kThreads);
+        hipError_t e = hipSuccess;
         // shortcut boxes of the any-hit walk: tight (pass 1), miss-proof (pass 2)
         float *fast = reinterpret_cast<float *>(reinterpret_cast<char *>(prim) + fast_offset(n, m));
         uint32_t *arrive = reinterpret_cast<uint32_t *>(fast + 2 * 16ull * (m + 1));
