@@ -45,10 +45,10 @@
 //     kernel's fmaf evaluation (x4 margin).  A lane failing one edge cannot
 //     be accepted by MT: the packet skips the triangle for it;
 //   leaf: the leaf holding the triangle (the one fast_verify checks).
-// Per leaf the root path goes into a per-camera table of 32 8-byte steps
-// {clip - O[axis] of the side taken, axis | side << 2}, end = 8 (16: path too
-// deep, never verified), so that the check loads it without a dependent
-// chain.
+// Per leaf whose triangle's plan is the full check, the root path goes into a
+// per-camera table of 32 8-byte steps {clip - O[axis] of the side taken,
+// axis | side << 2}, end = 8 (16: path too deep, never verified), so that the
+// check loads it without a dependent chain.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
@@ -216,60 +216,81 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
                 if (can_exit) slabX.L[j] = fmin(slabX.L[j], l.L[j]);
             }
         }
-    // the root path, leaf first
-    float pv[64];
-    uint8_t pa[64];
-    bool pl[64];
-    int n = 0;
-    {
-        uint32_t cidx = leaf;
-        bool cleaf = true;
-        for (int32_t p = leaf_parent[leaf]; p >= 0; p = parent[p]) {
-            if (n == 64) return kFull;
-            const uint4 r = node_prim[p];
-            const uint32_t split = r.z >> 8, ax = r.z & 0xffu;
-            if (ax > 2u) return kFull;
-            const bool leafL = (r.w >> 26) & 1u;
-            const bool left = cidx == split && cleaf == leafL;
-            pv[n] = __uint_as_float(left ? r.x : r.y);
-            pa[n] = (uint8_t)ax;
-            pl[n] = left;
-            ++n;
-            cidx = (uint32_t)p;
-            cleaf = false;
-        }
-    }
-    // root first: each plane against the last plane of the other kind
+    // the root path, root first (Karras: leaf k lies left of node n iff
+    // k <= split(n); every thread reads the top levels from cache), each
+    // plane against the last plane of the other kind
     PlanL lastE = slabE, lastX = slabX;
-    int lastEi = -1, lastXi = -1;             // -1: the slab endpoint
-    uint32_t meta = 0, nc = 0;
-    for (int i = n - 1; i >= 0; --i) {
-        const int ax = pa[i];
-        if (sgn[ax] == 0 || pv[i] == 0.0f || !(pv[i] == pv[i])) return kFull;
-        const bool le = pl[i];
+    float lastEv = 0.0f, lastXv = 0.0f;
+    uint32_t lastEa = 0, lastXa = 0;
+    bool lastEslab = true, lastXslab = true;
+    uint32_t meta = 0, nc = 0, node = 0;
+    for (int depth = 0;; ++depth) {
+        if (depth == 64) return kFull;
+        const uint4 r = node_prim[node];
+        const uint32_t split = r.z >> 8, ax = r.z & 0xffu;
+        if (ax > 2u) return kFull;
+        const bool le = leaf <= split;             // left child: region X[a] <= clip0 - O
+        const bool child_leaf = le ? ((r.w >> 26) & 1u) != 0u : (r.w >> 31) != 0u;
+        const float val = __uint_as_float(le ? r.x : r.y);
+        if (sgn[ax] == 0 || val == 0.0f || !(val == val)) return kFull;
         const bool is_exit = le == (sgn[ax] > 0);
-        const PlanL l = plane_l(X, ax, (double)pv[i], le, amin[ax], amax[ax]);
+        const PlanL l = plane_l(X, ax, (double)val, le, amin[ax], amax[ax]);
         const PlanL &q = is_exit ? lastE : lastX;
-        const int qi = is_exit ? lastEi : lastXi;
         bool ok = true;
         for (int j = 0; j < 3; ++j) ok = ok && (l.L[j] + q.L[j] > 0.0);
         if (!ok) {
             if (nc == 2) return kFull;
-            meta |= ((uint32_t)ax | (is_exit ? 4u : 0u) | ((qi >= 0 ? (uint32_t)pa[qi] : 0u) << 3) |
-                     (qi < 0 ? 32u : 0u)) << (2 + 6 * nc);
-            vals[2 * nc] = pv[i];
-            vals[2 * nc + 1] = qi >= 0 ? pv[qi] : 0.0f;
+            const bool qslab = is_exit ? lastEslab : lastXslab;
+            const uint32_t qa = is_exit ? lastEa : lastXa;
+            meta |= (ax | (is_exit ? 4u : 0u) | ((qslab ? 0u : qa) << 3) | (qslab ? 32u : 0u)) << (2 + 6 * nc);
+            vals[2 * nc] = val;
+            vals[2 * nc + 1] = qslab ? 0.0f : (is_exit ? lastEv : lastXv);
             ++nc;
         }
         if (is_exit) {
             lastX = l;
-            lastXi = i;
+            lastXv = val;
+            lastXa = ax;
+            lastXslab = false;
         } else {
             lastE = l;
-            lastEi = i;
+            lastEv = val;
+            lastEa = ax;
+            lastEslab = false;
         }
+        const uint32_t child = le ? split : split + 1u;
+        if (child_leaf) {
+            if (child != leaf) return kFull;       // (a malformed tree: never)
+            break;
+        }
+        node = child;
     }
     return meta | nc;
+}
+
+// Root path of leaf k as 32 steps root-first (header comment).  Written by
+// k_bin_fp for the leaves of the entries whose plan is the full check (the
+// only readers); several triangles of one leaf write the same values.
+__device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint2 *__restrict__ path) {
+    uint2 *out = path + 32ull * k;
+    uint32_t node = 0;
+    for (int j = 0;; ++j) {
+        if (j == 31) {
+            out[0] = make_uint2(0u, 8u | 16u);   // too deep: never verified, the exact walk decides
+            return;
+        }
+        const uint4 r = node_prim[node];
+        const uint32_t split = r.z >> 8, axis = r.z & 0xffu;
+        const bool le = k <= split;
+        const uint32_t side = le ? 0u : 1u;
+        out[j] = make_uint2(le ? r.x : r.y, axis | (side << 2));
+        const bool child_leaf = le ? ((r.w >> 26) & 1u) != 0u : (r.w >> 31) != 0u;
+        if (child_leaf) {
+            out[j + 1] = make_uint2(0u, 8u);
+            return;
+        }
+        node = le ? split : split + 1u;
+    }
 }
 
 // Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
@@ -279,7 +300,8 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
                                                      BinCamera c, const TreeHeader *__restrict__ hdr,
                                                      const uint4 *__restrict__ node_prim,
                                                      const int32_t *__restrict__ leaf_parent,
-                                                     const int32_t *__restrict__ parent, uint2 *__restrict__ brect,
+                                                     const int32_t *__restrict__ parent,
+                                                     uint2 *__restrict__ path, uint2 *__restrict__ brect,
                                                      float *__restrict__ binrec,
                                                      uint32_t *__restrict__ gcount,
                                                      uint32_t *__restrict__ glist) {
@@ -394,6 +416,11 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
         rec[9] = __uint_as_float(i);
         rec[10] = __uint_as_float(__float_as_uint(r[13]) | (plan == 0u ? 0x80000000u : 0u));
         rec[11] = __uint_as_float(plan);
+#ifndef BIH_FAST_COUNTERS
+#define BIH_FAST_COUNTERS 0
+#endif
+        // counter builds check every plan against the root-path check: all paths
+        if (plan == 3u || BIH_FAST_COUNTERS) write_path(node_prim, __float_as_uint(r[13]), path);
         for (int k = 0; k < 4; ++k) rec[12 + k] = plan_vals[k];
         float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
         for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
@@ -517,36 +544,6 @@ __global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restri
     const uint32_t i = glist[j];
     for (int k = 0; k < 4; ++k) gent[4ull * j + k] = binrec[4ull * i + k];
 }
-
-// Root path of leaf k as 32 steps root-first (header comment).
-__global__ void __launch_bounds__(kThreads) k_bin_paths(const uint4 *__restrict__ node_prim,
-                                                        const int32_t *__restrict__ leaf_parent,
-                                                        const int32_t *__restrict__ parent,
-                                                        uint32_t U, uint2 *__restrict__ path) {
-    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-    if (k >= U) return;
-    uint2 *out = path + 32ull * k;
-    int depth = 0;
-    for (int32_t p = leaf_parent[k]; p >= 0 && depth <= 32; p = parent[p]) ++depth;
-    if (depth > 31) {
-        out[0] = make_uint2(0u, 8u | 16u);   // never verified: the exact walk decides
-        return;
-    }
-    uint32_t cidx = k;
-    bool cleaf = true;
-    int j = depth - 1;
-    for (int32_t p = leaf_parent[k]; p >= 0; p = parent[p], --j) {
-        const uint4 r = node_prim[p];
-        const uint32_t split = r.z >> 8, axis = r.z & 0xffu;
-        const bool leafL = (r.w >> 26) & 1u;
-        const uint32_t side = (cidx == split && cleaf == leafL) ? 0u : 1u;
-        out[j] = make_uint2(side ? r.y : r.x, axis | (side << 2));
-        cidx = (uint32_t)p;
-        cleaf = false;
-    }
-    out[depth] = make_uint2(0u, 8u);
-}
-
 
 // Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of
 // its rows, bih_rows), in kRegions bands of tile rows, one per XCD (the
@@ -706,13 +703,12 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
     if (U > 0) {
         const dim3 g((U + kThreads - 1) / kThreads);
         hipLaunchKernelGGL(k_bin_leaf, g, dim3(kThreads), 0, st, first_idx, dup_cnt, U, prim);
-        hipLaunchKernelGGL(k_bin_paths, g, dim3(kThreads), 0, st, node_prim, leaf_parent, parent, U,
-                           b.path);
+
     }
     if (n > 0) {
         const dim3 g((n + kThreads - 1) / kThreads);
         hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, leaf_parent,
-                           parent, b.brect, b.binrec, b.gcount,
+                           parent, b.path, b.brect, b.binrec, b.gcount,
                            b.glist);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt);

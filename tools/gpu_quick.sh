@@ -8,7 +8,10 @@ tail -3 gpurun_out/${T}_tests.log
 J=gpurun_out/${T}_time.jsonl; rm -f $J
 timeout -k 10 120 python tools/time_render.py --tag bins >> $J 2>/dev/null || exit 1
 grep -o '"tag[^,]*\|"ms_mean[^,]*' $J
-BIH_LIB=bih-gpu-raytracer_amd/lib/variants/libbih_amd_fc.so timeout -k 10 120 python tools/fast_counters.py --frames 2 > gpurun_out/${T}_fc.log 2>&1 || exit 1
-grep bin-counters gpurun_out/${T}_fc.log | tail -1
+FC=bih-gpu-raytracer_amd/lib/variants/libbih_amd_fc.so
+if [ -f $FC ]; then
+  BIH_LIB=$FC timeout -k 10 120 python tools/fast_counters.py --frames 2 > gpurun_out/${T}_fc.log 2>&1 || exit 1
+  grep bin-counters gpurun_out/${T}_fc.log | tail -1
+fi
 timeout -k 10 300 python bench.py --traffic 0 --cpu-baseline 0 --headline-only > gpurun_out/${T}_bench.json 2>&1 || exit 1
 grep -o '"value[^,]*\|"ms_per_step[^,]*' gpurun_out/${T}_bench.json | head -2
