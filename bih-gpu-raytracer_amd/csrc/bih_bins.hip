@@ -466,10 +466,12 @@ __device__ __forceinline__ int tile_class(const float4 r0, const float4 r1, cons
                                           uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
                                           uint32_t tw, uint32_t th) {
     const double pad = 0x1p-20;
+    // x / W as x * (1 / W): off by ~1e-16, far inside the pad
+    const double iw = 1.0 / (double)w, ih = 1.0 / (double)h;
     const uint32_t xe = (bx + 1) * tw < w ? (bx + 1) * tw : w;
     const uint32_t ye = (by + 1) * th < h ? (by + 1) * th : h;
-    const double u0 = (double)(bx * tw) / w - pad, u1 = (double)xe / w + pad;
-    const double v0 = (double)(by * th) / h - pad, v1 = (double)ye / h + pad;
+    const double u0 = (double)(bx * tw) * iw - pad, u1 = (double)xe * iw + pad;
+    const double v0 = (double)(by * th) * ih - pad, v1 = (double)ye * ih + pad;
     const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
     bool all = true;
 #pragma unroll
@@ -484,19 +486,42 @@ __device__ __forceinline__ int tile_class(const float4 r0, const float4 r1, cons
     return all ? 2 : 1;
 }
 
+// A lane walks its own triangle's tile rectangle when it has at most
+// kBigRect tiles; larger rectangles (triangles close to the camera or seen
+// edge-on) are walked by the whole wave afterwards, 64 tiles at a time, so
+// one big footprint does not hold up its wave.
+constexpr uint32_t kBigRect = 32;
+template <typename F>
+__device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, uint32_t n, F &&visit) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
+    uint2 q = make_uint2(1u, 0u);
+    if (i < n) q = brect[i];
+    uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+    const bool any = i < n && bx0 <= bx1;
+    const uint32_t area = any ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0u;
+    if (any && area <= kBigRect)
+        for (uint32_t by = by0; by <= by1; ++by)
+            for (uint32_t bx = bx0; bx <= bx1; ++bx) visit(i, bx, by);
+    unsigned long long big = __ballot(area > kBigRect);
+    while (big) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(big);
+        big &= big - 1ull;
+        const uint32_t t = __builtin_amdgcn_readlane(i, j);
+        const uint2 r = brect[t];
+        const uint32_t x0 = r.x & 0xffffu, x1 = r.x >> 16, y0 = r.y & 0xffffu, y1 = r.y >> 16;
+        const uint32_t wx = x1 - x0 + 1, na = wx * (y1 - y0 + 1);
+        for (uint32_t k = lane; k < na; k += 64u) visit(t, x0 + k % wx, y0 + k / wx);
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect, uint32_t n,
                                                         uint32_t bins_x, const float4 *__restrict__ binrec,
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
                                                         uint32_t *__restrict__ cnt) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint2 q = brect[i];
-    const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-    if (bx0 > bx1) return;
-    const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
-    for (uint32_t by = by0; by <= by1; ++by)
-        for (uint32_t bx = bx0; bx <= bx1; ++bx)
-            if (tile_class(r0, r1, r2, bx, by, w, h, tw, th)) atomicAdd(cnt + by * bins_x + bx, 1u);
+    for_rect_tiles(brect, n, [&](uint32_t i, uint32_t bx, uint32_t by) {
+        const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
+        if (tile_class(r0, r1, r2, bx, by, w, h, tw, th)) atomicAdd(cnt + by * bins_x + bx, 1u);
+    });
 }
 
 // A thread per triangle copies its 64-byte entry into each of its tiles'
@@ -512,26 +537,19 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        uint32_t *__restrict__ fill2,
                                                        const float4 *__restrict__ binrec,
                                                        float4 *__restrict__ list) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint2 q = brect[i];
-    const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-    if (bx0 > bx1) return;
-    const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2],
-                 r3 = binrec[4ull * i + 3];
-    for (uint32_t by = by0; by <= by1; ++by)
-        for (uint32_t bx = bx0; bx <= bx1; ++bx) {
-            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
-            if (!cls) continue;
-            const uint32_t b = by * bins_x + bx;
-            const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
-                                          : off[b + 1] - 1u - atomicAdd(fill2 + b, 1u);
-            float4 *o = list + 4ull * pos;
-            o[0] = r0;
-            o[1] = r1;
-            o[2] = r2;
-            o[3] = r3;
-        }
+    for_rect_tiles(brect, n, [&](uint32_t i, uint32_t bx, uint32_t by) {
+        const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
+        const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+        if (!cls) return;
+        const uint32_t b = by * bins_x + bx;
+        const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
+                                      : off[b + 1] - 1u - atomicAdd(fill2 + b, 1u);
+        float4 *o = list + 4ull * pos;
+        o[0] = r0;
+        o[1] = r1;
+        o[2] = r2;
+        o[3] = binrec[4ull * i + 3];
+    });
 }
 
 // The global list's entries (the same 64-byte records).
