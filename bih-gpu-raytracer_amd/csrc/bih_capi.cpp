@@ -671,7 +671,7 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
     a.bin_queue = tr->q_list;
     a.bin_qhdr = tr->q_hdr;
     // timing experiments (BIH_DBG bits 1-2) and the fallback test mode
-    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d) & 3u;
+    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d) & ~4u;
     if (const char *d = getenv("BIH_BINS_FORCE_FALLBACK"))
         if (d[0] == '1') a.dbg |= 4u;
     const uint32_t par = tr->q_par[slot];
@@ -942,7 +942,7 @@ int bih_sync(const bih_tree *tr, void *stream) {
 #endif
 #if BIH_FAST_COUNTERS
     if (tr->work && tr->last_slot >= 0) {
-        uint32_t c[64];
+        uint32_t c[80];
         if (hipMemcpyAsync(c, tr->work + (size_t)tr->last_slot * bih::kWorkWords, sizeof c,
                            hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess) {
@@ -960,6 +960,10 @@ int bih_sync(const bih_tree *tr, void *stream) {
                     " unverified %u packets-with-miss %u planned %u plan-disagrees %u"
                     " | cycles walk %llu verify %llu\n",
                     c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], c[39], c[38], cb[0], cb[1]);
+            const unsigned long long *ph = reinterpret_cast<const unsigned long long *>(c + 64);
+            fprintf(stderr,
+                    "bin-phases (wave cycles) queue %llu background %llu setup %llu walk %llu verify %llu"
+                    " write %llu\n", ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
         }
     }
 #endif

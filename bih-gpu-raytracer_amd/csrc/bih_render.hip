@@ -1660,6 +1660,9 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #ifndef BIH_BIN_PREFETCH
 #define BIH_BIN_PREFETCH 1
 #endif
+#ifndef BIH_REC_PREFETCH
+#define BIH_REC_PREFETCH 0   // 1: neutral to slightly slower (0.0964 vs 0.094 ms/frame)
+#endif
 __device__ __forceinline__ float lane_f(float v, uint32_t j) {
     return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), j));
 }
@@ -1678,7 +1681,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                                                       float dy, float dz, unsigned long long live,
                                                       uint32_t lane, uint32_t &cand, uint32_t &cmeta,
                                                       uint32_t &cent, uint32_t &fc_ent,
-                                                      uint32_t &fc_mt) {
+                                                      uint32_t &fc_mt, uint32_t &pf) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
     const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
@@ -1698,6 +1701,15 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
             bin_chunk_load(ents, e, end, lane, d0, d1, d2);
 #endif
             const uint32_t n = end - e < 64u ? end - e : 64u;
+#if BIH_REC_PREFETCH
+            // touch every listed triangle's intersector record now (lane j:
+            // entry j's), so that the scalar loads below hit L2 instead of
+            // each paying a miss in turn; the value is folded into pf, which
+            // the caller consumes after the walk (keeps the load alive)
+            if (e + lane < end)
+                pf ^= *reinterpret_cast<const volatile uint32_t *>(
+                    reinterpret_cast<const uint32_t *>(a.tri_prim) + 16ull * __float_as_uint(d2.y));
+#endif
             for (uint32_t j = 0; j < n && rem; ++j) {
 #if BIH_BIN_PREFETCH
                 if (j == BIH_BIN_PREFETCH_AT && e + 64u < end)
@@ -1714,7 +1726,8 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 BIH_FC(++fc_ent);
                 if (!in) continue;
                 BIH_FC(++fc_mt);
-                const sf32x16 r = prim_rec(prims, __builtin_amdgcn_readlane(__float_as_uint(d2.y), j));
+                const uint32_t ti = (a.dbg & 1024u) ? 0u : __builtin_amdgcn_readlane(__float_as_uint(d2.y), j);
+                const sf32x16 r = prim_rec(prims, ti);
                 const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
                 if (h & me) {
                     cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
@@ -1855,7 +1868,13 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 #define BIH_BINS_OCC
 #endif
 constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hits lo/hi, pad
-constexpr uint32_t kBinBatch = 16;
+#ifndef BIH_BIN_BATCH
+#define BIH_BIN_BATCH 16
+#endif
+#ifndef BIH_QUEUE_AHEAD
+#define BIH_QUEUE_AHEAD 0   // 1: slower (0.112 vs 0.095 ms/frame): waves wait on refills held by busy waves
+#endif
+constexpr uint32_t kBinBatch = BIH_BIN_BATCH;
 constexpr uint32_t kBinSlot0 = 16 * 32;   // words: heads at b * 32, fallback count at 8 * 32
 struct BinQueue {
     const uint4 *hdr;                  // per band {start, live, bg, items}
@@ -1863,12 +1882,27 @@ struct BinQueue {
     unsigned long long *slot;
     uint32_t band, left;
     uint4 hb;                          // header of the band of the item next() returned
+    unsigned long long pending;        // a position claimed ahead (claim()), lane 0
+    bool has_pending;
+
+    // Claims the slot position next() will use, so that its round trip
+    // overlaps the current item's loads (BIH_QUEUE_AHEAD).
+    __device__ void claim(uint32_t lane) {
+        pending = 0;
+        if (lane == 0) pending = atomicAdd(slot, 1ull);
+        has_pending = true;
+    }
 
     // next item: band (this->hb / band) and index within the band
     __device__ bool next(uint32_t lane, uint32_t &item) {
         for (;;) {
             unsigned long long v = 0;
-            if (lane == 0) v = atomicAdd(slot, 1ull);
+            if (has_pending) {
+                v = pending;
+                has_pending = false;
+            } else if (lane == 0) {
+                v = atomicAdd(slot, 1ull);
+            }
             const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
             const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
             if (hi == 0xFFFFFFFFu) return false;
@@ -1926,9 +1960,20 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.slot = reinterpret_cast<unsigned long long *>(a.bin_heads + kBinSlot0 + cu_key() * 32);
     q.band = xcc_id();
     q.left = 8;
+    q.has_pending = false;
     uint32_t it = 0;
+#if BIH_FAST_COUNTERS
+    // per-phase wave cycles (s_memtime), summed over waves into work[64..75]
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // queue, background, setup, walk, verify, write
+    uint64_t tq = __builtin_amdgcn_s_memtime();
+#define BIH_PH(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - tq; tq = t_; } while (0)
+#else
+#define BIH_PH(k) do { } while (0)
+#endif
     while (q.next(lane, it)) {
+        BIH_PH(0);
         const uint4 hb = q.hb;
+        if (BIH_QUEUE_AHEAD && it < hb.y) q.claim(lane);   // a live tile: claim the next item now
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
             const uint32_t k = (it - hb.y) * 64u + lane;
@@ -1947,6 +1992,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                     }
                 }
             }
+            BIH_PH(1);
             continue;
         }
         if (a.dbg & 2u) continue;
@@ -1983,14 +2029,18 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         if (tzmax < tMax) tMax = tzmax;
         const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
         unsigned long long hits = 0ull, undecided = 0ull;
+        BIH_PH(2);
         if (live && sc.U > 1 && !(a.dbg & 8u)) {
-            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0;
+            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
             const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
-                                                      cmeta, cent, fc_ent, fc_mt);
+                                                      cmeta, cent, fc_ent, fc_mt, pf);
+            if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
+            BIH_PH(3);
             const bool ok = ((found >> lane) & 1ull) &&
                             ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
             hits = __ballot(ok);
             undecided = live & found & ~hits;
+            BIH_PH(4);
 #if BIH_FAST_COUNTERS
             {   // bin counters (bih_sync prints them): candidates decided by a
                 // plan, and plans that disagree with the root-path check (0)
@@ -2034,7 +2084,14 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
             a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
+        BIH_PH(5);
     }
+#if BIH_FAST_COUNTERS
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.work + 64) + k, ph[k]);
+#endif
+#undef BIH_PH
 }
 
 // The packets k_render_bins left undecided: the undecided lanes take the
