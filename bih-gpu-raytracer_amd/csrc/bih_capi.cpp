@@ -420,9 +420,11 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // per-slot accumulators, the host-path framebuffer, the per-camera
     // records, and the per-slot tile queues, spill areas and chunk orders
     info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 +
-                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 64 +
+                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 64 + tr->q_cap +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
-                          (size_t)kSlots * 2 * tr->chunk_cap) * 4;
+                          (size_t)kSlots * 2 * tr->chunk_cap +
+                          (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
+                          (size_t)kSlots * tr->fbq_cap * 8) * 4;
     info->build_ms = tr->build_ms;
     return BIH_OK;
 }

@@ -1871,6 +1871,9 @@ constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hi
 #ifndef BIH_BIN_BATCH
 #define BIH_BIN_BATCH 16
 #endif
+#ifndef BIH_QUEUE_STATIC
+#define BIH_QUEUE_STATIC 0
+#endif
 #ifndef BIH_QUEUE_AHEAD
 #define BIH_QUEUE_AHEAD 0   // 1: slower (0.112 vs 0.095 ms/frame): waves wait on refills held by busy waves
 #endif
@@ -1962,6 +1965,12 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.left = 8;
     q.has_pending = false;
     uint32_t it = 0;
+#if BIH_QUEUE_STATIC
+    // timing experiment: items dealt round-robin over the waves (no atomics)
+    const uint32_t nwv = gridDim.x * (kThreads / 64);
+    uint32_t g_next = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    g_next = __builtin_amdgcn_readfirstlane(g_next);
+#endif
 #if BIH_FAST_COUNTERS
     // per-phase wave cycles (s_memtime), summed over waves into work[64..75]
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // queue, background, setup, walk, verify, write
@@ -1970,7 +1979,23 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
 #else
 #define BIH_PH(k) do { } while (0)
 #endif
+#if BIH_QUEUE_STATIC
+    for (;;) {
+        {
+            uint32_t g = g_next, b = 0;
+            g_next += nwv;
+            uint4 h = q.hdr[0];
+            while (b < 8u && g >= h.w) {
+                g -= h.w;
+                if (++b < 8u) h = q.hdr[b];
+            }
+            if (b >= 8u) break;
+            q.hb = h;
+            it = g;
+        }
+#else
     while (q.next(lane, it)) {
+#endif
         BIH_PH(0);
         const uint4 hb = q.hb;
         if (BIH_QUEUE_AHEAD && it < hb.y) q.claim(lane);   // a live tile: claim the next item now
