@@ -486,6 +486,43 @@ __device__ __forceinline__ int tile_class(const float4 r0, const float4 r1, cons
     return all ? 2 : 1;
 }
 
+// Pixel mask of a 4 x 4-pixel tile against a triangle's edge pre-test: bit
+// 4 * row + col is clear only when no sample of that pixel can pass all
+// three edges (tile_class's test on the pixel's own rectangle).  The list
+// walk skips an entry for a packet whose remaining lanes all sit in pixels
+// outside its mask.  Other tile shapes: all ones.
+__device__ __forceinline__ uint32_t pixel_mask(const float4 r0, const float4 r1, const float4 r2,
+                                               uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
+                                               uint32_t tw, uint32_t th) {
+    if (tw != 4u || th != 4u) return 0xFFFFu;
+    const double pad = 0x1p-20;
+    const double iw = 1.0 / (double)w, ih = 1.0 / (double)h;
+    const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    double K0[3], Ku[3], Kv[3], sl[3];
+    for (int e = 0; e < 3; ++e) {
+        K0[e] = k[3 * e];
+        Ku[e] = k[3 * e + 1];
+        Kv[e] = k[3 * e + 2];
+        sl[e] = 0x1p-22 * (fabs(K0[e]) + fabs(Ku[e]) + fabs(Kv[e]));
+    }
+    uint32_t m = 0;
+    for (uint32_t py = 0; py < 4u; ++py) {
+        const uint32_t y = by * 4u + py;
+        const double v0 = (double)y * ih - pad, v1 = (double)(y + 1u) * ih + pad;
+        for (uint32_t px = 0; px < 4u; ++px) {
+            const uint32_t x = bx * 4u + px;
+            const double u0 = (double)x * iw - pad, u1 = (double)(x + 1u) * iw + pad;
+            bool may = true;
+            for (int e = 0; e < 3 && may; ++e) {
+                const double hi = K0[e] + fmax(Ku[e] * u0, Ku[e] * u1) + fmax(Kv[e] * v0, Kv[e] * v1);
+                if (hi < -sl[e]) may = false;
+            }
+            if (may || !(K0[0] == K0[0] && K0[1] == K0[1] && K0[2] == K0[2])) m |= 1u << (4u * py + px);
+        }
+    }
+    return m;
+}
+
 // A lane walks its own triangle's tile rectangle when it has at most
 // kBigRect tiles; larger rectangles (triangles close to the camera or seen
 // edge-on) are walked by the whole wave afterwards, 64 tiles at a time, so
@@ -544,10 +581,12 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
         const uint32_t b = by * bins_x + bx;
         const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
                                       : off[b + 1] - 1u - atomicAdd(fill2 + b, 1u);
+        // the entry's word 11: plan meta (bits 0-13) | pixel mask << 16
+        const uint32_t pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
         float4 *o = list + 4ull * pos;
         o[0] = r0;
         o[1] = r1;
-        o[2] = r2;
+        o[2] = make_float4(r2.x, r2.y, r2.z, __uint_as_float((__float_as_uint(r2.w) & 0xFFFFu) | (pm << 16)));
         o[3] = binrec[4ull * i + 3];
     });
 }
@@ -561,6 +600,8 @@ __global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restri
     if (j >= *gcount) return;
     const uint32_t i = glist[j];
     for (int k = 0; k < 4; ++k) gent[4ull * j + k] = binrec[4ull * i + k];
+    const float4 r2 = binrec[4ull * i + 2];   // every pixel of every tile
+    gent[4ull * j + 2] = make_float4(r2.x, r2.y, r2.z, __uint_as_float(__float_as_uint(r2.w) | 0xFFFF0000u));
 }
 
 // Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of

@@ -942,6 +942,22 @@ int bih_sync(const bih_tree *tr, void *stream) {
         }
     }
 #endif
+#ifndef BIH_PHASES
+#define BIH_PHASES BIH_FAST_COUNTERS
+#endif
+#if BIH_PHASES && !BIH_FAST_COUNTERS
+    if (tr->work && tr->last_slot >= 0) {
+        uint32_t c[80];
+        if (hipMemcpyAsync(c, tr->work + (size_t)tr->last_slot * bih::kWorkWords, sizeof c,
+                           hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            const unsigned long long *ph = reinterpret_cast<const unsigned long long *>(c + 64);
+            fprintf(stderr,
+                    "bin-phases (wave cycles) queue %llu background %llu setup %llu walk %llu verify %llu"
+                    " write %llu\n", ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+        }
+    }
+#endif
 #if BIH_FAST_COUNTERS
     if (tr->work && tr->last_slot >= 0) {
         uint32_t c[80];

@@ -1676,6 +1676,15 @@ __device__ __forceinline__ void bin_chunk_load(const float4 *ents, uint32_t e, u
         c2 = p[2];
     }
 }
+// 16-bit mask of the pixels (4 lanes each, spp 4) that still have a lane in m
+__device__ __forceinline__ uint32_t pixels_of(unsigned long long m) {
+    m = (m | (m >> 1) | (m >> 2) | (m >> 3)) & 0x1111111111111111ull;
+    m = (m | (m >> 3)) & 0x0303030303030303ull;
+    m = (m | (m >> 6)) & 0x000F000F000F000Full;
+    m = (m | (m >> 12)) & 0x000000FF000000FFull;
+    return (uint32_t)((m | (m >> 24)) & 0xFFFFull);
+}
+template <bool PMASK>
 __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, const cprim_t *prims,
                                                       uint32_t bin, float uf, float vf, float dx,
                                                       float dy, float dz, unsigned long long live,
@@ -1687,6 +1696,10 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
     uint32_t e = off[bin], end = off[bin + 1];
     unsigned long long rem = live;
     const unsigned long long me = lane_bit(lane);
+    // spp 4: an entry whose pixel mask (word 11 >> 16, bih_bins.hip
+    // pixel_mask) misses every pixel that still has a lane is skipped
+    // before its pre-test
+    uint32_t rpix = PMASK ? pixels_of(rem) : 0xFFFFu;
     for (int part = 0; part < 2; ++part) {
 #if BIH_BIN_PREFETCH
         float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
@@ -1715,6 +1728,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 if (j == BIH_BIN_PREFETCH_AT && e + 64u < end)
                     bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
 #endif
+                if (PMASK && !((__builtin_amdgcn_readlane(__float_as_uint(d2.w), j) >> 16) & rpix)) continue;
                 const float f0 = __builtin_fmaf(lane_f(d0.z, j), vf,
                                                 __builtin_fmaf(lane_f(d0.y, j), uf, lane_f(d0.x, j)));
                 const float f1 = __builtin_fmaf(lane_f(d1.y, j), vf,
@@ -1735,6 +1749,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                     cent = ((uint32_t)part << 31) | (e + j);
                 }
                 rem &= ~h;
+                if (PMASK && h) rpix = pixels_of(rem);
             }
             e += 64u;
         }
@@ -1820,6 +1835,7 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
                                             uint32_t cent, float ix, float iy, float iz, float tMin,
                                             float tMax) {
     if (cand >> 31) return true;
+    meta &= 0xFFFFu;                   // (bits 16-31: the entry's pixel mask)
     const uint32_t n = meta & 3u;
     if (n == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
     const float4 *base = reinterpret_cast<const float4 *>((cent >> 31) ? a.bin_glist : a.bin_list);
@@ -1870,6 +1886,9 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hits lo/hi, pad
 #ifndef BIH_BIN_BATCH
 #define BIH_BIN_BATCH 16
+#endif
+#ifndef BIH_PHASES
+#define BIH_PHASES BIH_FAST_COUNTERS   // per-phase wave cycles (bih_sync prints them)
 #endif
 #ifndef BIH_QUEUE_STATIC
 #define BIH_QUEUE_STATIC 0
@@ -1971,7 +1990,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     uint32_t g_next = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     g_next = __builtin_amdgcn_readfirstlane(g_next);
 #endif
-#if BIH_FAST_COUNTERS
+#if BIH_PHASES
     // per-phase wave cycles (s_memtime), summed over waves into work[64..75]
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};   // queue, background, setup, walk, verify, write
     uint64_t tq = __builtin_amdgcn_s_memtime();
@@ -2057,7 +2076,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         BIH_PH(2);
         if (live && sc.U > 1 && !(a.dbg & 8u)) {
             uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
-            const unsigned long long found = bin_walk(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
+            const unsigned long long found = bin_walk<LOG2SPP == 2>(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
                                                       cmeta, cent, fc_ent, fc_mt, pf);
             if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
             BIH_PH(3);
@@ -2111,7 +2130,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         }
         BIH_PH(5);
     }
-#if BIH_FAST_COUNTERS
+#if BIH_PHASES
     if (lane == 0)
         for (int k = 0; k < 6; ++k)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.work + 64) + k, ph[k]);
@@ -3049,7 +3068,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev
         // left undecided (the fallback grid stays within the spill area)
         const uint32_t fb = grid < 64u ? grid : 64u;
         const uint32_t gb = bins_grid_blocks(dev);
-        if (BIH_FAST_COUNTERS) {
+        if (BIH_FAST_COUNTERS || BIH_PHASES) {
             const hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
             if (e != hipSuccess) return (int)e;
         }
