@@ -1799,6 +1799,58 @@ __device__ __forceinline__ bool path_step(uint32_t val, uint32_t meta, float ix,
 }
 // The first 24 steps are requested at once (one round trip for most
 // leaves), the last 8 only by lanes whose path is longer.
+#ifndef BIH_PATH_FLAT
+#define BIH_PATH_FLAT 1
+#endif
+#if BIH_PATH_FLAT
+// path_step without control flow: the same decisions and intervals for a
+// lane still walking (live); the compare bound and the updated end coincide
+// (left: neg ? hi : lo, right: neg ? lo : hi -- the bound compared is the
+// one the child keeps, the other becomes t)
+__device__ __forceinline__ void path_step_flat(uint32_t val, uint32_t meta, float ix, float iy, float iz,
+                                               float &lo, float &hi, bool &live, bool &ok) {
+    const bool end = (meta & 8u) != 0u;
+    const float inv = sel3(meta & 3u, ix, iy, iz);
+    const bool neg = 0.0f > inv;
+    const float t = __uint_as_float(val) * inv;
+    const bool right = (meta & 4u) != 0u;
+    const bool use_hi = neg != right;
+    const bool gt = t > (use_hi ? hi : lo);
+    const bool g = (right ? !gt : gt) != neg;
+    ok = ok || (live && end && (meta & 16u) == 0u);
+    live = live && !end && g;
+    lo = (live && use_hi) ? t : lo;
+    hi = (live && !use_hi) ? t : hi;
+}
+__device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint32_t k, float ix,
+                                            float iy, float iz, float lo, float hi) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(path + 32ull * k);
+    bool live = true, ok = false;
+    {
+        uint4 q[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) q[j] = p[j];
+#pragma unroll
+        for (int j = 0; j < 24; ++j) {
+            const uint4 w = q[j >> 1];
+            path_step_flat((j & 1) ? w.z : w.x, (j & 1) ? w.w : w.y, ix, iy, iz, lo, hi, live, ok);
+        }
+    }
+    if (__ballot(live)) {
+        uint4 q[4];
+        if (live) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] = p[12 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint4 w = q[j >> 1];
+            path_step_flat((j & 1) ? w.z : w.x, (j & 1) ? w.w : w.y, ix, iy, iz, lo, hi, live, ok);
+        }
+    }
+    return ok;
+}
+#else
 __device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint32_t k, float ix,
                                             float iy, float iz, float lo, float hi) {
     const uint4 *p = reinterpret_cast<const uint4 *>(path + 32ull * k);
@@ -1825,6 +1877,7 @@ __device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint
     }
     return false;
 }
+#endif
 
 // The candidate's verification plan (triangle_plan, bih_bins.hip): the
 // entry's leaf carries bit 31 when every decision on its root path is

@@ -295,6 +295,30 @@ def test_frames_in_flight_on_streams(nstreams, gpu, bihrt_mod, oracle_mod):
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32).reshape(h, w), ref), (k, f)
 
 
+@pytest.mark.gpu
+def test_rng_ring_long_sequence_in_flight(gpu, bihrt_mod, oracle_mod):
+    """Twenty consecutive frames on three streams cycle the XORWOW ring
+    (kSlots + 1 buffers, one advance per frame) five times; a jump back and
+    one far ahead re-seed.  Every frame equals the oracle's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(20_000, seed=5)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 96, 64
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    frames = list(range(20)) + [12, 13, 700, 701]
+    outs = [torch.zeros(h * w, dtype=torch.int32, device="cuda") for _ in frames]
+    for k, f in enumerate(frames):
+        r.render_device(outs[k].data_ptr(), f, stream=streams[k % 3].cuda_stream)
+    torch.cuda.synchronize()
+    refs = {}
+    for k, f in enumerate(frames):
+        if f not in refs:
+            refs[f] = ot.render(w, h, frame=f)[0]
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32).reshape(h, w), refs[f]), (k, f)
+
+
 def _grazing_scene(n, seed):
     """Triangles seen almost edge-on: the view ray through each triangle's
     centre meets its plane at an angle of 1e-4 .. 0.3 rad, so det of the
