@@ -573,7 +573,9 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        uint32_t *__restrict__ fill,
                                                        uint32_t *__restrict__ fill2,
                                                        const float4 *__restrict__ binrec,
+                                                       const uint32_t *__restrict__ gstat,
                                                        float4 *__restrict__ list) {
+    if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
     for_rect_tiles(brect, n, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
@@ -591,17 +593,32 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
     });
 }
 
-// The global list's entries (the same 64-byte records).
-__global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restrict__ gcount,
+// The global list's entries (the same 64-byte records); gstat as k_bin_status
+// left it (a grid over kBinGlobalMax entries: no host copy of the count).
+__global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restrict__ gstat,
                                                         const uint32_t *__restrict__ glist,
                                                         const float4 *__restrict__ binrec,
                                                         float4 *__restrict__ gent) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    if (j >= *gcount) return;
+    const uint32_t gn = *gstat;
+    if (gn == kBinsUnusable || j >= gn) return;
     const uint32_t i = glist[j];
     for (int k = 0; k < 4; ++k) gent[4ull * j + k] = binrec[4ull * i + k];
     const float4 r2 = binrec[4ull * i + 2];   // every pixel of every tile
     gent[4ull * j + 2] = make_float4(r2.x, r2.y, r2.z, __uint_as_float(__float_as_uint(r2.w) | 0xFFFF0000u));
+}
+
+// The bins' device status word (gstat = gcount + 1, RenderArgs::bin_gstat):
+// the global list length when the lists fit `cap` entries and the global list
+// kBinGlobalMax, else kBinsUnusable -- k_bin_fill then writes nothing and the
+// render hands every live packet to the exact walk (k_render_fallback).  With
+// it the lists are built without a host round trip; the host reads {gcount,
+// gstat, total} back later (bih_capi.cpp: resolve_bins) and regrows.
+__global__ void k_bin_status(const uint32_t *__restrict__ total, uint32_t *__restrict__ g, uint32_t cap) {
+    if (threadIdx.x != 0) return;
+    const uint32_t tot = *total, gc = g[0];
+    g[1] = (tot <= cap && gc <= kBinGlobalMax) ? gc : kBinsUnusable;
+    g[2] = tot;
 }
 
 // Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of
@@ -622,7 +639,8 @@ __device__ __forceinline__ uint32_t queue_bin(uint32_t t, uint32_t tiles_x, uint
 }
 // qw: [0, 272) class counts, [288, 560) class starts, [576, 848) fill
 // cursors, [896, 928) per band {start, live, background, items}
-__global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__restrict__ off, uint32_t gn,
+__global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__restrict__ off,
+                                                          const uint32_t *__restrict__ gstat,
                                                           uint32_t ntiles, uint32_t tiles_x,
                                                           uint32_t tiles_y, uint32_t row0,
                                                           uint32_t band_h, uint32_t band_step,
@@ -637,6 +655,8 @@ __global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__rest
     const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
     if (t < ntiles) {
         const uint32_t b = queue_bin(t, tiles_x, row0, band_h, band_step, th, bins_x);
+        // unusable bins: every tile live (the render hands them to the exact walk)
+        const uint32_t g = *gstat, gn = g == kBinsUnusable ? 1u : g;
         const uint32_t len = off[b + 1] - off[b] + gn;
         const uint32_t band = (uint32_t)(((uint64_t)(t / tiles_x) * kQBands) / tiles_y);
         const uint32_t k = band * kQClasses + (len ? (lpt ? (uint32_t)__clz(len) : 0u) : kQClasses - 1);
@@ -778,27 +798,35 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
     return scan_exclusive(b.cnt, b.off, nb, b.partials, b.off + nb, stream);
 }
 
-int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBuffers &b, float *list,
-                    float *gent, void *stream) {
+int launch_bin_status(const BinBuffers &b, size_t cap, void *stream) {
+    const uint32_t nb = b.bins_x * b.bins_y;
+    hipLaunchKernelGGL(k_bin_status, dim3(1), dim3(64), 0, (hipStream_t)stream, b.off + nb, b.gcount,
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
+    return (int)hipGetLastError();
+}
+
+int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *list, float *gent,
+                    void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
+    const uint32_t *gstat = b.gcount + 1;
     hipError_t e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(b.cnt2, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                            b.brect, n, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt, b.cnt2,
-                           reinterpret_cast<const float4 *>(b.binrec), reinterpret_cast<float4 *>(list));
-    if (gcount > 0)
-        hipLaunchKernelGGL(k_bin_gfill, dim3((gcount + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.gcount, b.glist, reinterpret_cast<const float4 *>(b.binrec),
+                           reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
+    if (n > 0)
+        hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           gstat, b.glist, reinterpret_cast<const float4 *>(b.binrec),
                            reinterpret_cast<float4 *>(gent));
     return (int)hipGetLastError();
 }
 
 size_t bin_queue_bytes(uint32_t ntiles) { return ((size_t)ntiles * 6 + 1024 * 4 + 255) & ~(size_t)255; }
 
-int launch_bin_queue(const uint32_t *off, uint32_t gn, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
+int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
                      uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
                      uint32_t **queue, uint32_t **qhdr, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
@@ -817,7 +845,7 @@ int launch_bin_queue(const uint32_t *off, uint32_t gn, uint32_t bins_x, uint32_t
     }();
     if (ntiles > 0) {
         const dim3 g((ntiles + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_queue_class, g, dim3(kThreads), 0, st, off, gn, ntiles, tiles_x, tiles_y, row0,
+        hipLaunchKernelGGL(k_queue_class, g, dim3(kThreads), 0, st, off, gstat, ntiles, tiles_x, tiles_y, row0,
                            band_h, band_step, th, bins_x, lpt, cls, qw);
     }
     hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(64), 0, st, qw);

@@ -44,6 +44,7 @@ struct bih_tree {
     // waits on it, so a render on another stream never reads half-written
     // records.
     hipEvent_t ev_rng = nullptr;
+    hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
     bool rng_pending = false;
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
@@ -83,7 +84,14 @@ struct bih_tree {
     bool bins_usable = false;        // built and within the limits (else the kernel skips them)
     uint32_t bins_key[3] = {0, 0, 0};
     float *bin_gent = nullptr;       // global list entries (in bins_mem)
-    uint32_t bin_gn = 0;             // global list length
+    uint32_t bin_gn = 0;             // global list length (host copy once resolved)
+    // bins built without a host round trip (build_bins): the device status
+    // word decides the render; the host learns the totals from bins_host once
+    // ev_bins has passed (resolve_bins) and regrows the list if it overflowed
+    bool bins_pending = false;
+    bool bins_regrow = false;        // the last lists overflowed: rebuild with a sized list
+    bool bins_redo = false;          // the current lists are unusable but still read by renders
+    uint32_t *bins_host = nullptr;   // pinned: {gcount, status, total}
     uint32_t bins_gen = 0;           // incremented by every bins build
     uint64_t bin_entries = 0;        // list entries over all tiles
     // the render kernel's tile queue over one launch's rows (launch_bin_queue),
@@ -239,6 +247,8 @@ int create_tree(int device, void *stream, bih_tree **out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->evd[k], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_bins, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&tr->bins_host, 4 * sizeof(uint32_t), hipHostMallocDefault);
     if (e == hipSuccess && bih::upload_rng_tables(device) != 0) e = hipErrorUnknown;
     if (e != hipSuccess) {
         delete tr;
@@ -395,6 +405,8 @@ void bih_free(bih_tree *tr) {
         if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
+    if (tr->ev_bins) (void)hipEventDestroy(tr->ev_bins);
+    if (tr->bins_host) (void)hipHostFree(tr->bins_host);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
     delete tr;
 }
@@ -594,31 +606,82 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     int le = bih::launch_bin_footprints(tr->prim, n, tr->t.hdr, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
                                         tr->t.parent, node_prim, U, bc, b, st);
     if (le) return map_hip(le);
-    uint32_t tot[2] = {0, 0};
-    hipError_t e = hipMemcpyAsync(tot, b.off + nb, 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(tot + 1, b.gcount, 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return map_hip((int)e);
-    // every packet tests the whole global list: beyond a few thousand
-    // triangles the shortcut passes are the better proof
-    if (tot[1] > 4096) return BIH_OK;
-    if (tr->bin_list_cap < (size_t)tot[0] + 1) {
-        if (tr->bin_list) (void)hipFree(tr->bin_list);
-        tr->bin_list = nullptr;
-        tr->bin_list_cap = 0;
-        const size_t cap = (size_t)tot[0] + tot[0] / 8 + 1024;
-        e = hipMalloc((void **)&tr->bin_list, cap * 64);
+    hipError_t e = hipSuccess;
+    // A list buffer from an earlier camera: build into it without a host
+    // round trip (k_bin_status tells the fill and the render whether the
+    // lists fit; resolve_bins reads the totals later).  Otherwise size the
+    // list from the counts (one synchronisation).  BIH_BINS_SYNC=1 always
+    // synchronises (A/B); BIH_BINS_CAP caps the list (tests: overflow).
+    static const bool always_sync = [] {
+        const char *v = getenv("BIH_BINS_SYNC");
+        return v && v[0] == '1';
+    }();
+    size_t cap_test = 0;
+    if (const char *v = getenv("BIH_BINS_CAP")) cap_test = (size_t)strtoull(v, nullptr, 10);
+    const bool speculative = tr->bin_list_cap > 0 && !always_sync && !tr->bins_regrow;
+    if (speculative) {
+        const size_t cap = cap_test ? std::min(cap_test, tr->bin_list_cap) : tr->bin_list_cap;
+        le = bih::launch_bin_status(b, cap, st);
+        if (le) return map_hip(le);
+        e = hipMemcpyAsync(tr->bins_host, b.gcount, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(tr->ev_bins, st);
         if (e != hipSuccess) return map_hip((int)e);
-        tr->bin_list_cap = cap;
+        tr->bins_pending = true;
+    } else {
+        tr->bins_pending = false;
+        uint32_t tot[2] = {0, 0};
+        e = hipMemcpyAsync(tot, b.off + nb, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(tot + 1, b.gcount, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->bins_regrow = false;
+        // every packet tests the whole global list: beyond a few thousand
+        // triangles the shortcut passes are the better proof
+        if (tot[1] > bih::kBinGlobalMax) return BIH_OK;
+        if (tr->bin_list_cap < (size_t)tot[0] + 1) {
+            if (tr->bin_list) (void)hipFree(tr->bin_list);   // st waited for every render
+            tr->bin_list = nullptr;
+            tr->bin_list_cap = 0;
+            const size_t cap = (size_t)tot[0] + tot[0] / 8 + 1024;
+            e = hipMalloc((void **)&tr->bin_list, cap * 64);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->bin_list_cap = cap;
+        }
+        le = bih::launch_bin_status(b, tr->bin_list_cap, st);
+        if (le) return map_hip(le);
+        tr->bin_gn = tot[1];
+        tr->bin_entries = tot[0];
     }
-    le = bih::launch_bin_fill(n, tot[1], bc, b, tr->bin_list, gent, st);
+    le = bih::launch_bin_fill(n, bc, b, tr->bin_list, gent, st);
     if (le) return map_hip(le);
     tr->bins = b;
     tr->bin_gent = gent;
-    tr->bin_gn = tot[1];
-    tr->bin_entries = tot[0];
     tr->bins_usable = true;
     return BIH_OK;
+}
+
+// The totals of a bins build made without a host round trip, once its
+// readback has landed (`block`: wait for it).  A global list past
+// kBinGlobalMax turns the bins off for this camera (the shortcut walk); lists
+// past the buffer make the next render rebuild them with a sized buffer.
+// Until then the device status word already kept every render exact (the
+// lists were not written; every live packet took the exact walk).
+static void resolve_bins(bih_tree *tr, bool block) {
+    if (!tr->bins_pending) return;
+    const hipError_t e = block ? hipEventSynchronize(tr->ev_bins) : hipEventQuery(tr->ev_bins);
+    if (e != hipSuccess) return;   // hipErrorNotReady: later
+    tr->bins_pending = false;
+    const uint32_t gc = tr->bins_host[0], st = tr->bins_host[1], tot = tr->bins_host[2];
+    tr->bin_gn = gc;
+    tr->bin_entries = tot;
+    if (st != bih::kBinsUnusable) return;
+    if (gc > bih::kBinGlobalMax) {
+        tr->bins_usable = false;
+    } else {
+        tr->bins_regrow = true;
+        tr->bins_valid = false;   // rebuilt by the next render (after its readers)
+        tr->bins_redo = true;
+    }
 }
 
 // The render kernel's tile queue for this launch's rows (launch_bin_queue):
@@ -652,7 +715,7 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
             if (e != hipSuccess) return map_hip((int)e);
             tr->q_cap = need;
         }
-        int le = bih::launch_bin_queue(tr->bins.off, tr->bin_gn, tr->bins.bins_x, tiles_x, ntiles, rows.row0,
+        int le = bih::launch_bin_queue(tr->bins.off, tr->bins.gcount + 1, tr->bins.bins_x, tiles_x, ntiles, rows.row0,
                                        rows.band_h, rows.band_step, th, tr->q_mem, &tr->q_list, &tr->q_hdr,
                                        st);
         if (le) return map_hip(le);
@@ -700,6 +763,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+    resolve_bins(tr, false);
     if (!tr->work) {
         tr->spill_per_slot = bih::spill_words(bih::wave_grid_blocks(tr->t.device));
         hipError_t e = hipMalloc((void **)&tr->work, kSlots * bih::kWorkWords * sizeof(uint32_t));
@@ -778,7 +842,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
         if (bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0 &&
             (!tr->bins_valid || !bins_key_ok)) {
-            if (tr->bins_valid) {
+            if (tr->bins_valid || tr->bins_redo) {
                 // rewritten in place (the records' words 13-15 too)
                 rc = wait_renders(tr, st);
                 if (rc) return rc;
@@ -787,6 +851,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             (void)bih_camera_ray_bound(cam, dmax);
             rc = build_bins(tr, cam, dmax, w, h, spp, st);
             if (rc) return rc;
+            tr->bins_redo = false;
         }
     }
     bih::RenderArgs a;
@@ -802,10 +867,9 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         a.bin_off = tr->bins.off;
         a.bin_list = tr->bin_list;
         a.bin_glist = tr->bin_gent;
-        a.bin_gcount = tr->bins.gcount;
         a.bin_path = tr->bins.path;
         a.bins_x = tr->bins.bins_x;
-        a.bin_gn = tr->bin_gn;
+        a.bin_gstat = tr->bins.gcount + 1;
         rc = prepare_bin_queue(tr, w, h, spp, rows, slot, st, a);
         if (rc) return rc;
     } else {
@@ -1023,8 +1087,12 @@ int bih_last_render_ms(const bih_tree *tr, double *ms) {
     return BIH_OK;
 }
 
-int bih_bins_get_stats(const bih_tree *tr, bih_bins_stats *out) {
-    if (!tr || !out) return BIH_ERR_INVALID;
+int bih_bins_get_stats(const bih_tree *ctr, bih_bins_stats *out) {
+    if (!ctr || !out) return BIH_ERR_INVALID;
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    resolve_bins(tr, true);
     memset(out, 0, sizeof *out);
     out->usable = tr->bins_usable && tr->bins_valid ? 1u : 0u;
     out->tiles_x = tr->bins.bins_x;

@@ -41,6 +41,8 @@ constexpr int kLdsStack = BIH_LDS_STACK;
 constexpr uint32_t kSlotStrideWords = 32;
 constexpr uint32_t kWorkWords = 64 + kSlotStrideWords * 1024 + 64;   // + histograms (counter builds)
 constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
+constexpr uint32_t kBinGlobalMax = 4096;          // longer global lists: no bins (the shortcut walk)
+constexpr uint32_t kBinsUnusable = 0xFFFFFFFFu;   // bins status: lists not built (k_bin_status)
 constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue state per set
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
@@ -86,14 +88,13 @@ struct RenderArgs {
     // frustum bins (bih_bins.hip) of this camera and image: per TW x TH tile
     // of the full image the triangles whose footprint touches it
     // (bin_list[bin_off[b] .. bin_off[b+1])), and the global list
-    // (bin_glist[0 .. *bin_gcount)); null: no bins (rows not tile-aligned)
+    // (bin_glist[0 .. *bin_gstat)); null: no bins (rows not tile-aligned)
     const uint32_t *bin_off = nullptr;
     const float *bin_list = nullptr;        // 64-byte entries (bih_bins.hip)
     const float *bin_glist = nullptr;       // global list entries
-    const uint32_t *bin_gcount = nullptr;
     const uint2 *bin_path = nullptr;        // [U][32] root path steps per leaf
     uint32_t bins_x = 0;
-    uint32_t bin_gn = 0;                    // == *bin_gcount (host copy)
+    const uint32_t *bin_gstat = nullptr;    // bins status: global list length or kBinsUnusable
     // the launch's tile queue (launch_bin_queue) and this render slot's queue
     // state (kBinSetWords, zero at launch: band heads, fallback count, per-CU
     // slots), plus the other set, which this launch zeroes for the slot's next one
@@ -124,7 +125,7 @@ struct BinBuffers {
     uint32_t *cnt = nullptr;      // [nb] counts / fill cursors (front)
     uint32_t *cnt2 = nullptr;     // [nb] fill cursors (back)
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
-    uint32_t *gcount = nullptr;   // [1] global list length
+    uint32_t *gcount = nullptr;   // [3] global list length, status (k_bin_status), list total
     uint32_t *glist = nullptr;    // [n] global list (triangles)
     uint32_t *partials = nullptr; // scan scratch
     float *binrec = nullptr;      // [n][16] list entry of each triangle
@@ -209,14 +210,18 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
                           const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
 // lists of 64-byte entries (list: per-tile, gent: the global list's)
-int launch_bin_fill(uint32_t n, uint32_t gcount, const BinCamera &c, const BinBuffers &b, float *list,
-                    float *gent, void *stream);
+// the status word gcount[1] (k_bin_status: the global list length, or
+// kBinsUnusable when the lists exceed `cap` entries or the global list
+// kBinGlobalMax) and gcount[2] = the list total; the fill and the render read it
+int launch_bin_status(const BinBuffers &b, size_t cap, void *stream);
+int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *list, float *gent,
+                    void *stream);
 // the render kernel's work queue over one launch's tiles (k_queue_*), in 8
 // bands of tile rows: per band the live tiles by descending list length,
 // then the background tiles; qhdr (device) = per band {start, live,
 // background, items}.  mem: bin_queue_bytes(ntiles)
 size_t bin_queue_bytes(uint32_t ntiles);
-int launch_bin_queue(const uint32_t *off, uint32_t gn, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
+int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
                      uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
                      uint32_t **queue, uint32_t **qhdr, void *stream);
 // exclusive scan of n u32 (bih_build.hip); *total_dev = the sum

@@ -1756,7 +1756,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
         if (!rem) break;
         ents = reinterpret_cast<const float4 *>(a.bin_glist);
         e = 0;
-        end = a.bin_gn;
+        end = *a.bin_gstat;   // the global list's length (the bins are usable here)
     }
     return live & ~rem;
 }
@@ -2127,7 +2127,9 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
         unsigned long long hits = 0ull, undecided = 0ull;
         BIH_PH(2);
-        if (live && sc.U > 1 && !(a.dbg & 8u)) {
+        // bins_ok: the lists were built (k_bin_status); else the exact walk decides
+        const bool bins_ok = *a.bin_gstat != kBinsUnusable;
+        if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
             uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
             const unsigned long long found = bin_walk<LOG2SPP == 2>(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
                                                       cmeta, cent, fc_ent, fc_mt, pf);
@@ -2164,7 +2166,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 undecided = live;
             }
         } else if (live) {
-            undecided = live;              // one leaf (U == 1): the exact walk decides
+            undecided = live;              // one leaf (U == 1) or no lists: the exact walk decides
         }
         if (undecided) {
             uint32_t r = 0;

@@ -458,3 +458,43 @@ def test_camera_change_mid_sequence_on_streams(nstreams, gpu, bihrt_mod):
         assert np.array_equal(alone[k], overlapped[k]), (k, seq[k], int((alone[k] != overlapped[k]).sum()))
     # the cameras see different images (the check has teeth)
     assert not np.array_equal(alone[0], alone[2])
+
+
+def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
+    """Camera changes build the frustum bins without a host round trip into
+    the list buffer of an earlier camera (bih_capi.cpp build_bins): when the
+    lists do not fit (BIH_BINS_CAP forces it) the device status word sends
+    every live packet to the exact walk, the host notices afterwards
+    (resolve_bins) and the next render rebuilds a sized list.  Every frame
+    equals the reference walk's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(1_000_000, seed=1)
+    w, h = 640, 360
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, w, h)
+    cams = [bihrt_mod.camera_reference(w, h), _moved_camera(bihrt_mod, w, h, 0.05, -0.03, 0.2),
+            _moved_camera(bihrt_mod, w, h, -0.3, 0.1, -0.1)]
+    # (frame, camera, forced list capacity or None, bins usable after the frame)
+    plan = [(0, 0, None, True), (1, 1, "1000", False), (2, 1, None, True), (3, 2, None, True),
+            (4, 0, "1000", False), (5, 0, None, True), (6, 1, None, True)]
+    out = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    for f, c, cap, usable in plan:
+        if cap is None:
+            monkeypatch.delenv("BIH_BINS_CAP", raising=False)
+        else:
+            monkeypatch.setenv("BIH_BINS_CAP", cap)
+        r.camera = cams[c]
+        out.fill_(-1)
+        r.render_device(out.data_ptr(), f)
+        r.sync()
+        a = out.cpu().numpy().view(np.uint32).reshape(h, w).copy()
+        st = g.bins_stats()
+        assert bool(st.usable) == usable, (f, c, cap, st.usable, st.list_entries)
+        assert st.list_entries > 1000, (f, st.list_entries)
+        out.fill_(-1)
+        r.render_device(out.data_ptr(), f, traverse=bihrt_mod.TRAVERSE_REFERENCE)
+        r.sync()
+        b = out.cpu().numpy().view(np.uint32).reshape(h, w)
+        assert np.array_equal(a, b), (f, c, cap, int((a != b).sum()))
+    monkeypatch.delenv("BIH_BINS_CAP", raising=False)
+    g.close()
