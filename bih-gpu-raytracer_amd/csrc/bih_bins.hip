@@ -495,30 +495,34 @@ __device__ __forceinline__ uint32_t pixel_mask(const float4 r0, const float4 r1,
                                                uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
                                                uint32_t tw, uint32_t th) {
     if (tw != 4u || th != 4u) return 0xFFFFu;
+    const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    // NaN coefficients never exclude a pixel
+    if (!(k[0] == k[0] && k[3] == k[3] && k[6] == k[6])) return 0xFFFFu;
     const double pad = 0x1p-20;
     const double iw = 1.0 / (double)w, ih = 1.0 / (double)h;
-    const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
-    double K0[3], Ku[3], Kv[3], sl[3];
+    // the affine edge function's largest value over pixel (px, py)'s (u, v)
+    // rectangle is K0 + cu[px] + cv[py] (the same f64 expressions, in the
+    // same order, as tile_class on the pixel's rectangle): 8 products per edge
+    // instead of 16 rectangles
+    uint32_t m = 0xFFFFu;
+#pragma unroll
     for (int e = 0; e < 3; ++e) {
-        K0[e] = k[3 * e];
-        Ku[e] = k[3 * e + 1];
-        Kv[e] = k[3 * e + 2];
-        sl[e] = 0x1p-22 * (fabs(K0[e]) + fabs(Ku[e]) + fabs(Kv[e]));
-    }
-    uint32_t m = 0;
-    for (uint32_t py = 0; py < 4u; ++py) {
-        const uint32_t y = by * 4u + py;
-        const double v0 = (double)y * ih - pad, v1 = (double)(y + 1u) * ih + pad;
-        for (uint32_t px = 0; px < 4u; ++px) {
-            const uint32_t x = bx * 4u + px;
+        const double K0 = k[3 * e], Ku = k[3 * e + 1], Kv = k[3 * e + 2];
+        const double sl = 0x1p-22 * (fabs(K0) + fabs(Ku) + fabs(Kv));
+        double cu[4], cv[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t x = bx * 4u + j, y = by * 4u + j;
             const double u0 = (double)x * iw - pad, u1 = (double)(x + 1u) * iw + pad;
-            bool may = true;
-            for (int e = 0; e < 3 && may; ++e) {
-                const double hi = K0[e] + fmax(Ku[e] * u0, Ku[e] * u1) + fmax(Kv[e] * v0, Kv[e] * v1);
-                if (hi < -sl[e]) may = false;
-            }
-            if (may || !(K0[0] == K0[0] && K0[1] == K0[1] && K0[2] == K0[2])) m |= 1u << (4u * py + px);
+            const double v0 = (double)y * ih - pad, v1 = (double)(y + 1u) * ih + pad;
+            cu[j] = fmax(Ku * u0, Ku * u1);
+            cv[j] = fmax(Kv * v0, Kv * v1);
         }
+#pragma unroll
+        for (uint32_t py = 0; py < 4u; ++py)
+#pragma unroll
+            for (uint32_t px = 0; px < 4u; ++px)
+                if (K0 + cu[px] + cv[py] < -sl) m &= ~(1u << (4u * py + px));
     }
     return m;
 }
@@ -667,17 +671,32 @@ __global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__rest
     for (uint32_t k = threadIdx.x; k < kQBands * kQClasses; k += kThreads)
         if (hist[k]) atomicAdd(qw + k, hist[k]);
 }
-__global__ void k_queue_scan(uint32_t *__restrict__ qw) {
-    if (threadIdx.x != 0) return;
-    uint32_t acc = 0;
-    for (uint32_t b = 0; b < kQBands; ++b) {
-        const uint32_t start = acc;
+__global__ void __launch_bounds__(kThreads) k_queue_scan(uint32_t *__restrict__ qw) {
+    // one block: the counts to LDS in one parallel load, band totals and
+    // starts from LDS, then each band's class starts (a serial chain of
+    // global loads took 19 us)
+    __shared__ uint32_t c[kQBands * kQClasses], bstart[kQBands + 1];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = t; k < kQBands * kQClasses; k += kThreads) c[k] = qw[k];
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < kQBands; ++b) {
+            bstart[b] = acc;
+            for (uint32_t k = 0; k < kQClasses; ++k) acc += c[b * kQClasses + k];
+        }
+        bstart[kQBands] = acc;
+    }
+    __syncthreads();
+    if (t < kQBands) {
+        const uint32_t b = t, start = bstart[b];
+        uint32_t acc = start;
         for (uint32_t k = 0; k < kQClasses; ++k) {
             qw[288 + b * kQClasses + k] = acc;
             qw[576 + b * kQClasses + k] = 0;
-            acc += qw[b * kQClasses + k];
+            acc += c[b * kQClasses + k];
         }
-        const uint32_t bg = qw[b * kQClasses + kQClasses - 1];
+        const uint32_t bg = c[b * kQClasses + kQClasses - 1];
         const uint32_t live = acc - start - bg;
         qw[896 + 4 * b] = start;
         qw[896 + 4 * b + 1] = live;
@@ -848,7 +867,7 @@ int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x
         hipLaunchKernelGGL(k_queue_class, g, dim3(kThreads), 0, st, off, gstat, ntiles, tiles_x, tiles_y, row0,
                            band_h, band_step, th, bins_x, lpt, cls, qw);
     }
-    hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(64), 0, st, qw);
+    hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(kThreads), 0, st, qw);
     if (ntiles > 0)
         hipLaunchKernelGGL(k_queue_fill, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0, st, cls,
                            ntiles, qw, q);
