@@ -7,10 +7,10 @@
 //   radix sort    stable LSD sort of (code, tri idx)    (Renderer.cpp:441-445)
 //   k_runs*       reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
 //   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710)
-//   k_fit         clip planes, bottom-up, one arrival
-//                 counter per node instead of the leaf->root atomics of
+//   k_fit         clip planes as range queries over a segment tree of the
+//                 leaf boxes instead of the leaf->root atomics of
 //                 FindClipPlanes (CUDAKernels.cu:497-549): same max/min, no
-//                 root contention
+//                 atomics
 //   k_pack        16-B render nodes + sorted {v0,e1,e2} triangles
 // Everything is integer/byte work or exact f32 compares; all arithmetic is
 // compiled with -ffp-contract=off so it matches the strict-IEEE oracle.
@@ -397,7 +397,8 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
                                                      uint8_t *__restrict__ is_leaf,
                                                      int32_t *__restrict__ axis_out,
                                                      int32_t *__restrict__ parent,
-                                                     int32_t *__restrict__ leaf_parent) {
+                                                     int32_t *__restrict__ leaf_parent,
+                                                     int2 *__restrict__ node_rng) {
     const int U = (int)hdr->n_unique;
     uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
     if (U < 2 || idx > (uint32_t)(U - 2)) return;
@@ -435,6 +436,7 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
     children[2 * idx + 1] = split + 1;
     uint32_t mn = idx < (uint32_t)other ? idx : (uint32_t)other;
     uint32_t mx = idx > (uint32_t)other ? idx : (uint32_t)other;
+    node_rng[idx] = make_int2((int32_t)mn, (int32_t)mx);   // the node's leaves (k_fit)
     uint8_t l0 = (mn == (uint32_t)split), l1 = (mx == (uint32_t)(split + 1));
     is_leaf[2 * idx] = l0;
     is_leaf[2 * idx + 1] = l1;
@@ -447,84 +449,176 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
 // k_fit: clip planes.  Reference: every leaf walks to the root doing
 // atomicMaxFloat(clip[0], leafHi[axis]) / atomicMinFloat(clip[1],
 // leafLo[axis]) (CUDAKernels.cu:511-547), i.e. clip[0] = max over the left
-// subtree's leaves, clip[1] = min over the right subtree's leaves.  Here each
-// subtree's full AABB climbs once: a child deposits its box in the parent's
-// slot with device-scope atomics, then bumps the parent's arrival counter;
-// the second arriver reads both slots (atomics, so no cross-XCD cache
-// hand-off is involved), writes the parent's clips and climbs on.  The
-// result is the same max/min, independent of arrival order.
+// subtree's leaves, clip[1] = min over the right subtree's leaves (IEEE
+// totalOrder, tkey).  A Karras node's subtree is the contiguous leaf range
+// [mn, mx] (k_karras, node_rng) with the left child [mn, split] and the right
+// [split + 1, mx], so each clip is one range query over the leaf boxes:
+//   k_seg_leaf  leaf boxes (CUDAKernels.cu:511-529) = level 0 of a segment
+//               tree of the six box components (SoA), entry i of level L =
+//               leaves [i 2^L, (i+1) 2^L) (min for lo, max for hi);
+//   k_seg_up    10 levels per launch through LDS (2 launches at 1M leaves);
+//   k_fit       per node two O(log U) queries (no atomics, no hand-offs).
+// totalOrder max/min is associative and commutative, so any grouping gives
+// the reference's result bit for bit.  (Before: boxes handed bottom-up through
+// device-scope atomics and arrival counters, three atomic round trips per
+// level on the root's chain: 0.47 ms at 1M.)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void box_put(int32_t *slot, const float lo[3], const float hi[3]) {
-    // returning atomics whose results are consumed: the wave waits for all six
-    // to be performed before the arrival counter is bumped
-    int32_t acc = 0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        acc ^= atomicExch(slot + a, __float_as_int(lo[a]));
-        acc ^= atomicExch(slot + 3 + a, __float_as_int(hi[a]));
+constexpr uint32_t kSegBlock = 1024;   // level-L entries per k_seg_up block
+constexpr int kSegSteps = 10;          // levels per k_seg_up launch (1024 = 2^10)
+constexpr uint32_t kMaxKeyBits = 0xFFFFFFFFu;   // tkey minimum: identity of tmax
+constexpr uint32_t kMinKeyBits = 0x7FFFFFFFu;   // tkey maximum: identity of tmin
+
+// entries per component: sum over levels of ceil(nn / 2^L)
+uint64_t seg_capacity(uint64_t nn) {
+    uint64_t c = 0, s = nn;
+    for (;;) {
+        c += s;
+        if (s <= 1) break;
+        s = (s + 1) / 2;
     }
-    asm volatile("" ::"v"(acc) : "memory");
+    return c;
 }
-__device__ __forceinline__ void box_get(int32_t *slot, float lo[3], float hi[3]) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = __int_as_float(atomicOr(slot + a, 0));
-        hi[a] = __int_as_float(atomicOr(slot + 3 + a, 0));
+__device__ __forceinline__ uint64_t seg_level_off(uint64_t nn, int L) {
+    uint64_t off = 0, s = nn;
+    for (int l = 0; l < L; ++l) {
+        off += s;
+        s = (s + 1) / 2;
     }
+    return off;
 }
 
-__global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
-                                                  const uint32_t *__restrict__ tri_idx,
-                                                  const float *__restrict__ lo,
-                                                  const float *__restrict__ hi,
-                                                  const int32_t *__restrict__ first,
-                                                  const uint32_t *__restrict__ cnt,
-                                                  const int32_t *__restrict__ leaf_parent,
-                                                  const int32_t *__restrict__ parent,
-                                                  const int32_t *__restrict__ children,
-                                                  const int32_t *__restrict__ axis,
-                                                  uint32_t *__restrict__ arrive, int32_t *box,
-                                                  float *__restrict__ clip) {
+__global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restrict__ hdr,
+                                                       const uint32_t *__restrict__ tri_idx,
+                                                       const float *__restrict__ lo,
+                                                       const float *__restrict__ hi,
+                                                       const int32_t *__restrict__ first,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       float *__restrict__ seg, uint64_t cap) {
     const uint32_t U = hdr->n_unique;
-    uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
     if (U < 2 || k >= U) return;
     // leaf AABB (CUDAKernels.cu:511-529)
-    int32_t f = first[k];
-    uint32_t c = cnt[k];
+    const int32_t f = first[k];
+    const uint32_t c = cnt[k];
     float blo[3], bhi[3];
-    uint32_t t0 = tri_idx[f];
+    const uint32_t t0 = tri_idx[f];
 #pragma unroll
     for (int a = 0; a < 3; ++a) { blo[a] = lo[3ull * t0 + a]; bhi[a] = hi[3ull * t0 + a]; }
     for (uint32_t i = 1; i < c; ++i) {
-        uint32_t t = tri_idx[f + i];
+        const uint32_t t = tri_idx[f + i];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             blo[a] = tmin(blo[a], lo[3ull * t + a]);
             bhi[a] = tmax(bhi[a], hi[3ull * t + a]);
         }
     }
-    int32_t prev = (int32_t)k;
-    int32_t p = leaf_parent[k];
-    while (p >= 0) {
-        // node data the second arriver needs, requested before the hand-off
-        const int32_t c0 = children[2 * p];
-        const int ax = axis[p];
-        const int32_t pp = parent[p];
-        int side = (c0 == prev) ? 0 : 1;
-        box_put(box + (size_t)p * 12 + side * 6, blo, bhi);
-        uint32_t old = atomicAdd(arrive + p, 1u);
-        if (old == 0u) return;                      // first arriver stops
-        float slo[3], shi[3];
-        box_get(box + (size_t)p * 12 + (1 - side) * 6, slo, shi);
-        const float *lhi = side ? shi : bhi;    // left child's box is the sibling's when side==1
-        const float *rlo = side ? blo : slo;
-        clip[2 * p] = tmax(-FLT_MAX, lhi[ax]);        // initial values GPUArrayManager.cpp:79-80
-        clip[2 * p + 1] = tmin(FLT_MAX, rlo[ax]);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) { blo[a] = tmin(blo[a], slo[a]); bhi[a] = tmax(bhi[a], shi[a]); }
-        prev = p;
-        p = pp;
+    for (int a = 0; a < 3; ++a) {
+        seg[a * cap + k] = blo[a];
+        seg[(3 + a) * cap + k] = bhi[a];
     }
+}
+
+// Levels L0+1 .. L0+kSegSteps from level L0: block b owns level-L0 entries
+// [b kSegBlock, (b+1) kSegBlock).  Only entries of the U valid leaves are
+// combined (a partial last entry is never read by a query).
+__global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restrict__ hdr,
+                                                     float *__restrict__ seg, uint64_t cap, uint64_t nn,
+                                                     int L0) {
+    __shared__ float v[6][kSegBlock];
+    const uint32_t U = hdr->n_unique;
+    if (U < 2) return;
+    const uint32_t tid = threadIdx.x;
+    uint64_t off = seg_level_off(nn, L0), size = nn;
+    uint64_t vsize = U;                             // valid entries of the level
+    for (int l = 0; l < L0; ++l) {
+        size = (size + 1) / 2;
+        vsize = (vsize + 1) / 2;
+    }
+    const uint64_t base = (uint64_t)blockIdx.x * kSegBlock;
+    for (uint32_t j = tid; j < kSegBlock; j += kThreads)
+        if (base + j < vsize)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) v[c][j] = seg[c * cap + off + base + j];
+    __syncthreads();
+    uint32_t cnt = kSegBlock;
+    for (int s = 1; s <= kSegSteps; ++s) {
+        if (size <= 1) break;                       // the top level is done (uniform)
+        const uint64_t pvsize = vsize;
+        off += size;
+        size = (size + 1) / 2;
+        vsize = (vsize + 1) / 2;
+        cnt >>= 1;
+        const uint64_t gb = base >> s;              // this block's first entry at level L0+s
+        float r[4][6];
+        uint32_t nj = 0;
+        for (uint32_t j = tid; j < cnt; j += kThreads, ++nj) {
+            const uint64_t g = gb + j;
+            if (g < vsize) {
+                const bool two = 2 * g + 1 < pvsize;
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    const float a = v[c][2 * j];
+                    r[nj][c] = two ? (c < 3 ? tmin(a, v[c][2 * j + 1]) : tmax(a, v[c][2 * j + 1])) : a;
+                }
+            }
+        }
+        __syncthreads();
+        nj = 0;
+        for (uint32_t j = tid; j < cnt; j += kThreads, ++nj) {
+            const uint64_t g = gb + j;
+            if (g < vsize)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    v[c][j] = r[nj][c];
+                    seg[c * cap + off + g] = r[nj][c];
+                }
+        }
+        __syncthreads();
+    }
+}
+
+// totalOrder max (HI) / min over leaves [a, b] of component c
+template <bool HI>
+__device__ __forceinline__ float seg_query(const float *__restrict__ seg, uint64_t nn, uint32_t a,
+                                           uint32_t b) {
+    float res = __uint_as_float(HI ? kMaxKeyBits : kMinKeyBits);
+    uint64_t l = a, r = (uint64_t)b + 1, off = 0, size = nn;
+    while (l < r) {
+        if (l & 1) {
+            const float x = seg[off + l];
+            res = HI ? tmax(res, x) : tmin(res, x);
+            ++l;
+        }
+        if (r & 1) {
+            --r;
+            const float x = seg[off + r];
+            res = HI ? tmax(res, x) : tmin(res, x);
+        }
+        l >>= 1;
+        r >>= 1;
+        off += size;
+        size = (size + 1) / 2;
+    }
+    return res;
+}
+
+__global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
+                                                  const int2 *__restrict__ node_rng,
+                                                  const int32_t *__restrict__ children,
+                                                  const int32_t *__restrict__ axis,
+                                                  const float *__restrict__ seg, uint64_t cap, uint64_t nn,
+                                                  float *__restrict__ clip) {
+    const uint32_t U = hdr->n_unique;
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (U < 2 || p >= U - 1) return;
+    const int2 rg = node_rng[p];
+    const uint32_t split = (uint32_t)children[2 * p];
+    const int ax = axis[p];
+    const float lhi = seg_query<true>(seg + (3 + ax) * cap, nn, (uint32_t)rg.x, split);
+    const float rlo = seg_query<false>(seg + ax * cap, nn, split + 1u, (uint32_t)rg.y);
+    clip[2 * p] = tmax(-FLT_MAX, lhi);          // initial values GPUArrayManager.cpp:79-80
+    clip[2 * p + 1] = tmin(FLT_MAX, rlo);
 }
 
 // ---------------------------------------------------------------------------
@@ -596,7 +690,7 @@ size_t scan_partials_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile 
 void free_tree_device(DeviceTree &t) {
     void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
                     t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,
-                    t.children, t.parent, t.is_leaf, t.fit_cnt, t.fit_box, t.nodes, t.tris_s,
+                    t.children, t.parent, t.is_leaf, t.fit_rng, t.fit_seg, t.nodes, t.tris_s,
                     t.hist, t.partials, t.prep_part};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -637,8 +731,8 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.children, 2 * nn, b));
         BIH_TRY(dalloc(&t.parent, nn, b));
         BIH_TRY(dalloc(&t.is_leaf, 2 * nn, b));
-        BIH_TRY(dalloc(&t.fit_cnt, nn, b));
-        BIH_TRY(dalloc(&t.fit_box, 12 * nn, b));
+        BIH_TRY(dalloc(&t.fit_rng, nn, b));
+        BIH_TRY(dalloc(&t.fit_seg, 6 * seg_capacity(nn), b));
         BIH_TRY(dalloc(&t.nodes, nn, b));
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
         BIH_TRY(dalloc(&t.hist, hist_n, b));
@@ -680,12 +774,19 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         hipLaunchKernelGGL(k_run_counts, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.first_idx,
                            t.hdr, n, t.dup_cnt, t.leaf_parent);
         BIH_TRY(hipMemsetAsync(t.parent, 0xFF, sizeof(int32_t) * nn, st));
-        BIH_TRY(hipMemsetAsync(t.fit_cnt, 0, sizeof(uint32_t) * nn, st));
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr,
-                           t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent);
-        hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.tri_lo,
-                           t.tri_hi, t.first_idx, t.dup_cnt, t.leaf_parent, t.parent, t.children,
-                           t.axis, t.fit_cnt, t.fit_box, t.clip);
+                           t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
+        const uint64_t cap = seg_capacity(nn);
+        hipLaunchKernelGGL(k_seg_leaf, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.tri_lo,
+                           t.tri_hi, t.first_idx, t.dup_cnt, t.fit_seg, cap);
+        uint64_t lsize = nn;   // capacity of level L0 (>= its valid entries)
+        for (int L0 = 0; lsize > 1; L0 += kSegSteps) {
+            hipLaunchKernelGGL(k_seg_up, dim3((uint32_t)((lsize + kSegBlock - 1) / kSegBlock)), dim3(kThreads), 0,
+                               st, t.hdr, t.fit_seg, cap, nn, L0);
+            for (int s2 = 0; s2 < kSegSteps; ++s2) lsize = (lsize + 1) / 2;
+        }
+        hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
+                           t.axis, t.fit_seg, cap, nn, t.clip);
         hipLaunchKernelGGL(k_pack_nodes, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.clip,
                            t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
         hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.v, t.vals, n,

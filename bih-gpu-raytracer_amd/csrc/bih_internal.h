@@ -150,8 +150,8 @@ struct DeviceTree {
     float *clip = nullptr;
     int32_t *axis = nullptr, *children = nullptr, *parent = nullptr;
     uint8_t *is_leaf = nullptr;
-    uint32_t *fit_cnt = nullptr;                    // u32[U-1] arrival counters
-    int32_t *fit_box = nullptr;                     // i32[U-1][2][6] child boxes
+    int2 *fit_rng = nullptr;                        // [U-1] leaf range of each node (k_karras)
+    float *fit_seg = nullptr;                       // [6][seg_capacity] leaf-box segment tree (k_fit)
     uint4 *nodes = nullptr;
     float *tris_s = nullptr;
     uint32_t *hist = nullptr;                       // radix histograms
