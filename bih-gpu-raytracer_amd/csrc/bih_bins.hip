@@ -293,6 +293,54 @@ __device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint
     }
 }
 
+// The triangles a primary ray from the camera can hit (alive: 0 < tnum <
+// inf; about half of a soup, the other half faces away), compacted in
+// Morton order: k_bin_fp, k_bin_count and k_bin_fill run over this list, so
+// their waves are not half idle.  Per-block counts (k_bin_alive_count), an
+// exclusive scan, then the writes (k_bin_compact): one atomic per wave on a
+// single counter cost 0.18 ms (the head-word limit of k_render_bins' queue).
+// A dead triangle gets the empty footprint here.
+__device__ __forceinline__ uint32_t block_alive(const float *prim, uint32_t n, uint32_t *s_w,
+                                                unsigned long long &m, uint32_t &wave_off) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const bool al = i < n && alive(prim, i);
+    m = __ballot(al);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t tot = 0;
+    wave_off = 0;
+    for (uint32_t k = 0; k < kThreads / 64; ++k) {
+        if (k == w) wave_off = tot;
+        tot += s_w[k];
+    }
+    return tot;
+}
+__global__ void __launch_bounds__(kThreads) k_bin_alive_count(float *__restrict__ prim, uint32_t n,
+                                                              uint2 *__restrict__ brect,
+                                                              uint32_t *__restrict__ bcnt) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n && !alive(prim, i)) {
+        brect[i] = make_uint2(1u, 0u);
+        prim[16ull * i + 14] = __uint_as_float(1u);   // empty pixel range
+        prim[16ull * i + 15] = __uint_as_float(1u);
+    }
+    unsigned long long m;
+    uint32_t wo;
+    const uint32_t tot = block_alive(prim, n, s_w, m, wo);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(kThreads) k_bin_compact(const float *__restrict__ prim, uint32_t n,
+                                                          const uint32_t *__restrict__ boff,
+                                                          uint32_t *__restrict__ live) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
+    unsigned long long m;
+    uint32_t wo;
+    (void)block_alive(prim, n, s_w, m, wo);
+    if ((m >> lane) & 1ull) live[boff[blockIdx.x] + wo + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+}
+
 // Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
 // by0 | by1 << 16; empty = bx0 > bx1), the pixel rectangle in r[14..15] and
 // its list entry binrec[i]; the global list takes the rest.
@@ -304,9 +352,12 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
                                                      uint2 *__restrict__ path, uint2 *__restrict__ brect,
                                                      float *__restrict__ binrec,
                                                      uint32_t *__restrict__ gcount,
-                                                     uint32_t *__restrict__ glist) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
+                                                     uint32_t *__restrict__ glist,
+                                                     const uint32_t *__restrict__ live,
+                                                     const uint32_t *__restrict__ live_count) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= *live_count) return;
+    const uint32_t i = live[j];   // k_bin_compact
     float *r = prim + 16ull * i;
     const uint2 none = make_uint2(1u, 0u);
     if (!alive(prim, i)) {
@@ -532,13 +583,20 @@ __device__ __forceinline__ uint32_t pixel_mask(const float4 r0, const float4 r1,
 // edge-on) are walked by the whole wave afterwards, 64 tiles at a time, so
 // one big footprint does not hold up its wave.
 constexpr uint32_t kBigRect = 32;
+// Lane j takes the j-th alive triangle (k_bin_compact's list).
 template <typename F>
-__device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, uint32_t n, F &&visit) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
+__device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, const uint32_t *__restrict__ live,
+                                               const uint32_t *__restrict__ live_count, F &&visit) {
+    const uint32_t j0 = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t nl = *live_count;
     uint2 q = make_uint2(1u, 0u);
-    if (i < n) q = brect[i];
+    uint32_t i = 0;
+    if (j0 < nl) {
+        i = live[j0];
+        q = brect[i];
+    }
     uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-    const bool any = i < n && bx0 <= bx1;
+    const bool any = j0 < nl && bx0 <= bx1;
     const uint32_t area = any ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0u;
     if (any && area <= kBigRect)
         for (uint32_t by = by0; by <= by1; ++by)
@@ -555,11 +613,13 @@ __device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, 
     }
 }
 
-__global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect, uint32_t n,
+__global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect,
+                                                        const uint32_t *__restrict__ live,
+                                                        const uint32_t *__restrict__ live_count,
                                                         uint32_t bins_x, const float4 *__restrict__ binrec,
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
                                                         uint32_t *__restrict__ cnt) {
-    for_rect_tiles(brect, n, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         if (tile_class(r0, r1, r2, bx, by, w, h, tw, th)) atomicAdd(cnt + by * bins_x + bx, 1u);
     });
@@ -570,7 +630,9 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
 // back (fill2), so a packet meets the triangles that cover its whole tile
 // first.  The order within each part follows the atomics (it can change
 // which candidate a lane verifies, never a pixel).
-__global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect, uint32_t n,
+__global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect,
+                                                       const uint32_t *__restrict__ live,
+                                                       const uint32_t *__restrict__ live_count,
                                                        uint32_t bins_x, uint32_t w, uint32_t h,
                                                        uint32_t tw, uint32_t th,
                                                        const uint32_t *__restrict__ off,
@@ -580,7 +642,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        const uint32_t *__restrict__ gstat,
                                                        float4 *__restrict__ list) {
     if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
-    for_rect_tiles(brect, n, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
         if (!cls) return;
@@ -795,7 +857,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
-    hipError_t e = hipMemsetAsync(b.gcount, 0, sizeof(uint32_t), st);
+    // gcount[0] = global list length, gcount[3] = alive triangles (k_bin_compact)
+    hipError_t e = hipMemsetAsync(b.gcount, 0, 4 * sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (U > 0) {
@@ -805,10 +868,14 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
     }
     if (n > 0) {
         const dim3 g((n + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_bin_alive_count, g, dim3(kThreads), 0, st, prim, n, b.brect, b.bcnt);
+        e = (hipError_t)scan_exclusive(b.bcnt, b.boff, g.x, b.bpart, b.gcount + 3, stream);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_bin_compact, g, dim3(kThreads), 0, st, prim, n, b.boff, b.live);
         hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, leaf_parent,
                            parent, b.path, b.brect, b.binrec, b.gcount,
-                           b.glist);
-        hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, n, b.bins_x,
+                           b.glist, b.live, b.gcount + 3);
+        hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt);
     }
     e = hipGetLastError();
@@ -834,7 +901,7 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
     if (e != hipSuccess) return (int)e;
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, n, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt, b.cnt2,
+                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt, b.cnt2,
                            reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
     if (n > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,

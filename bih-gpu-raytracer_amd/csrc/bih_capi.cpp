@@ -387,6 +387,8 @@ void bih_free(bih_tree *tr) {
     if (tr->stream) (void)hipStreamSynchronize(tr->stream);
     for (int k = 0; k < kSlots; ++k)
         if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
+    // a bins readback into bins_host may still be in flight (a failed render)
+    if (tr->bins_pending) (void)hipEventSynchronize(tr->ev_bins);
     bih::free_tree_device(tr->t);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
@@ -579,8 +581,12 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
                  s_g = al(4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
-                 s_gent = al((size_t)4097 * 64);
-    const size_t need = s_brect + s_cnt + s_cnt2 + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent;
+                 s_gent = al((size_t)4097 * 64), s_live = al((size_t)n * 4 + 4);
+    const uint32_t nblk = (n + 255) / 256;   // k_bin_compact blocks (bih::kThreads)
+    const size_t s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
+                 s_bpart = al(bih::scan_partials_words(nblk) * 4);
+    const size_t need = s_brect + s_cnt + s_cnt2 + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
+                        s_live + s_bcnt + s_boff + s_bpart;
     if (tr->bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -601,7 +607,11 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.partials = reinterpret_cast<uint32_t *>(p); p += s_part;
     b.binrec = reinterpret_cast<float *>(p); p += s_rec;
     b.path = reinterpret_cast<uint2 *>(p); p += s_path;
-    float *gent = reinterpret_cast<float *>(p);
+    float *gent = reinterpret_cast<float *>(p); p += s_gent;
+    b.live = reinterpret_cast<uint32_t *>(p); p += s_live;
+    b.bcnt = reinterpret_cast<uint32_t *>(p); p += s_bcnt;
+    b.boff = reinterpret_cast<uint32_t *>(p); p += s_boff;
+    b.bpart = reinterpret_cast<uint32_t *>(p);
     const uint4 *node_prim = reinterpret_cast<const uint4 *>(tr->prim + 16ull * n);
     int le = bih::launch_bin_footprints(tr->prim, n, tr->t.hdr, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
                                         tr->t.parent, node_prim, U, bc, b, st);

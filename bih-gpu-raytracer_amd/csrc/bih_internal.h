@@ -125,7 +125,11 @@ struct BinBuffers {
     uint32_t *cnt = nullptr;      // [nb] counts / fill cursors (front)
     uint32_t *cnt2 = nullptr;     // [nb] fill cursors (back)
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
-    uint32_t *gcount = nullptr;   // [3] global list length, status (k_bin_status), list total
+    uint32_t *gcount = nullptr;   // [4] global list length, status (k_bin_status), list total, alive count
+    uint32_t *live = nullptr;     // [n] alive triangles (k_bin_compact)
+    uint32_t *bcnt = nullptr;     // [blocks] alive triangles per k_bin_compact block
+    uint32_t *boff = nullptr;     // [blocks + 1] their exclusive scan
+    uint32_t *bpart = nullptr;    // its scan scratch
     uint32_t *glist = nullptr;    // [n] global list (triangles)
     uint32_t *partials = nullptr; // scan scratch
     float *binrec = nullptr;      // [n][16] list entry of each triangle
