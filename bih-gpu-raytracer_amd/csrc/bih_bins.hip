@@ -627,7 +627,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
 
 // A thread per triangle copies its 64-byte entry into each of its tiles'
 // lists: every-sample entries from the front (fill), the others from the
-// back (fill2), so a packet meets the triangles that cover its whole tile
+// back (fill2, the per-tile counts, counted down: no second memset), so a packet meets the triangles that cover its whole tile
 // first.  The order within each part follows the atomics (it can change
 // which candidate a lane verifies, never a pixel).
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect,
@@ -647,8 +647,10 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
         if (!cls) return;
         const uint32_t b = by * bins_x + bx;
+        // fill: front cursors (zeroed); fill2: the counts k_bin_count left,
+        // counted down (off[b] + count - 1 = off[b + 1] - 1 first)
         const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
-                                      : off[b + 1] - 1u - atomicAdd(fill2 + b, 1u);
+                                      : off[b] + atomicSub(fill2 + b, 1u) - 1u;
         // the entry's word 11: plan meta (bits 0-13) | pixel mask << 16
         const uint32_t pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
         float4 *o = list + 4ull * pos;
@@ -896,12 +898,11 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
     const uint32_t *gstat = b.gcount + 1;
-    hipError_t e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
-    if (e == hipSuccess) e = hipMemsetAsync(b.cnt2, 0, (size_t)nb * sizeof(uint32_t), st);
+    hipError_t e = hipMemsetAsync(b.cnt2, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt, b.cnt2,
+                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt2, b.cnt,
                            reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
     if (n > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,

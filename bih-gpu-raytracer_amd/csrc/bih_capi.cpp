@@ -72,6 +72,7 @@ struct bih_tree {
     size_t prim_cap = 0;             // bytes
     bool prim_valid = false;
     bool fast_valid = false;         // the BIH walk's shortcut boxes match the records
+    bool cull_valid = false;         // node_cull matches the records (launch_prim_cull)
     uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
     // frustum bins (bih_bins.hip) of the camera the records were built for,
     // for one image size and tile shape (bins_key = {w, h, spp})
@@ -848,6 +849,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
             tr->prim_valid = true;
             tr->bins_valid = false;
             tr->fast_valid = false;
+            tr->cull_valid = false;
         }
         const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
         if (bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0 &&
@@ -887,6 +889,16 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         // packets are short and the order's own launch costs more (A/B)
         rc = prepare_chunk_order(tr, w, spp, rows, slot, st, a);
         if (rc) return rc;
+    }
+    // the BIH walk kernels read the culled node records: built on first use
+    // for this camera (renders through the bins never need them)
+    if (!use_bins && bih::render_uses_prim(spp) && tr->prim && n_int > 0 && !tr->cull_valid) {
+        rc = wait_renders(tr, st);
+        if (rc) return rc;
+        const int le = bih::launch_prim_cull(tr->t.n, tr->t.nodes, tr->t.first_idx, tr->t.dup_cnt, n_int,
+                                             cam->origin, tr->prim, st);
+        if (le) return map_hip(le);
+        tr->cull_valid = true;
     }
     // the BIH walk's shortcut boxes (any-hit without bins), built on first
     // use for this camera

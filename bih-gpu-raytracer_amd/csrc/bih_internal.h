@@ -199,6 +199,9 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
                 const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
                 uint32_t m, const float origin[3], const float dmax[3], float *prim,
                 void *stream);
+// node_cull (the second set of node records above) and the alive bytes
+int launch_prim_cull(uint32_t n, const uint4 *nodes, const int32_t *first_idx, const uint32_t *dup_cnt,
+                     uint32_t m, const float origin[3], float *prim, void *stream);
 int launch_fast_boxes(const float *tris, uint32_t n, const uint4 *nodes, const int32_t *first_idx,
                       const uint32_t *dup_cnt, const int32_t *leaf_parent, const int32_t *parent,
                       uint32_t m, const float origin[3], const float dmax[3], float *prim, void *stream);

@@ -2635,6 +2635,7 @@ __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict_
     uint4 r = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
                          __float_as_uint(__uint_as_float(nd.y) - org), z, w);
     out[i] = r;
+    if (!out_cull) return;   // records only (launch_prim); the culled set follows in launch_prim_cull
     const bool aL = ((nd.z >> 29) & 1u) ? leaf_alive[split] : node_alive[split];
     const bool aR = ((nd.z >> 30) & 1u) ? leaf_alive[split + 1] : node_alive[split + 1];
     if (!aL) r.x = 0xff800000u;   // -inf
@@ -2963,6 +2964,21 @@ int launch_prim(const float *tris, uint32_t n, const uint4 *nodes, const int32_t
     if (n > 0)
         hipLaunchKernelGGL(k_tri_prim, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                            tris, n, origin[0], origin[1], origin[2], prim);
+    if (m > 0) {
+        uint4 *rec = reinterpret_cast<uint4 *>(prim + 16ull * n);
+        const dim3 gn((m + kThreads - 1) / kThreads);
+        hipLaunchKernelGGL(k_node_prim, gn, dim3(kThreads), 0, st, nodes, m, origin[0], origin[1],
+                           origin[2], nullptr, nullptr, rec, nullptr);
+    }
+    return (int)hipGetLastError();
+}
+
+// The culled node records (node_cull) for the records launch_prim wrote:
+// only the BIH walk kernels read them, so renders through the frustum bins
+// never pay for them (bih_capi.cpp builds them on first use per camera).
+int launch_prim_cull(uint32_t n, const uint4 *nodes, const int32_t *first_idx, const uint32_t *dup_cnt,
+                     uint32_t m, const float origin[3], float *prim, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
     if (m > 0) {
         uint4 *rec = reinterpret_cast<uint4 *>(prim + 16ull * n);
         uint8_t *leaf_alive = reinterpret_cast<uint8_t *>(rec + 2 * (size_t)(m + 1));
