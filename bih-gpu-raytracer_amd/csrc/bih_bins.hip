@@ -668,15 +668,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
 
 // A thread per triangle copies its 64-byte entry into each of its tiles'
 // lists: every-sample entries from the front (fill), the others from the
-// back (fill2, the per-tile counts, counted down: no second memset), so
-// a packet meets the triangles that cover its whole tile first.  As in
-// k_bin_count the block aggregates in LDS over its footprints' bounding
-// rectangle: (1) per-tile front/back counts, (2) one global reservation per
-// tile and kind (the LDS word becomes the reserved cursor), (3) each pair
-// takes its position from the LDS cursor.  Blocks with a larger rectangle
-// take positions from the global cursors directly.  The order within each
-// part follows the atomics (it can change which candidate a lane verifies,
-// never a pixel).
+// back (fill2, the per-tile counts, counted down: no second memset), so a
+// packet meets the triangles that cover its whole tile first.  The order
+// within each part follows the atomics (it can change which candidate a
+// lane verifies, never a pixel).  Positions stay per-entry global atomics:
+// taking them from per-block LDS cursors (as k_bin_count counts) made the
+// fill 0.20 -> 0.13 ms but the render 1 % slower (A/B on one box,
+// 0.0938 vs 0.0929 ms/frame): the block-grouped list order costs more per
+// frame than it saves per camera.
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect,
                                                        const uint32_t *__restrict__ live,
                                                        const uint32_t *__restrict__ live_count,
@@ -688,63 +687,16 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        const float4 *__restrict__ binrec,
                                                        const uint32_t *__restrict__ gstat,
                                                        float4 *__restrict__ list) {
-    if (*gstat == kBinsUnusable) return;   // the lists would not fit (grid-uniform): the render falls back
-    __shared__ uint32_t s_front[kCountLds], s_back[kCountLds];
-    __shared__ uint32_t s_rect[4];
-    const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid;
-    if (tid == 0) {
-        s_rect[0] = s_rect[2] = 0xffffu;
-        s_rect[1] = s_rect[3] = 0u;
-    }
-    __syncthreads();
-    {
-        const uint32_t nl = *live_count;
-        if (j0 < nl) {
-            const uint2 q = brect[live[j0]];
-            const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-            if (bx0 <= bx1) {
-                atomicMin(&s_rect[0], bx0);
-                atomicMax(&s_rect[1], bx1);
-                atomicMin(&s_rect[2], by0);
-                atomicMax(&s_rect[3], by1);
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t rx0 = s_rect[0], rx1 = s_rect[1], ry0 = s_rect[2], ry1 = s_rect[3];
-    const uint32_t rw = rx1 - rx0 + 1;
-    const bool use_lds = rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kCountLds;   // block-uniform
-    const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
-    if (use_lds) {
-        for (uint32_t k = tid; k < rarea; k += kThreads) s_front[k] = s_back[k] = 0u;
-        __syncthreads();
-        for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
-            const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
-            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
-            if (!cls) return;
-            atomicAdd(cls == 2 ? &s_front[(by - ry0) * rw + (bx - rx0)] : &s_back[(by - ry0) * rw + (bx - rx0)], 1u);
-        });
-        __syncthreads();
-        for (uint32_t k = tid; k < rarea; k += kThreads) {
-            const uint32_t b = (ry0 + k / rw) * bins_x + rx0 + k % rw;
-            const uint32_t cf = s_front[k], cb = s_back[k];
-            if (cf) s_front[k] = off[b] + atomicAdd(fill + b, cf);   // first front position
-            if (cb) s_back[k] = off[b] + atomicSub(fill2 + b, cb);   // one past the first back position
-        }
-        __syncthreads();
-    }
+    if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
     for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
         if (!cls) return;
-        uint32_t pos;
-        if (use_lds) {
-            const uint32_t k = (by - ry0) * rw + (bx - rx0);
-            pos = cls == 2 ? atomicAdd(&s_front[k], 1u) : atomicSub(&s_back[k], 1u) - 1u;
-        } else {
-            const uint32_t b = by * bins_x + bx;
-            pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u) : off[b] + atomicSub(fill2 + b, 1u) - 1u;
-        }
+        const uint32_t b = by * bins_x + bx;
+        // fill: front cursors (zeroed); fill2: the counts k_bin_count left,
+        // counted down (off[b] + count - 1 = off[b + 1] - 1 first)
+        const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
+                                      : off[b] + atomicSub(fill2 + b, 1u) - 1u;
         // the entry's word 11: plan meta (bits 0-13) | pixel mask << 16
         const uint32_t pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
         float4 *o = list + 4ull * pos;
