@@ -147,6 +147,19 @@ def dodecahedron(start=None, variant: int = 0) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(tris).astype(np.float32)), faces, V
 
 
+# Fan apex per face (variant 1) of the one triangulation, out of 5^12 per
+# orientation and vertex precision, whose BIH reproduces the reference's own
+# tree dump node for node (BIH1.txt:1-348; search: tests/golden/
+# make_bih1_soup.py, record: tests/golden/bih1_dodecahedron.json).
+BIH1_APEX = (1, 4, 4, 0, 3, 3, 3, 1, 3, 0, 4, 1)
+
+
+def dodecahedron_bih1() -> np.ndarray:
+    """The reference's 36-triangle dodecahedron (the mesh behind BIH1.txt),
+    recovered by exhaustive search; 36 x 9 float32."""
+    return dodecahedron(start=BIH1_APEX, variant=1)[0]
+
+
 def _dodeca_faces(V):
     """12 pentagonal faces as CCW (outward) vertex cycles."""
     d = np.linalg.norm(V[:, None] - V[None], axis=-1)

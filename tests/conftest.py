@@ -69,4 +69,37 @@ def edge_scenes():
     out["signed_zero"] = sz
     out["cornell"] = S.cornell()
     out["dodeca"] = S.dodecahedron()[0]
+    out["bih1_dodeca"] = S.dodecahedron_bih1()
     return out
+
+
+def parse_bih1_dump(path=None):
+    """The reference's tree dump (BIH1.txt:1-348): one dict per node."""
+    nodes, cur = [], None
+    for line in open(path or os.path.join(GOLDEN, "reference_BIH1.txt")):
+        line = line.strip()
+        if line.startswith("NODE"):
+            cur = {"id": int(line.split()[1])}
+            nodes.append(cur)
+        elif ":" in line and cur is not None:
+            k, v = [x.strip() for x in line.split(":", 1)]
+            cur[k] = v
+    return nodes
+
+
+def bih1_mismatches(parent, children, axis, is_leaf, clip):
+    """(node, field) pairs where a built tree differs from BIH1.txt.  All 8
+    printed fields per node; clip planes compared at the dump's printed
+    precision (std::cout default, %g with 6 significant digits, as the
+    reference's printer at src/Renderer.cpp:617-636 writes them)."""
+    bad = []
+    for n in parse_bih1_dump():
+        i = n["id"]
+        got = {"parent": str(int(parent[i])), "leftChild": str(int(children[i][0])),
+               "rightChild": str(int(children[i][1])), "axis": str(int(axis[i])),
+               "isLeftLeaf": "TRUE" if is_leaf[i][0] else "FALSE",
+               "isRightLeaf": "TRUE" if is_leaf[i][1] else "FALSE",
+               "clipPlaneLEFT": "%g" % float(clip[i][0]),
+               "clipPlaneRIGHT": "%g" % float(clip[i][1])}
+        bad += [(i, k) for k, v in got.items() if n[k] != v]
+    return bad

@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "bih-gpu-raytracer_amd"))
 
 CASES = [("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
          ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
-         ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0)]
+         ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0),
+         ("bih1_dodeca_640x480_f0.npy", "bih1_dodeca", 640, 480, 0)]
 
 
 def main():

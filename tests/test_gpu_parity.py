@@ -45,6 +45,17 @@ def test_build_matches_oracle_soup(n, seed, gpu, bihrt_mod, oracle_mod):
     _tree_equal(g.arrays(), ot)
 
 
+def test_build_equals_reference_dump(gpu, bihrt_mod):
+    """The HIP builder's tree of the recovered mesh is the reference's own
+    dump, BIH1.txt (all 35 nodes x 8 fields)."""
+    from conftest import GOLDEN, bih1_mismatches
+    tris = np.load(os.path.join(GOLDEN, "bih1_dodecahedron.npy"))
+    g = bihrt_mod.GPUArrayManager(tris)
+    a = g.arrays()
+    assert g.info().n_unique == 36
+    assert bih1_mismatches(a["parent"], a["children"], a["axis"], a["is_leaf"], a["clip"]) == []
+
+
 def test_build_torus(gpu, bihrt_mod, oracle_mod):
     tris = bihrt_mod.scenes.torus()
     _tree_equal(bihrt_mod.GPUArrayManager(tris).arrays(), oracle_mod.OracleTree(tris))
@@ -60,7 +71,7 @@ def test_rebuild_deterministic(gpu, bihrt_mod):
         assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
 
 
-@pytest.mark.parametrize("name", ["cornell", "dodeca", "clustered", "signed_zero", "one_tri",
+@pytest.mark.parametrize("name", ["cornell", "dodeca", "bih1_dodeca", "clustered", "signed_zero", "one_tri",
                                   "dup_all", "flat_z"])
 @pytest.mark.parametrize("w,h,spp", [(64, 48, 4), (37, 29, 3)])
 def test_render_matches_oracle_small(name, w, h, spp, gpu, bihrt_mod, oracle_mod):
@@ -180,7 +191,8 @@ def test_1m_1080p_properties(gpu, bihrt_mod, oracle_mod):
 @pytest.mark.parametrize("fname,scene,w,h,frame", [
     ("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
     ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
-    ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0)])
+    ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0),
+         ("bih1_dodeca_640x480_f0.npy", "bih1_dodeca", 640, 480, 0)])
 def test_render_matches_golden_fixture(fname, scene, w, h, frame, gpu, bihrt_mod):
     """The committed golden framebuffers (tests/golden/make_golden.py)."""
     from conftest import GOLDEN

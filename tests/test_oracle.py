@@ -212,13 +212,55 @@ def test_bih1_fixture_invariants():
 
 
 def test_dodecahedron_tree_has_fixture_shape(oracle_mod):
-    """Our dodecahedron (the mesh itself is not in the reference) builds a
-    tree of the dump's shape: 35 nodes, 36 leaves, every clip plane a
-    dodecahedron coordinate."""
+    """Our default dodecahedron builds a tree of the dump's shape: 35 nodes,
+    36 leaves, every clip plane a dodecahedron coordinate."""
     ot = oracle_mod.OracleTree(edge_scenes()["dodeca"])
     assert ot.U == 36 and ot.clip.shape == (35, 2)
     vals = np.unique(np.round(np.abs(ot.clip.astype(np.float64)), 6))
     assert set(vals.tolist()) <= {0.0, 0.356822, 0.57735, 0.934172}
+
+
+def test_bih1_soup_fixture_is_the_pinned_triangulation(bihrt_mod):
+    """The committed soup (tests/golden/make_bih1_soup.py --write) is the
+    variant-1 dodecahedron fanned from scenes.BIH1_APEX, bit for bit."""
+    a = np.load(os.path.join(GOLDEN, "bih1_dodecahedron.npy"))
+    b = bihrt_mod.scenes.dodecahedron_bih1()
+    assert a.dtype == np.float32 and a.shape == (36, 9)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_oracle_tree_equals_reference_dump(oracle_mod):
+    """The oracle's BIH of the recovered mesh IS the reference's own tree dump:
+    35 nodes x {parent, children, axis, leaf flags, both clip planes}.  This
+    pins Morton (Renderer.cpp:114-145), host prep (App.cpp:103-156), the
+    stable sort / run-length (Renderer.cpp:441-472), BuildTree
+    (CUDAKernels.cu:591-710) and FindClipPlanes (:497-549) to data the
+    reference itself produced."""
+    from conftest import bih1_mismatches
+    ot = oracle_mod.OracleTree(np.load(os.path.join(GOLDEN, "bih1_dodecahedron.npy")))
+    assert ot.U == 36 and ot.n == 36
+    assert bih1_mismatches(ot.parent, ot.children, ot.axis, ot.is_leaf, ot.clip) == []
+    # the search found exactly one triangulation (of 5^12 per orientation and
+    # precision); the record says so
+    import json
+    rec = json.load(open(os.path.join(GOLDEN, "bih1_dodecahedron.json")))
+    assert rec["apex"] == list(bihrt_mod_apex())
+    assert sum(r["n_matches"] for r in rec["search"]) == 3     # one per precision, variant 1
+    assert all(r["n_matches"] == 0 for r in rec["search"] if r["variant"] == 0)
+
+
+def bihrt_mod_apex():
+    from bihrt import scenes
+    return scenes.BIH1_APEX
+
+
+def test_oracle_dump_check_has_teeth(oracle_mod, bihrt_mod):
+    """Other triangulations of the same dodecahedron do not pass the check."""
+    from conftest import bih1_mismatches
+    for apex in ([0] * 12, [1, 4, 4, 0, 3, 3, 3, 1, 3, 0, 4, 2]):
+        tris = bihrt_mod.scenes.dodecahedron(start=apex, variant=1)[0]
+        ot = oracle_mod.OracleTree(tris)
+        assert bih1_mismatches(ot.parent, ot.children, ot.axis, ot.is_leaf, ot.clip) != []
 
 
 # --- XORWOW (curand_init / curand_uniform, CUDAKernels.cu:411-419,458) --------
@@ -343,7 +385,8 @@ def test_pixels_take_the_five_binary_shades(oracle_mod):
 
 GOLDEN_CASES = [("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
                 ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
-                ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0)]
+                ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0),
+         ("bih1_dodeca_640x480_f0.npy", "bih1_dodeca", 640, 480, 0)]
 
 
 @pytest.mark.parametrize("fname,scene,w,h,frame", GOLDEN_CASES)
