@@ -37,8 +37,11 @@ def test_build_matches_oracle_edge(name, gpu, bihrt_mod, oracle_mod):
     _tree_equal(g.arrays(), ot)
 
 
-@pytest.mark.parametrize("n,seed", [(1000, 11), (70_000, 1), (300_000, 2)])
+@pytest.mark.parametrize("n,seed", [(1000, 11), (70_000, 1), (300_000, 2), (1_000_000, 1),
+                                    (10_000_000, 1)])
 def test_build_matches_oracle_soup(n, seed, gpu, bihrt_mod, oracle_mod):
+    """Every canonical array bit-equal, up to SURVEY 8f-1's 10M triangles
+    (where the segment tree of k_seg_up takes 3 launches)."""
     tris = bihrt_mod.scenes.soup(n, seed=seed)
     g = bihrt_mod.GPUArrayManager(tris)
     ot = oracle_mod.OracleTree(tris)
@@ -178,9 +181,9 @@ def test_1m_1080p_properties(gpu, bihrt_mod, oracle_mod):
     b = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_REFERENCE)
     assert np.array_equal(a, b)
     ot = oracle_mod.OracleTree(tris)
-    rows = (311, 6, 97)   # 6 rows spread over the frame
-    ref, _ = ot.render(w, h, rows=rows, mode=oracle_mod.MODE_GPU_ANYHIT)
-    ys = [311 + 97 * k for k in range(6)]
+    # every 16th row (68 rows, 522k rays) against the oracle
+    ref, _ = ot.render(w, h, rows=(0, 68, 16), mode=oracle_mod.MODE_GPU_ANYHIT)
+    ys = list(range(0, h, 16))
     assert np.array_equal(a[ys], ref)
     vals = np.unique(a)
     # k of 4 samples hit -> floor((255k + 20(4-k))/4), B = 10(4-k) (CUDAKernels.cu:384-388, :420)
@@ -406,7 +409,7 @@ def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
         assert np.array_equal(a, ref[f]), (scene, "in flight", f, int((a != ref[f]).sum()))
 
 
-def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod):
+def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod, oracle_mod):
     """Config C5's scene and size on one GPU (10M-triangle soup, 3840x2160,
     4 spp): the any-hit shortcut and the exact walk agree on every pixel of
     two frames; every pixel is one of the five shades."""
@@ -415,10 +418,14 @@ def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod):
     d = torch.from_numpy(tris).cuda()
     g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
     w, h = 3840, 2160
+    ot = oracle_mod.OracleTree(tris)
     for frame in (0, 5):
         a = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_ANYHIT)
         b = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_REFERENCE)
         assert np.array_equal(a, b), (frame, int((a != b).sum()))
+        # 6 rows spread over the frame against the oracle
+        ref, _ = ot.render(w, h, frame=frame, rows=(137, 6, 353), mode=oracle_mod.MODE_GPU_ANYHIT)
+        assert np.array_equal(a[[137 + 353 * k for k in range(6)]], ref), frame
     assert set(np.unique(a).tolist()) <= {0x281414, 0x1e4e4e, 0x148989, 0x0ac4c4, 0x00ffff}
 
 
