@@ -4,13 +4,14 @@
 Workload (BASELINE.json configs[2]): 1,000,000-triangle
 random soup (splitmix64 seed 1), 1920x1080, 4 jittered primary rays per
 pixel, reference camera, cuRAND-XORWOW seed 1984.  One step = one frame
-per GPU: frames are independent units of work, so with N GPUs rank r renders
-whole frames r, r+N, r+2N, ... of the reference's frame sequence (byte-
-identical to the frames a one-GPU run renders at those indices) with no
-collective in the step -- weak scaling, value = N x rays per frame x steps /
-max-over-ranks time.  For N > 1 a second, informational leg ("strong_tiled")
-splits every frame into interleaved 8-row bands across the ranks and
-assembles it with an RCCL all-gather.  The BIH is built once before the timed
+pass.  With N GPUs (the north star's decomposition) every frame is
+cut into interleaved 8-row bands dealt round-robin to the ranks; each rank
+renders its bands with global pixel indices (so the frame is byte-identical
+to a one-GPU render) and ONE RCCL gather per frame brings the bands to rank 0,
+which lays them out in frame order (bihrt.tiling.BandGather) -- strong
+scaling, value = rays per frame x steps / max-over-ranks time.  A side leg
+renders whole frames per rank (weak scaling, no collective).  At N = 1 the
+"band_share" leg times each rank's share of an 8-GPU split on this GPU.  The BIH is built once before the timed
 region (its device time is reported as build_ms; the reference rebuilds it
 every frame, Renderer.cpp:415-503 -- the "with_rebuild" leg times that).
 
@@ -49,15 +50,22 @@ def parse():
     ap.add_argument("--in-flight", type=int, default=3,
                     help="frames in flight: consecutive frames on this many streams, so the "
                          "next frame fills the tail of the one before (1 = one frame at a time)")
-    ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
-                    help="N > 1: whole frames per rank (weak) or row bands of one frame + "
-                         "all-gather (strong) as the headline; the other runs as a side leg")
+    ap.add_argument("--mode", choices=["weak", "strong"], default="strong",
+                    help="N > 1: row bands of every frame + RCCL gather to rank 0 (strong, the "
+                         "north star's decomposition) or whole frames per rank (weak) as the "
+                         "headline; the other runs as a side leg")
+    ap.add_argument("--share-world", type=int, default=8,
+                    help="N=1: time each of the bands one of this many GPUs would render (the "
+                         "strong decomposition's per-rank work) -> projected per-GPU efficiency")
     ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on rank 0 (N=1)")
-    ap.add_argument("--cpu-row-step", type=int, default=1,
+    ap.add_argument("--cpu-row-step", type=int, default=4,
                     help="rows of frame 0 timed on all host threads (every k-th row)")
-    ap.add_argument("--cpu-serial-row-step", type=int, default=8,
-                    help="rows timed single-threaded (the reference's serial host loop)")
+    ap.add_argument("--cpu-serial-row-step", type=int, default=16,
+                    help="rows timed single-threaded (reference walk)")
+    ap.add_argument("--cpu-debug-row-step", type=int, default=1080,
+                    help="rows timed single-threaded with the reference's host debug rules "
+                         "(CPUTraverseTree visits ~40k nodes per ray at 1M triangles: one row)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", type=int, default=1,
                     help="N=1: measure HBM traffic per launch with rocprofv3 PMC passes "
@@ -101,7 +109,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import bihrt
-    from bihrt.tiling import band_rows, frame_of_step, gather_order, max_rows
+    from bihrt.tiling import BandGather, band_rows, frame_of_step, max_rows
 
     W, H, SPP = args.width, args.height, args.spp
     # explicit streams: the build and untimed work on streams[0]; frame k of a
@@ -126,9 +134,11 @@ def main():
     outs = [torch.zeros(H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
     out = outs[0]
     if world > 1:
-        gathered = [torch.zeros(world * mrows * W, dtype=torch.int32, device="cuda") for _ in range(F)]
-        order = torch.from_numpy(gather_order(H, args.band, world)).cuda()
-        frame_img = [torch.zeros(H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
+        # one gather (and receive buffer on rank 0) per frame in flight
+        gathers = [BandGather(dist, H, W, args.band, rank, world, torch.device("cuda", local))
+                   for _ in range(F)]
+        frame_img = [torch.zeros(H * W, dtype=torch.int32, device="cuda") if rank == 0 else None
+                     for _ in range(F)]
     trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 
     def plan(mode):
@@ -150,9 +160,8 @@ def main():
             if ev is not None:
                 ev[1].record(s)
             if mode == "strong" and world > 1:
-                dist.all_gather_into_tensor(gathered[j], outs[j][: mrows * W])
-                torch.index_select(gathered[j].view(world * mrows, W), 0, order,
-                                   out=frame_img[j].view(H, W))
+                # frame k's gather runs on stream j while frame k+1 renders on j+1
+                gathers[j](outs[j], frame_img[j])
 
     def sync_all():
         if dist is not None:
@@ -205,6 +214,34 @@ def main():
         serial_leg = {"value": fps5 * rays_per_frame * args.steps / el5, "unit": "rays/s",
                       "ms_per_step": 1e3 * el5 / args.steps, "kernel_ms": kms5,
                       "note": "in_flight 1: each frame starts after the previous one ends"}
+
+    # N = 1: the strong decomposition's per-rank work at --share-world GPUs.
+    # Rank q of Q renders the interleaved bands band_rows(H, B, q, Q) of every
+    # frame; each share is timed alone here (same in-flight pipelining as the
+    # headline).  Projected per-GPU efficiency = full-frame ms / (Q x slowest
+    # share ms): what the row tiling costs per GPU before the gather.
+    share_leg = None
+    Q = args.share_world
+    if world == 1 and Q > 1 and not args.headline_only:
+        full_ms = 1e3 * elapsed / args.steps
+        shares = []
+        for q in range(Q):
+            rows_q = band_rows(H, args.band, q, Q)
+            for k in range(args.warmup):
+                step("weak", rows_q, k, 7000 + k, trav)
+            sync_all()
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                step("weak", rows_q, args.warmup + k, 7000 + args.warmup + k, trav)
+            sync_all()
+            shares.append(1e3 * (time.perf_counter() - t0) / args.steps)
+        share_leg = {"world": Q, "band": args.band, "share_ms_per_step": shares,
+                     "full_frame_ms_per_step": full_ms,
+                     "projected_efficiency": full_ms / (Q * max(shares)),
+                     "note": f"each of the {Q} ranks' interleaved {args.band}-row bands rendered alone "
+                             "on this GPU, frames in flight as the headline; efficiency = full ms / "
+                             f"({Q} x slowest share ms); excludes the gather to rank 0 "
+                             f"({H * W * 4 * (Q - 1) // Q / 1e6:.1f} MB over xGMI per frame)"}
 
     # N > 1: the other decomposition, informational
     side_leg = None
@@ -294,6 +331,21 @@ def main():
     achieved = traffic["bytes_per_launch"] / (launch_ms * 1e-3) / 1e9 if traffic else None
 
     bst = arrays.bins_stats()
+    # algorithmic bytes of one k_render_bins launch:
+    # every list entry of the frame read once (48 B: 3 edge functions + pixel
+    # mask), one 64-B intersector record per packet-level intersector call,
+    # the XORWOW state (20 B) and the framebuffer word (4 B) per pixel
+    alg = None
+    bc = (traffic or {}).get("bin_counters")
+    if bc and trav == 0 and bst.usable and launch_ms:
+        pix = rows.nrows * W
+        alg_bytes = 48 * int(bst.list_entries) + 64 * bc["mt"] + 24 * pix
+        alg = {"bytes_per_launch": alg_bytes,
+               "terms": {"list_entries": int(bst.list_entries), "intersector_calls": bc["mt"],
+                         "pixels": pix, "entries_pretested": bc["entries"], "live_lanes": bc["lanes"],
+                         "live_packets": bc["packets"]},
+               "formula": "48 x list entries + 64 x intersector calls + (20 + 4) x pixels",
+               "gbs": alg_bytes / (launch_ms * 1e-3) / 1e9}
     bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
             "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
             "entry_bytes": 64,
@@ -343,6 +395,8 @@ def main():
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "achieved_source": "measured bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) / "
                                    "launch_ms" if achieved is not None else "traffic not measured",
+                "algorithmic": alg,
+                "frac_algorithmic": alg["gbs"] / HBM_PEAK_GBS if alg else None,
                 "launch_ms": launch_ms,
                 "launch_ms_source": (f"HIP events around the render kernel on its stream "
                                      f"(bih_last_render_ms), mean of {len(kms_iso)} isolated launches")
@@ -374,6 +428,7 @@ def main():
             "moving_camera": moving_leg,
             "one_in_flight": serial_leg,
             "other_decomposition": side_leg,
+            "band_share": share_leg,
         }
         if parity_rows is not None:
             res["parity_sample_rows_equal"] = parity_rows
@@ -388,7 +443,8 @@ def parallelism(mode, band, world):
         return "1 GPU, whole frames"
     if mode == "weak":
         return f"whole frames round-robin over {world} GPUs (rank r: frames r, r+{world}, ...), no collective"
-    return f"row bands of {band} rows interleaved over {world} GPUs + RCCL all_gather"
+    return (f"row bands of {band} rows interleaved over {world} GPUs + one RCCL gather of the bands "
+            "to rank 0 per frame")
 
 
 def cpu_model():
@@ -401,42 +457,68 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_threads(args):
+    """Host threads for the OpenMP legs: every CPU this process may run on
+    (sched_getaffinity), unless OMP_NUM_THREADS names the box's CPU share
+    (the GPU pool sets it to 16 per GPU) or --cpu-threads overrides."""
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = args.cpu_threads or (min(aff, omp) if omp > 0 else aff)
+    return n, aff, omp
+
+
 def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
-    """The oracle (strict-IEEE C restatement of the reference's render path)
-    timed on the host: (i) OpenMP over the box's CPU share on every
-    --cpu-row-step-th row of frame 0 (the reported value), (ii) one thread on
-    every --cpu-serial-row-step-th row (the reference's serial host loop,
-    Renderer.cpp:374-412).  Also checks those rows of the GPU frame
-    bit-exactly."""
+    """The oracle (strict-IEEE C restatement of the reference's render path,
+    oracle/bih_oracle.c) timed on the host, on bounded row samples of frame 0
+    of the same workload:
+      value   -- the reference walk (TraverseTree, CUDAKernels.cu:227-368,
+                 MODE_GPU_REF) with OpenMP over the host threads;
+      anyhit  -- the same walk stopped at the first hit (MODE_GPU_ANYHIT),
+                 OpenMP;
+      serial  -- the reference walk on one thread;
+      host_debug_serial -- the reference's own serial host loop and rules
+                 (DebugRender / CPUTraverseTree, Renderer.cpp:202-412,
+                 MODE_HOST_DEBUG), one thread: config C1's semantics.
+    Also checks those rows of the GPU frame bit-exactly (all four walks give
+    the same pixels)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
-        min(16, os.cpu_count() or 1)
+    threads, aff, omp = cpu_threads(args)
     ot = oracle.OracleTree(tris)
-    mode = oracle.MODE_GPU_ANYHIT if trav == 0 else oracle.MODE_GPU_REF
-    walk = "any-hit" if trav == 0 else "reference"
-    step = args.cpu_row_step
-    nrows = math.ceil(H / step)
-    img, st = ot.render(W, H, spp=SPP, frame=0, rows=(0, nrows, step), mode=mode, threads=threads)
-    s1 = args.cpu_serial_row_step
-    n1 = math.ceil(H / s1)
-    img1, st1 = ot.render(W, H, spp=SPP, frame=0, rows=(0, n1, s1), mode=mode, threads=1)
+    legs = {}
+    imgs = []
+
+    def leg(name, mode, step, nthreads, row0=0):
+        nrows = math.ceil((H - row0) / step)
+        img, st = ot.render(W, H, spp=SPP, frame=0, rows=(row0, nrows, step), mode=mode,
+                            threads=nthreads)
+        imgs.append((row0, step, img))
+        legs[name] = {"value": st.rays / st.render_seconds, "unit": "rays/s", "cores": st.threads,
+                      "seconds": st.render_seconds, "rays": st.rays,
+                      "sample": f"rows {row0}::{step} of frame 0 ({nrows} rows x {W} px x {SPP} spp)",
+                      "per_ray": {"nodes": st.node_visits / st.rays, "leaves": st.leaf_visits / st.rays,
+                                  "tris": st.tri_tests / st.rays}}
+
+    leg("reference_walk", oracle.MODE_GPU_REF, args.cpu_row_step, threads)
+    leg("anyhit", oracle.MODE_GPU_ANYHIT, args.cpu_row_step, threads)
+    leg("serial", oracle.MODE_GPU_REF, args.cpu_serial_row_step, 1)
+    leg("host_debug_serial", oracle.MODE_HOST_DEBUG, args.cpu_debug_row_step, 1,
+        row0=args.cpu_debug_row_step // 2)
     # GPU frame 0, untimed, same rows
     full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     r.render_device(full.data_ptr(), 0, traverse=trav, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     g = full.cpu().numpy().view(np.uint32).reshape(H, W)
-    same = bool(np.array_equal(g[0:H:step], img) and np.array_equal(g[0:H:s1], img1))
-    res = {"value": st.rays / st.render_seconds, "unit": "rays/s", "cores": st.threads,
-           "kind": "port",
-           "sample": f"every {step}th row of frame 0 ({nrows} rows x {W} px x {SPP} spp = "
-                     f"{st.rays} rays), oracle/bih_oracle.c {walk} traversal, OpenMP "
-                     f"{st.threads} threads",
-           "seconds": st.render_seconds,
-           "cpu_model": cpu_model(),
-           "serial": {"value": st1.rays / st1.render_seconds, "unit": "rays/s", "cores": 1,
-                      "sample": f"every {s1}th row of frame 0 ({st1.rays} rays), 1 thread",
-                      "seconds": st1.render_seconds}}
+    same = all(np.array_equal(g[row0:H:step], img) for row0, step, img in imgs)
+    main = legs["reference_walk"]
+    res = {"value": main["value"], "unit": "rays/s", "cores": main["cores"], "kind": "port",
+           "sample": main["sample"] + ", oracle/bih_oracle.c reference walk (TraverseTree rules), "
+                     f"OpenMP {main['cores']} threads",
+           "seconds": main["seconds"],
+           "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": aff,
+           "omp_num_threads_env": omp or None,
+           "threads_rule": "min(sched_getaffinity, OMP_NUM_THREADS) -- the box's CPU share",
+           "legs": legs}
     return res, same
 
 
@@ -487,7 +569,33 @@ def measure_traffic(args):
     fetch = 2.0 * res["FETCH_SIZE"] * 1024.0
     write = res["WRITE_SIZE"] * 1024.0
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024", "kernel": kernel_name}
+            "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024", "kernel": kernel_name,
+            "bin_counters": bin_counters(args, env)}
+
+
+FC_LIB = os.path.join(ROOT, "bih-gpu-raytracer_amd", "lib", "variants", "libbih_amd_fc.so")
+
+
+def bin_counters(args, env):
+    """Work counters of k_render_bins on this workload's frame: a child
+    process renders two frames with the BIH_FAST_COUNTERS=1 build of the same
+    sources (lib/variants/libbih_amd_fc.so, built by __graft_entry__.build)
+    and prints them (tools/fast_counters.py).  Frame 1's line is returned."""
+    import subprocess
+    if not os.path.exists(FC_LIB):
+        return None
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "fast_counters.py"), "--frames", "2",
+           "--tris", str(args.tris), "--width", str(args.width), "--height", str(args.height)]
+    try:
+        p = subprocess.run(cmd, env=dict(env, BIH_LIB=FC_LIB), capture_output=True, text=True,
+                           timeout=300)
+    except (OSError, subprocess.TimeoutExpired):
+        return None
+    lines = [l for l in p.stderr.splitlines() if l.startswith("bin-counters")]
+    if p.returncode != 0 or not lines:
+        return None
+    tok = lines[-1].split("|")[0].split()[1:]
+    return {k: int(v) for k, v in zip(tok[0::2], tok[1::2])}
 
 
 if __name__ == "__main__":

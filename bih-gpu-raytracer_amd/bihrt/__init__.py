@@ -166,6 +166,14 @@ class Renderer:
         check(load().bih_last_render_ms(self.arrays.handle, C.byref(ms)), "bih_last_render_ms")
         return ms.value
 
+    def last_render_times(self) -> tuple[float, float]:
+        """(main render kernel ms, ms of the render call's device work after it:
+        k_render_fallback for frustum-bin renders)."""
+        k, t = C.c_double(0.0), C.c_double(0.0)
+        check(load().bih_last_render_times(self.arrays.handle, C.byref(k), C.byref(t)),
+              "bih_last_render_times")
+        return k.value, t.value
+
 
 def load_obj(path: str) -> np.ndarray:
     """Wavefront OBJ -> float32 (n, 9) soup in file order (bih_scene_load_obj;

@@ -624,13 +624,16 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
                                                         const uint32_t *__restrict__ live_count,
                                                         uint32_t bins_x, const float4 *__restrict__ binrec,
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
-                                                        uint32_t *__restrict__ cnt) {
+                                                        uint32_t *__restrict__ cnt,
+                                                        unsigned long long *__restrict__ total64) {
     __shared__ uint32_t s_cnt[kCountLds];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
+    __shared__ unsigned long long s_tot;   // the block's entries (64-bit: the list total may pass 2^32)
     const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid;
     if (tid == 0) {
         s_rect[0] = s_rect[2] = 0xffffu;
         s_rect[1] = s_rect[3] = 0u;
+        s_tot = 0ull;
     }
     __syncthreads();
     {
@@ -653,17 +656,21 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
     for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0u;
     __syncthreads();
+    unsigned long long mine = 0ull;
     for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         if (!tile_class(r0, r1, r2, bx, by, w, h, tw, th)) return;
+        ++mine;
         if (use_lds) atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1u);
         else atomicAdd(cnt + by * bins_x + bx, 1u);
     });
+    if (mine) atomicAdd(&s_tot, mine);
     __syncthreads();
     for (uint32_t k = tid; k < rarea; k += kThreads) {
         const uint32_t c = s_cnt[k];
         if (c) atomicAdd(cnt + (ry0 + k / rw) * bins_x + rx0 + k % rw, c);
     }
+    if (tid == 0 && s_tot) atomicAdd(total64, s_tot);
 }
 
 // A thread per triangle copies its 64-byte entry into each of its tiles'
@@ -728,11 +735,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restri
 // render hands every live packet to the exact walk (k_render_fallback).  With
 // it the lists are built without a host round trip; the host reads {gcount,
 // gstat, total} back later (bih_capi.cpp: resolve_bins) and regrows.
-__global__ void k_bin_status(const uint32_t *__restrict__ total, uint32_t *__restrict__ g, uint32_t cap) {
+// The total is k_bin_count's 64-bit sum (g[4..5]), not the u32 scan's, so a
+// list total past 2^32 (whose u32 offsets wrapped) is unusable too.
+__global__ void k_bin_status(uint32_t *__restrict__ g, uint32_t cap) {
     if (threadIdx.x != 0) return;
-    const uint32_t tot = *total, gc = g[0];
+    const unsigned long long tot = *reinterpret_cast<const unsigned long long *>(g + 4);
+    const uint32_t gc = g[0];
     g[1] = (tot <= cap && gc <= kBinGlobalMax) ? gc : kBinsUnusable;
-    g[2] = tot;
+    g[2] = tot > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)tot;
 }
 
 // Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of
@@ -905,8 +915,9 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
                           uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
-    // gcount[0] = global list length, gcount[3] = alive triangles (k_bin_compact)
-    hipError_t e = hipMemsetAsync(b.gcount, 0, 4 * sizeof(uint32_t), st);
+    // gcount[0] = global list length, gcount[3] = alive triangles (k_bin_compact),
+    // gcount[4..5] = the list total as a 64-bit sum (k_bin_count)
+    hipError_t e = hipMemsetAsync(b.gcount, 0, 6 * sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     if (U > 0) {
@@ -924,7 +935,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
                            parent, b.path, b.brect, b.binrec, b.gcount,
                            b.glist, b.live, b.gcount + 3);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
-                           reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt);
+                           reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt,
+                           reinterpret_cast<unsigned long long *>(b.gcount + 4));
     }
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
@@ -934,7 +946,8 @@ int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const 
 
 int launch_bin_status(const BinBuffers &b, size_t cap, void *stream) {
     const uint32_t nb = b.bins_x * b.bins_y;
-    hipLaunchKernelGGL(k_bin_status, dim3(1), dim3(64), 0, (hipStream_t)stream, b.off + nb, b.gcount,
+    (void)nb;
+    hipLaunchKernelGGL(k_bin_status, dim3(1), dim3(64), 0, (hipStream_t)stream, b.gcount,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
     return (int)hipGetLastError();
 }

@@ -19,6 +19,10 @@
 #include "../../include/bih.h"
 #include "bih_internal.h"
 
+#ifndef BIH_DEBUG_KNOBS
+#define BIH_DEBUG_KNOBS 0   // 1: honour BIH_DBG (timing experiments; changes pixels)
+#endif
+
 // Up to kSlots renders through one tree may be in flight together (issued
 // on as many streams): each launch takes one of kSlots {tile queue, spill
 // area, events} in turn, and reads its frame's XORWOW state from a ring of
@@ -640,28 +644,38 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
         tr->bins_pending = true;
     } else {
         tr->bins_pending = false;
-        uint32_t tot[2] = {0, 0};
-        e = hipMemcpyAsync(tot, b.off + nb, 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(tot + 1, b.gcount, 4, hipMemcpyDeviceToHost, st);
+        uint32_t g[6] = {0, 0, 0, 0, 0, 0};   // gcount words; [4..5] = 64-bit list total
+        e = hipMemcpyAsync(g, b.gcount, sizeof g, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return map_hip((int)e);
         tr->bins_regrow = false;
+        const uint64_t total = (uint64_t)g[4] | ((uint64_t)g[5] << 32);
         // every packet tests the whole global list: beyond a few thousand
         // triangles the shortcut passes are the better proof
-        if (tot[1] > bih::kBinGlobalMax) return BIH_OK;
-        if (tr->bin_list_cap < (size_t)tot[0] + 1) {
+        if (g[0] > bih::kBinGlobalMax) return BIH_OK;
+        // lists past the u32 offsets or half the free device memory: no bins
+        // for this camera (the BIH walk with its shortcut passes renders it)
+        size_t mem_free = 0, mem_total = 0;
+        if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 0;
+        const uint64_t cap = total + total / 8 + 1024;
+        if (cap > 0xFFFFFFFFull || cap * 64 > (uint64_t)mem_free / 2 + (uint64_t)tr->bin_list_cap * 64)
+            return BIH_OK;
+        if (tr->bin_list_cap < total + 1) {
             if (tr->bin_list) (void)hipFree(tr->bin_list);   // st waited for every render
             tr->bin_list = nullptr;
             tr->bin_list_cap = 0;
-            const size_t cap = (size_t)tot[0] + tot[0] / 8 + 1024;
             e = hipMalloc((void **)&tr->bin_list, cap * 64);
-            if (e != hipSuccess) return map_hip((int)e);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();   // not sticky: this camera renders without bins
+                tr->bin_list = nullptr;
+                return BIH_OK;
+            }
             tr->bin_list_cap = cap;
         }
         le = bih::launch_bin_status(b, tr->bin_list_cap, st);
         if (le) return map_hip(le);
-        tr->bin_gn = tot[1];
-        tr->bin_entries = tot[0];
+        tr->bin_gn = g[0];
+        tr->bin_entries = total;
     }
     le = bih::launch_bin_fill(n, bc, b, tr->bin_list, gent, st);
     if (le) return map_hip(le);
@@ -746,14 +760,18 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
     a.bin_queue = tr->q_list;
     a.bin_qhdr = tr->q_hdr;
-    // timing experiments (BIH_DBG bits 1-2) and the fallback test mode
+    // timing experiments (BIH_DBG bits: skip phases or checks; they change
+    // pixels, so only a BIH_DEBUG_KNOBS=1 build reads them) and the fallback
+    // test mode (routes packets to the exact walk: same pixels)
+#if BIH_DEBUG_KNOBS
     if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d) & ~4u;
+#endif
     if (const char *d = getenv("BIH_BINS_FORCE_FALLBACK"))
         if (d[0] == '1') a.dbg |= 4u;
+    // (q_par[slot] flips once the launch that zeroes the other set is issued)
     const uint32_t par = tr->q_par[slot];
     a.bin_heads = tr->q_count + (size_t)(2 * slot + par) * bih::kBinSetWords;
     a.bin_heads_next = tr->q_count + (size_t)(2 * slot + (par ^ 1u)) * bih::kBinSetWords;
-    tr->q_par[slot] = par ^ 1u;
     return BIH_OK;
 }
 
@@ -954,6 +972,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.spill = tr->spill + (size_t)slot * tr->spill_per_slot;
     rc = bih::launch_render(a, traverse, st, tr->ev0[slot], tr->ev1[slot]);
     if (rc) return map_hip(rc);
+    if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
@@ -1106,6 +1125,21 @@ int bih_last_render_ms(const bih_tree *tr, double *ms) {
     e = hipEventElapsedTime(&f, tr->ev0[k], tr->ev1[k]);
     if (e != hipSuccess) return map_hip((int)e);
     *ms = f;
+    return BIH_OK;
+}
+
+int bih_last_render_times(const bih_tree *tr, double *kernel_ms, double *tail_ms) {
+    if (!tr || !kernel_ms || !tail_ms || tr->last_slot < 0) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    const int k = tr->last_slot;
+    hipError_t e = hipEventSynchronize(tr->evd[k]);
+    if (e != hipSuccess) return map_hip((int)e);
+    float f0 = 0.f, f1 = 0.f;
+    e = hipEventElapsedTime(&f0, tr->ev0[k], tr->ev1[k]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&f1, tr->ev1[k], tr->evd[k]);
+    if (e != hipSuccess) return map_hip((int)e);
+    *kernel_ms = f0;
+    *tail_ms = f1;
     return BIH_OK;
 }
 

@@ -169,7 +169,7 @@ void free_tree_device(DeviceTree &t);
 
 // render (bih_render.hip)
 int upload_rng_tables(int device);
-const uint32_t *rng_tables_device(int device);      // [32 seq][160][5] ++ [64 step][160][5]
+const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host() on the device
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
@@ -238,6 +238,11 @@ size_t scan_partials_words(uint32_t n);
 
 // host XORWOW helpers (xorwow_host.cpp)
 void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);
-const uint32_t *xorwow_tables_host();   // same layout as rng_tables_device
+const uint32_t *xorwow_tables_host();   // [32 seq][160][5] ++ [64 step][160][5]
+// v = M^skip v (skip draws ahead, host)
+void xorwow_skip(uint32_t v[5], uint64_t skip);
+// k_rng_init's device tables: jump bytes [4][256][160][5] ++ J by nibbles [40][16][5]
+constexpr size_t kRngInitWords = (size_t)4 * 256 * 800 + 40 * 16 * 5;
+const uint32_t *xorwow_init_tables_host();
 
 }  // namespace bih

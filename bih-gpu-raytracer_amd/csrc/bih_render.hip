@@ -13,20 +13,21 @@
 // rounded f32 reciprocal (double rounding is innocuous for division).
 //
 // Kernels
-//   k_render_tile    persistent waves; a wave takes a tile of 64/spp pixels x
-//                    spp samples (lane = one ray), walks until all 64 rays end,
-//                    combines each pixel's samples with one ballot.
-//   k_render_refill  persistent waves; a lane that finishes its ray takes the
-//                    next ray id from a global counter (wave-aggregated
-//                    atomic), so SIMD lanes stay busy; pixels are combined
-//                    with a per-pixel atomic hit counter.
-//   k_render_pixel   any spp: one lane per pixel, samples in sequence.
-// The traversal core (Walker) is shared: it makes the reference's 4-way
-// decision per node, queues the node's tested leaves (at most two) and tests
-// their triangles before fetching the next node, so the visit order and the
-// per-ray counters equal TraverseTree's.  The stack keeps its first
-// kLdsStack entries per lane in LDS ([entry][lane], conflict-free) and spills
-// deeper ones to a per-lane HBM area.
+//   k_render_bins        any-hit default: the frustum-bin list walk,
+//                        k_render_fallback finishes undecided packets.
+//   k_render_packet_asm  the exact packet walk (TRAVERSE_REFERENCE, counters,
+//                        renders without bins), hand-scheduled gfx950 asm.
+//   k_render_packet2     the same packet walk in HIP: the asm walk's cross-check
+//                        (BIH_RENDER_KERNEL=packet2, test_kernel_variants_agree).
+//   k_render_packet      the packet walk over the canonical packed nodes: scenes
+//                        past the camera-relative records' 2^26 triangles.
+//   k_render_pixel       spp not a power of two: one lane per pixel, samples in
+//                        sequence (cudaRender's own loop order).
+// k_render_pixel's traversal core (Walker) makes the reference's 4-way
+// decision per node in TraverseTree's order, so its per-ray counters equal
+// the oracle's any-hit prefix.  Its stack keeps the first kLdsStack entries
+// per lane in LDS ([entry][lane], conflict-free) and spills deeper ones to a
+// per-lane HBM area.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdlib.h>
@@ -75,25 +76,51 @@ __device__ __forceinline__ uint32_t global_row(uint32_t lr, uint32_t row0, uint3
     return row0 + (lr / band_h) * band_h * band_step + (lr % band_h);
 }
 
+// Per-pixel curand_init(seed, pixel, 0) + skip (InitRandGPU,
+// CUDAKernels.cu:450-459): a thread seeds a run of kRngRun consecutive pixels
+// of one row.  The host applied M^skip to the seed state (powers of M
+// commute); the run's first pixel jumps to its subsequence with at most 4
+// byte-table applies (J^(b << 8k)), each next pixel is one J step through the
+// nibble table in LDS.
+constexpr uint32_t kRngRun = 16;
+__device__ __forceinline__ void jump1_lds(const uint32_t *__restrict__ nib, uint32_t x[5]) {
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+#pragma unroll
+    for (int g = 0; g < 40; ++g) {
+        const uint32_t n = (x[g >> 3] >> ((g & 7) * 4)) & 15u;
+        const uint32_t *c = nib + (g * 16 + n) * 5;
+        r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
+    }
+    x[0] = r0; x[1] = r1; x[2] = r2; x[3] = r3; x[4] = r4;
+}
+
 __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rng, uint32_t w,
                                                        uint32_t row0, uint32_t nrows, uint32_t band_h,
                                                        uint32_t band_step, uint32_t s0, uint32_t s1,
                                                        uint32_t s2, uint32_t s3, uint32_t s4,
-                                                       unsigned long long skip,
                                                        const uint32_t *__restrict__ tables) {
-    const uint64_t P = (uint64_t)nrows * w;
-    uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (lp >= P) return;
-    uint32_t lr = (uint32_t)(lp / w), x = (uint32_t)(lp % w);
-    uint64_t pix = (uint64_t)global_row(lr, row0, band_h, band_step) * w + x;
+    __shared__ uint32_t s_nib[40 * 16 * 5];
+    const uint32_t *nib = tables + 4 * 256 * 800;
+    for (uint32_t k = threadIdx.x; k < 40 * 16 * 5; k += kThreads) s_nib[k] = nib[k];
+    __syncthreads();
+    const uint32_t runs = (w + kRngRun - 1) / kRngRun;
+    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= (uint64_t)nrows * runs) return;
+    const uint32_t lr = (uint32_t)(t / runs), x0 = (uint32_t)(t % runs) * kRngRun;
+    const uint64_t pix = (uint64_t)global_row(lr, row0, band_h, band_step) * w + x0;
     uint32_t v[5] = {s0, s1, s2, s3, s4};
-    const uint32_t *seq = tables, *step = tables + 32 * 800;
-    for (int k = 0; pix && k < 32; ++k, pix >>= 1)
-        if (pix & 1) gf2_apply(seq + k * 800, v);
-    for (int k = 0; skip && k < 64; ++k, skip >>= 1)
-        if (skip & 1) gf2_apply(step + k * 800, v);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) rng[(uint64_t)i * P + lp] = v[i];
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t b = (uint32_t)(pix >> (8 * k)) & 255u;
+        if (b) gf2_apply(tables + ((uint32_t)k * 256 + b) * 800, v);
+    }
+    const uint64_t P = (uint64_t)nrows * w, lp0 = (uint64_t)lr * w + x0;
+    const uint32_t n = w - x0 < kRngRun ? w - x0 : kRngRun;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (i) jump1_lds(s_nib, v);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) rng[(uint64_t)j * P + lp0 + i] = v[j];
+    }
 }
 
 // dst = every pixel's XORWOW xorshift state `steps` draws after src's (dst
@@ -428,155 +455,6 @@ __device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uin
     for (uint32_t k = 0; k <= s; ++k) {
         ru = xorwow_uniform(v, d);
         rv = xorwow_uniform(v, d);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_render_tile
-// ---------------------------------------------------------------------------
-template <bool ANYHIT, bool STATS, int LOG2SPP>
-__global__ void __launch_bounds__(kThreads) k_render_tile(const RenderArgs a) {
-    constexpr uint32_t SPP = 1u << LOG2SPP;
-    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
-    __shared__ uint32_t s_node[kLdsStack * kThreads];
-    __shared__ float s_min[kLdsStack * kThreads];
-    __shared__ float s_max[kLdsStack * kThreads];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
-                      (uint64_t)blockIdx.x * kThreads + tid};
-    const SceneU sc = load_scene(a);
-    const uint32_t tiles_x = (a.w + TW - 1) / TW;
-    const uint32_t ntiles = tiles_x * ((a.nrows + TH - 1) / TH);
-    const float fw = (float)a.w, fh = (float)a.h;
-    const uint32_t pix = lane >> LOG2SPP;
-
-    for (;;) {
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(a.work, 1u);
-        tile = __builtin_amdgcn_readfirstlane(tile);
-        if (tile >= ntiles) break;
-        uint32_t x, lr, s;
-        ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
-        const bool valid = x < a.w && lr < a.nrows;
-        const uint64_t lp = (uint64_t)lr * a.w + x;
-        float dx = 0.f, dy = 0.f, dz = 1.f;
-        if (valid) {
-            float ru = 0.f, rv = 0.f;
-            ray_jitter<SPP>(a, lp, s, ru, rv);
-            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
-            const float u = ((float)x + ru) / fw;     // :414-415
-            const float v = ((float)y + rv) / fh;
-            camera_dir(a, u, v, dx, dy, dz);
-        }
-        Walker<ANYHIT, STATS> w;
-        w.start(sc, valid, dx, dy, dz);
-        while (w.alive) w.step(sc, st);
-        if (STATS && valid) {
-            const uint64_t rid = lp * SPP + s;
-            a.ray_stats[3 * rid] = w.cnt.nodes;
-            a.ray_stats[3 * rid + 1] = w.cnt.leaves;
-            a.ray_stats[3 * rid + 2] = w.cnt.tris;
-        }
-        const unsigned long long hb = __ballot(w.hit);
-        if (valid && s == SPP - 1) {
-            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
-            a.out[lp] = pixel_from_hits(__popcll((hb >> (pix * SPP)) & m), SPP);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_render_refill
-// ---------------------------------------------------------------------------
-template <bool ANYHIT, bool STATS, int LOG2SPP>
-__global__ void __launch_bounds__(kThreads) k_render_refill(const RenderArgs a) {
-    constexpr uint32_t SPP = 1u << LOG2SPP;
-    constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
-    constexpr int kRefillMin = 16;   // refill once this many lanes are idle
-    __shared__ uint32_t s_node[kLdsStack * kThreads];
-    __shared__ float s_min[kLdsStack * kThreads];
-    __shared__ float s_max[kLdsStack * kThreads];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const Stack st = {s_node, s_min, s_max, tid, a.spill, (uint64_t)gridDim.x * kThreads,
-                      (uint64_t)blockIdx.x * kThreads + tid};
-    const SceneU sc = load_scene(a);
-    const uint32_t tiles_x = (a.w + TW - 1) / TW;
-    const uint64_t nrays = (uint64_t)tiles_x * ((a.nrows + TH - 1) / TH) * 64;
-    const float fw = (float)a.w, fh = (float)a.h;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-
-    Walker<ANYHIT, STATS> w;
-    w.alive = false;
-    w.hit = false;
-    uint64_t lp = 0;
-    uint32_t s = 0;
-    bool exhausted = false;
-    bool own = false;                  // lane holds a valid ray to finalise
-
-    auto finish = [&]() {
-        if (STATS) {
-            const uint64_t rid = lp * SPP + s;
-            a.ray_stats[3 * rid] = w.cnt.nodes;
-            a.ray_stats[3 * rid + 1] = w.cnt.leaves;
-            a.ray_stats[3 * rid + 2] = w.cnt.tris;
-        }
-        if (SPP == 1) {
-            a.out[lp] = pixel_from_hits(w.hit ? 1u : 0u, 1u);
-        } else {
-            const uint32_t old = atomicAdd(a.pixacc + lp, w.hit ? 0x10001u : 1u);
-            if ((old & 0xFFFFu) + 1u == SPP) {       // last sample of the pixel
-                a.out[lp] = pixel_from_hits((old >> 16) + (w.hit ? 1u : 0u), SPP);
-                a.pixacc[lp] = 0u;                   // ready for the next frame
-            }
-        }
-        own = false;
-    };
-
-    for (;;) {
-        // ---- refill idle lanes (wave-aggregated atomic on the ray counter)
-        while (!exhausted) {
-            const unsigned long long need = __ballot(!w.alive);
-            if (need == 0ull) break;
-            const uint32_t cnt = (uint32_t)__popcll(need);
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(a.work, cnt);
-            base = __builtin_amdgcn_readfirstlane(base);
-            if ((uint64_t)base + cnt >= nrays) exhausted = true;
-            if (!w.alive) {
-                const uint64_t rid = (uint64_t)base + __popcll(need & lt);
-                bool valid = false;
-                float dx = 0.f, dy = 0.f, dz = 1.f;
-                if (rid < nrays) {
-                    uint32_t x, lr;
-                    ray_coords<LOG2SPP>(rid, tiles_x, x, lr, s);
-                    valid = x < a.w && lr < a.nrows;
-                    if (valid) {
-                        lp = (uint64_t)lr * a.w + x;
-                        float ru = 0.f, rv = 0.f;
-                        ray_jitter<SPP>(a, lp, s, ru, rv);
-                        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
-                        const float u = ((float)x + ru) / fw;
-                        const float v = ((float)y + rv) / fh;
-                        camera_dir(a, u, v, dx, dy, dz);
-                    }
-                }
-                w.start(sc, valid, dx, dy, dz);
-                own = valid;
-                if (own && !w.alive) finish();          // slab miss: done at once
-            }
-            if (__ballot(!w.alive) == 0ull) break;
-        }
-        if (__ballot(w.alive) == 0ull) break;           // queue empty, all lanes idle
-        // ---- walk until enough lanes are idle to make a refill worthwhile
-        for (;;) {
-            if (w.alive) {
-                w.step(sc, st);
-                if (!w.alive) finish();
-            }
-            const unsigned long long idle = __ballot(!w.alive);
-            if (idle == ~0ull) break;
-            if (!exhausted && __popcll(idle) >= kRefillMin) break;
-        }
     }
 }
 
@@ -2019,10 +1897,13 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    // the slot's next launch starts from a zeroed set
-    if (tid == 0 && blockIdx.x < 1024u)
-        *reinterpret_cast<unsigned long long *>(a.bin_heads_next + kBinSlot0 + blockIdx.x * 32) = 0ull;
-    if (tid == 0 && blockIdx.x < 9u) a.bin_heads_next[blockIdx.x * 32] = 0u;
+    // the slot's next launch starts from a zeroed set: every one of the 1024
+    // per-CU slot lines (cu_key() spans 0..1023 sparsely, whatever the grid)
+    if (tid == 0)
+        for (uint32_t k = blockIdx.x; k < 1024u; k += gridDim.x)
+            *reinterpret_cast<unsigned long long *>(a.bin_heads_next + kBinSlot0 + k * 32) = 0ull;
+    if (tid == 0)
+        for (uint32_t k = blockIdx.x; k < 9u; k += gridDim.x) a.bin_heads_next[k * 32] = 0u;
     const SceneU sc = load_scene(a);
     const cprim_t *prims = (const cprim_t *)(const void *)a.tri_prim;
     const uint32_t tiles_x = (a.w + TW - 1) / TW;
@@ -2831,12 +2712,10 @@ __global__ void __launch_bounds__(kThreads) k_fast_refs(const uint4 *__restrict_
 std::mutex g_tab_mu;
 uint32_t *g_tab_dev[64] = {nullptr};
 
-enum class Variant { Tile, Refill, Packet1, Packet2, PacketAsm };
+enum class Variant { Packet1, Packet2, PacketAsm };
 
 Variant variant_from_env() {
     const char *e = getenv("BIH_RENDER_KERNEL");
-    if (e && strcmp(e, "tile") == 0) return Variant::Tile;
-    if (e && strcmp(e, "refill") == 0) return Variant::Refill;
     if (e && strcmp(e, "packet1") == 0) return Variant::Packet1;
     if (e && strcmp(e, "packet2") == 0) return Variant::Packet2;
     return Variant::PacketAsm;
@@ -2853,23 +2732,7 @@ hipError_t launch_persistent(Variant var, const RenderArgs &a, uint32_t traverse
                              uint32_t blocks) {
     const bool stats = a.ray_stats != nullptr;
     const dim3 g(blocks), b(kThreads);
-    if (var == Variant::Tile) {
-        if (traverse == 0) {
-            if (stats) hipLaunchKernelGGL((k_render_tile<true, true, L>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_render_tile<true, false, L>), g, b, 0, st, a);
-        } else {
-            if (stats) hipLaunchKernelGGL((k_render_tile<false, true, L>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_render_tile<false, false, L>), g, b, 0, st, a);
-        }
-    } else if (var == Variant::Refill) {
-        if (traverse == 0) {
-            if (stats) hipLaunchKernelGGL((k_render_refill<true, true, L>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_render_refill<true, false, L>), g, b, 0, st, a);
-        } else {
-            if (stats) hipLaunchKernelGGL((k_render_refill<false, true, L>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((k_render_refill<false, false, L>), g, b, 0, st, a);
-        }
-    } else if (var == Variant::Packet1 || !packet_records_fit(a)) {
+    if (var == Variant::Packet1 || !packet_records_fit(a)) {
         // packed canonical nodes: any scene size
         if (traverse == 0) {
             if (stats) hipLaunchKernelGGL((k_render_packet<true, true, L>), g, b, 0, st, a);
@@ -2904,11 +2767,11 @@ int upload_rng_tables(int device) {
     if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lk(g_tab_mu);
     if (g_tab_dev[device]) return 0;
-    const size_t bytes = (32 + 64) * 800 * sizeof(uint32_t);
+    const size_t bytes = kRngInitWords * sizeof(uint32_t);
     uint32_t *p = nullptr;
     hipError_t e = hipMalloc((void **)&p, bytes);
     if (e != hipSuccess) return (int)e;
-    e = hipMemcpy(p, xorwow_tables_host(), bytes, hipMemcpyHostToDevice);
+    e = hipMemcpy(p, xorwow_init_tables_host(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(p); return (int)e; }
     g_tab_dev[device] = p;
     return 0;
@@ -2925,12 +2788,12 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     if (!tab) return (int)hipErrorNotInitialized;
     uint32_t v[5], d;
     xorwow_seed(seed, v, &d);
-    const uint64_t P = (uint64_t)nrows * w;
-    if (P == 0) return 0;
-    const uint32_t blocks = (uint32_t)((P + kThreads - 1) / kThreads);
+    xorwow_skip(v, skip);   // M^skip commutes with the subsequence jumps
+    const uint64_t threads = (uint64_t)nrows * ((w + kRngRun - 1) / kRngRun);
+    if (threads == 0) return 0;
+    const uint32_t blocks = (uint32_t)((threads + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_rng_init, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, rng, w, row0,
-                       nrows, band_h, band_step, v[0], v[1], v[2], v[3], v[4],
-                       (unsigned long long)skip, tab);
+                       nrows, band_h, band_step, v[0], v[1], v[2], v[3], v[4], tab);
     return (int)hipGetLastError();
 }
 
@@ -3026,8 +2889,7 @@ int launch_fast_boxes(const float *tris, uint32_t n, const uint4 *nodes, const i
 }
 
 bool render_uses_prim(uint32_t spp) {
-    static const Variant var = variant_from_env();
-    return var != Variant::Tile && var != Variant::Refill && spp <= 64 && (spp & (spp - 1)) == 0;
+    return spp <= 64 && (spp & (spp - 1)) == 0;
 }
 
 // Resident blocks of the persistent kernels on `device` (grid size).
@@ -3040,8 +2902,6 @@ uint32_t wave_grid_blocks(int device) {
         // resident blocks per CU: the largest over the persistent kernels
         // (the LDS-stack kernels fit fewer than the register-stack packet ones)
         const void *kernels[] = {
-            reinterpret_cast<const void *>(k_render_refill<true, false, 2>),
-            reinterpret_cast<const void *>(k_render_tile<true, false, 2>),
             reinterpret_cast<const void *>(k_render_packet<true, false, 2>),
             reinterpret_cast<const void *>(k_render_packet2<true, false, 2>),
             reinterpret_cast<const void *>(k_render_packet_asm<true, false, 2>),

@@ -52,8 +52,19 @@ void square(const Gf2 &A, Gf2 &out) {
     }
 }
 
-std::once_flag g_once;
+// C = A o B (all tables are powers of one matrix, so they commute)
+void mul(const Gf2 &A, const Gf2 &B, Gf2 &C) {
+    for (int b = 0; b < 160; ++b) {
+        uint32_t x[5];
+        memcpy(x, B.c[b], sizeof x);
+        apply(A, x);
+        memcpy(C.c[b], x, sizeof x);
+    }
+}
+
+std::once_flag g_once, g_once_dev;
 std::vector<uint32_t> g_tables;   // [32 seq][160][5] ++ [64 step][160][5]
+std::vector<uint32_t> g_dev;      // device init tables, see xorwow_init_tables_host
 
 void build_tables() {
     std::vector<Gf2> step(64), seq(32);
@@ -95,6 +106,48 @@ void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d) {
 const uint32_t *xorwow_tables_host() {
     std::call_once(g_once, build_tables);
     return g_tables.data();
+}
+
+void xorwow_skip(uint32_t v[5], uint64_t skip) {
+    const uint32_t *step = xorwow_tables_host() + 32 * 800;
+    for (int k = 0; skip && k < 64; ++k, skip >>= 1)
+        if (skip & 1) {
+            Gf2 m;
+            memcpy(m.c, step + k * 800, sizeof m.c);
+            apply(m, v);
+        }
+}
+
+// k_rng_init's tables: jump bytes [4][256][160][5], entry (k, b) = J^(b << 8k)
+// with J = M^(2^67) (one subsequence), so a pixel's subsequence start is at
+// most 4 matrix applies; then J itself by 4-bit input groups [40][16][5]
+// (entry (g, n) = XOR of J's columns 4g + set bits of n), the step from one
+// pixel to the next from LDS.
+static void build_init_tables() {
+    const uint32_t *seqt = xorwow_tables_host();
+    std::vector<Gf2> seq(32);
+    for (int k = 0; k < 32; ++k) memcpy(seq[k].c, seqt + k * 800, 800 * 4);
+    g_dev.assign(kRngInitWords, 0u);
+    uint32_t *bytes = g_dev.data();
+    Gf2 id{};
+    for (int b = 0; b < 160; ++b) id.c[b][b >> 5] = 1u << (b & 31);
+    std::vector<Gf2> lvl(256);
+    for (int k = 0; k < 4; ++k) {
+        lvl[0] = id;
+        for (int b = 1; b < 256; ++b) mul(lvl[b & (b - 1)], seq[8 * k + __builtin_ctz(b)], lvl[b]);
+        for (int b = 0; b < 256; ++b) memcpy(bytes + ((size_t)k * 256 + b) * 800, lvl[b].c, 800 * 4);
+    }
+    uint32_t *nib = bytes + 4 * 256 * 800;
+    for (int g = 0; g < 40; ++g)
+        for (int n = 0; n < 16; ++n)
+            for (int j = 0; j < 4; ++j)
+                if ((n >> j) & 1)
+                    for (int w = 0; w < 5; ++w) nib[(g * 16 + n) * 5 + w] ^= seq[0].c[4 * g + j][w];
+}
+
+const uint32_t *xorwow_init_tables_host() {
+    std::call_once(g_once_dev, build_init_tables);
+    return g_dev.data();
 }
 
 }  // namespace bih

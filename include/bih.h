@@ -173,6 +173,11 @@ int bih_sync(const bih_tree *tree, void *stream);
  * and after the main render kernel) of the last render launched through this
  * tree. */
 int bih_last_render_ms(const bih_tree *tree, double *ms);
+/* The same render split in two: *kernel_ms as bih_last_render_ms (the main
+ * render kernel, the figure rocprofv3 reports for it) and *tail_ms from its
+ * end to the end of the render call's device work (k_render_fallback, the
+ * exact walk of packets the frustum-bin kernel left undecided). */
+int bih_last_render_times(const bih_tree *tree, double *kernel_ms, double *tail_ms);
 
 /* The frustum bins of the tree's current camera and image (any-hit renders):
  * usable = 1 when renders walk them; list entries over all tiles, entries of

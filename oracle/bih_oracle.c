@@ -417,6 +417,22 @@ static inline int find_nearest(const ob_tree *T, const ray_t *r, int leaf,
     return 0;
 }
 
+/* C4 closest-hit rule over a leaf (see bih_oracle.h): min (t, i) with
+ * t_lo < t < FLT_MAX; order-independent. */
+static inline void find_closest(const ob_tree *T, const ray_t *r, int leaf, float t_lo,
+                                float *bt, int32_t *bi, cnt_t *c) {
+    c->leaves++;
+    int32_t f = T->first_idx[leaf];
+    int32_t e = f + (int32_t)T->dup_cnt[leaf];
+    for (int32_t i = f; i < e; ++i) {
+        float t;
+        c->tris++;
+        if (!mt_test(T->tris + 9 * (size_t)T->tri_idx[i], r, &t)) continue;
+        if (!(t > t_lo && t < FLT_MAX)) continue;
+        if (t < *bt || (t == *bt && i < *bi)) { *bt = t; *bi = i; }
+    }
+}
+
 static int slab(const ob_tree *T, const ray_t *r, float *tmin_o, float *tmax_o) {
     /* CUDAKernels.cu:237-262 */
     const float *bb[2] = {T->scene_lo, T->scene_hi};
@@ -501,6 +517,120 @@ static int traverse_gpu_ref(const ob_tree *T, const ray_t *r, cnt_t *c, int anyh
     return rec.idx >= 0;
 }
 
+/* The reference walk's visit set (traverse_gpu_ref's decisions, no early
+ * exit) with the C4 closest-hit rule at its leaves. */
+static void traverse_closest(const ob_tree *T, const ray_t *r, float t_lo, float *bt, int32_t *bi,
+                             cnt_t *c) {
+    *bt = FLT_MAX; *bi = -1;
+    float tMin, tMax;
+    if (!slab(T, r, &tMin, &tMax)) return;
+    int U = T->n_unique;
+    if (U <= 0) return;
+    if (U == 1) { find_closest(T, r, 0, t_lo, bt, bi, c); return; }
+    stk_t stack[64];
+    int sp = 0;
+    stack[sp].node = -1; sp++;
+    int cur = 0;
+    while (cur != -1) {
+        c->nodes++;
+        int ax = T->axis[cur];
+        float org = r->o[ax], inv = r->inv[ax];
+        int nr = r->sign[ax], fr = 1 - nr;
+        float t[2];
+        t[0] = (T->clip[2 * cur] - org) * inv;
+        t[1] = (T->clip[2 * cur + 1] - org) * inv;
+        int A = tMin < t[nr];
+        int B = tMax < t[fr];
+        const int32_t *ch = T->children + 2 * cur;
+        const uint8_t *lf = T->is_leaf + 2 * cur;
+        int pop = 0;
+        if (!A && B) {
+            pop = 1;
+        } else if (A && B) {
+            if (lf[nr]) { find_closest(T, r, ch[nr], t_lo, bt, bi, c); pop = 1; }
+            else { cur = ch[nr]; tMax = t[nr]; }
+        } else if (!A && !B) {
+            if (lf[fr]) { find_closest(T, r, ch[fr], t_lo, bt, bi, c); pop = 1; }
+            else { cur = ch[fr]; tMin = t[fr]; }
+        } else {
+            if (lf[nr] && lf[fr]) {
+                find_closest(T, r, ch[nr], t_lo, bt, bi, c);
+                find_closest(T, r, ch[fr], t_lo, bt, bi, c);
+                pop = 1;
+            } else if (!lf[nr] && lf[fr]) {
+                find_closest(T, r, ch[fr], t_lo, bt, bi, c);
+                cur = ch[nr]; tMax = t[nr];
+            } else if (lf[nr] && !lf[fr]) {
+                find_closest(T, r, ch[nr], t_lo, bt, bi, c);
+                cur = ch[fr]; tMin = t[fr];
+            } else {
+                stack[sp].node = ch[fr]; stack[sp].tmin = t[fr]; stack[sp].tmax = tMax;
+                sp++;
+                cur = ch[nr]; tMax = t[nr];
+            }
+        }
+        if (pop) {
+            sp--;
+            cur = stack[sp].node; tMin = stack[sp].tmin; tMax = stack[sp].tmax;
+        }
+    }
+}
+
+int ob_closest(const ob_tree *T, const float o[3], const float d[3], float t_lo,
+               float *t_out, int32_t *idx_out) {
+    if (!T || !o || !d || !t_out || !idx_out) return -1;
+    ray_t r; make_ray(o, d, &r);
+    cnt_t c; memset(&c, 0, sizeof c);
+    traverse_closest(T, &r, t_lo, t_out, idx_out, &c);
+    return 0;
+}
+
+/* C4: hits along the mirror path of one primary ray, 0..OB_WHITTED_BOUNCES+1 */
+static int whitted_path(const ob_tree *T, const float o0[3], const float d0[3], cnt_t *c,
+                        uint64_t *rays) {
+    float o[3] = {o0[0], o0[1], o0[2]}, d[3] = {d0[0], d0[1], d0[2]};
+    int hits = 0;
+    for (int depth = 0; depth <= OB_WHITTED_BOUNCES; ++depth) {
+        ray_t r; make_ray(o, d, &r);
+        float t; int32_t i;
+        (*rays)++;
+        traverse_closest(T, &r, depth ? 1e-4f : 0.0f, &t, &i, c);
+        if (i < 0) break;
+        hits++;
+        if (depth == OB_WHITTED_BOUNCES) break;
+        const float *v = T->tris + 9 * (size_t)T->tri_idx[i];
+        float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+        float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        float n[3]; cross3(e1, e2, n);
+        float dn = dot3(d, n), nn = dot3(n, n);
+        float k = (2.0f * dn) / nn;
+        float p[3], rd[3];
+        for (int a = 0; a < 3; ++a) {
+            float td = t * d[a];
+            p[a] = o[a] + td;
+            float kn = k * n[a];
+            rd[a] = d[a] - kn;
+        }
+        memcpy(o, p, sizeof p);
+        memcpy(d, rd, sizeof rd);
+    }
+    return hits;
+}
+
+/* shade of a sample with h hits (bih_oracle.h), f32 */
+static void whitted_shade(int h, float col[3]) {
+    float c[3];
+    if (h > OB_WHITTED_BOUNCES) { c[0] = 255.0f; c[1] = 255.0f; c[2] = 0.0f; h = OB_WHITTED_BOUNCES; }
+    else { c[0] = 20.0f; c[1] = 20.0f; c[2] = 40.0f; }
+    /* h hits at depths 0..h-1, each: 0.5*Y + 0.5*(deeper) */
+    for (int d = h - 1; d >= 0; --d) {
+        c[0] = 0.5f * 255.0f + 0.5f * c[0];
+        c[1] = 0.5f * 255.0f + 0.5f * c[1];
+        c[2] = 0.5f * 0.0f + 0.5f * c[2];
+    }
+    col[0] = c[0]; col[1] = c[1]; col[2] = c[2];
+}
+
 /* CPUTraverseTree, Renderer.cpp:202-349 (host debug semantics; the
  * debug-only ID==9 bookkeeping and printf are side effects, not restated). */
 static int traverse_host_debug(const ob_tree *T, const ray_t *r, cnt_t *c) {
@@ -582,11 +712,11 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
-              uint32_t spp, uint32_t frame, uint64_t seed,
-              uint32_t row0, uint32_t nrows, uint32_t row_step,
-              uint32_t *out, int mode, int nthreads, ob_stats *stats,
-              uint32_t *ray_counts) {
+static int render_impl(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
+                       uint32_t spp, uint32_t frame, uint64_t seed,
+                       uint32_t row0, uint32_t nrows, uint32_t row_step,
+                       uint32_t *out, int mode, int nthreads, ob_stats *stats,
+                       uint32_t *ray_counts, int whitted, uint8_t *depth_out) {
     if (!T || !cam || !out || w == 0 || h == 0 || spp == 0 || row_step == 0) return -1;
     if ((uint64_t)row0 + (uint64_t)(nrows ? nrows - 1 : 0) * row_step >= h && nrows) return -1;
     rng_tables_init();
@@ -638,6 +768,17 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
                         float vv = v * cam[9 + a];
                         d[a] = ((cam[3 + a] + hu) + vv) - cam[a];
                     }
+                    if (whitted) {
+                        uint64_t nr = 0;
+                        int hh = whitted_path(T, cam, d, &c, &nr);
+                        if (depth_out) depth_out[((size_t)k * w + i) * spp + sm] = (uint8_t)hh;
+                        g_hit += (uint64_t)(hh > 0);
+                        g_miss += nr;      /* rays traced (primary + secondary) */
+                        float sc[3];
+                        whitted_shade(hh, sc);
+                        col[0] += sc[0]; col[1] += sc[1]; col[2] += sc[2];
+                        continue;
+                    }
                     ray_t r; make_ray(cam, d, &r);
                     uint64_t n0 = c.nodes, l0 = c.leaves, t0r = c.tris;
                     int hit = trace_one(T, &r, mode, &c);
@@ -678,6 +819,24 @@ int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
         for (int q = 0; q < 33; ++q) stats->push_at[q] = g_push[q];
     }
     return 0;
+}
+
+int ob_render(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
+              uint32_t spp, uint32_t frame, uint64_t seed,
+              uint32_t row0, uint32_t nrows, uint32_t row_step,
+              uint32_t *out, int mode, int nthreads, ob_stats *stats,
+              uint32_t *ray_counts) {
+    return render_impl(T, cam, w, h, spp, frame, seed, row0, nrows, row_step, out, mode, nthreads,
+                       stats, ray_counts, 0, NULL);
+}
+
+/* stats->slab_miss counts every ray traced (primary + secondary) here. */
+int ob_render_whitted(const ob_tree *T, const float cam[12], uint32_t w, uint32_t h,
+                      uint32_t spp, uint32_t frame, uint64_t seed,
+                      uint32_t row0, uint32_t nrows, uint32_t row_step,
+                      uint32_t *out, int nthreads, ob_stats *stats, uint8_t *depth_out) {
+    return render_impl(T, cam, w, h, spp, frame, seed, row0, nrows, row_step, out, OB_MODE_GPU_REF,
+                       nthreads, stats, NULL, 1, depth_out);
 }
 
 int ob_trace_rays(const ob_tree *T, const float *orig, const float *dir, int32_t n,

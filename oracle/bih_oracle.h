@@ -84,6 +84,31 @@ int ob_render(const ob_tree *t, const float cam[12], uint32_t w, uint32_t h,
               uint32_t *out, int mode, int nthreads, ob_stats *stats,
               uint32_t *ray_counts);
 
+/* Config C4 (BASELINE.json configs[3]): 8-bounce Whitted mirror rays.  A
+ * build-defined extension (the reference has no secondary rays,
+ * CUDAKernels.cu:370-389); semantics, all f32 without contraction:
+ *   closest hit of a ray = min (t, sorted position i) over the triangles the
+ *     reference walk visits (TraverseTree's visit set, CUDAKernels.cu:227-368;
+ *     RayTriangleIntersection :17-50) with OB_WHITTED_TMIN[depth] < t < FLT_MAX
+ *     (depth 0: t > 0 as FindNearestTriangle :212; bounces: t > 1e-4);
+ *   hit point P = O + t*D; n = cross(e1, e2) (glm order, e = v - v0 of the
+ *     original triangle); k = (2*dot(D, n)) / dot(n, n); R = D - k*n;
+ *   shade(d) = miss ? (20,20,40) : d == 8 ? (255,255,0)
+ *              : 0.5*(255,255,0) + 0.5*shade(d+1)   (d = 0 primary .. 8)
+ *   pixel = rgbToInt(sum of the spp samples / spp) as cudaRender (:420-422).
+ * The shades are dyadic, so the pixel depends only on each sample's hit
+ * count h (0..9): bit-exact.  depth_out (optional) receives h per sample at
+ * [(k*w + x)*spp + s]. */
+#define OB_WHITTED_BOUNCES 8
+int ob_render_whitted(const ob_tree *t, const float cam[12], uint32_t w, uint32_t h,
+                      uint32_t spp, uint32_t frame, uint64_t seed,
+                      uint32_t row0, uint32_t nrows, uint32_t row_step,
+                      uint32_t *out, int nthreads, ob_stats *stats, uint8_t *depth_out);
+/* One closest-hit query with the C4 rule (tests): *t_out, *idx_out (sorted
+ * position, -1 on a miss) for ray (o, d) accepting t_lo < t < FLT_MAX. */
+int ob_closest(const ob_tree *t, const float o[3], const float d[3], float t_lo,
+               float *t_out, int32_t *idx_out);
+
 /* Per-ray hit flag + counters for a list of explicit rays (tests). */
 int ob_trace_rays(const ob_tree *t, const float *orig, const float *dir, int32_t n,
                   int mode, uint8_t *hit, uint32_t *nodes, uint32_t *tris);

@@ -151,8 +151,14 @@ def test_per_ray_counters_match_oracle(scene, gpu, bihrt_mod, oracle_mod):
     assert np.array_equal(img2, ref)
     assert np.array_equal(ref2, ref)
     assert (s2 <= s).all()
-    if os.environ.get("BIH_RENDER_KERNEL") in ("tile", "refill"):
-        assert np.array_equal(s2, rs2), "any-hit counters differ from the oracle's prefix"
+    # spp = 3 runs k_render_pixel (one lane per pixel, TraverseTree's order):
+    # both walks' counters equal the oracle's exactly
+    for trav, mode in ((bihrt_mod.TRAVERSE_REFERENCE, oracle_mod.MODE_GPU_REF),
+                       (bihrt_mod.TRAVERSE_ANYHIT, oracle_mod.MODE_GPU_ANYHIT)):
+        img3, s3 = _device_render(bihrt_mod, g, 64, 36, 3, 1, trav, stats=True)
+        ref3, _, rs3 = ot.render(64, 36, spp=3, frame=1, mode=mode, ray_stats=True)
+        assert np.array_equal(img3, ref3)
+        assert np.array_equal(s3, rs3), ("spp 3 counters differ from the oracle's", trav)
 
 
 def test_interleaved_bands(gpu, bihrt_mod, oracle_mod):
@@ -230,7 +236,7 @@ np.savez(sys.argv[2], **out)
 '''
 
 
-@pytest.mark.parametrize("variant", ["packet2", "packet1", "tile", "refill"])
+@pytest.mark.parametrize("variant", ["packet2", "packet1"])
 def test_kernel_variants_agree(variant, gpu, tmp_path):
     """Every render kernel (BIH_RENDER_KERNEL; the default is the inline-asm
     packet walk) gives the same RGBA, and the same per-ray counters for the

@@ -1,6 +1,6 @@
 """Multi-rank path on CPU (gloo): each rank renders its interleaved row bands
-(with the oracle, since there is no GPU here), the bands are all-gathered and
-reassembled with the same tiling code bench.py uses on RCCL; the result must
+(with the oracle, since there is no GPU here), the bands are gathered to rank
+0 and reassembled with the same code bench.py uses on RCCL (BandGather); the result must
 equal a one-process render byte for byte."""
 import os
 import socket
@@ -30,7 +30,7 @@ def _worker(rank, world, port, w, h, band, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle
-    from bihrt.tiling import band_rows, gather_order, max_rows, rows_of_rank
+    from bihrt.tiling import BandGather, band_rows, max_rows, rows_of_rank
     ot = oracle.OracleTree(edge_scenes()["cornell"])
     rows = band_rows(h, band, rank, world)
     ys = rows_of_rank(h, band, rank, world)
@@ -43,24 +43,26 @@ def _worker(rank, world, port, w, h, band, out_dir):
     local = np.zeros((mrows, w), np.uint32)
     for k, y in enumerate(ys):
         local[k], _ = ot.render(w, h, rows=(int(y), 1, 1))
+    # the exchange step bench.py runs for N > 1 (gather to rank 0 + reassembly)
     t = torch.from_numpy(local.view(np.int32).reshape(-1))
-    parts = [torch.zeros_like(t) for _ in range(world)]
-    dist.all_gather(parts, t)
-    gathered = torch.cat(parts).view(world * mrows, w)
-    frame = torch.index_select(gathered, 0, torch.from_numpy(gather_order(h, band, world)))
-    np.save(os.path.join(out_dir, f"frame_{rank}.npy"), frame.numpy().view(np.uint32))
+    gather = BandGather(dist, h, w, band, rank, world, "cpu")
+    frame = torch.full((h * w,), -1, dtype=torch.int32) if rank == 0 else None
+    gather(t, frame)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "frame.npy"), frame.numpy().view(np.uint32).reshape(h, w))
+    else:
+        assert gather.recv is None     # nothing lands on non-root ranks
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band", [(2, 8), (3, 4)])
+@pytest.mark.parametrize("world,band", [(2, 8), (3, 4), (4, 8)])
 def test_band_tiling_gather_equals_single_render(tmp_path, world, band, oracle_mod):
     w, h = 48, 40
     mp.start_processes(_worker, args=(world, _free_port(), w, h, band, str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")
     ref, _ = oracle_mod.OracleTree(edge_scenes()["cornell"]).render(w, h)
-    for r in range(world):
-        assert np.array_equal(np.load(tmp_path / f"frame_{r}.npy"), ref)
+    assert np.array_equal(np.load(tmp_path / "frame.npy"), ref)
 
 
 def _frames_worker(rank, world, port, w, h, steps, out_dir):

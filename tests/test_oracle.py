@@ -368,6 +368,51 @@ def test_traversal_modes_agree_with_brute_force(oracle_mod, bihrt_mod):
     assert np.mean(h_ref != h_bf) < 1e-3
 
 
+# --- Host debug semantics: CPUTraverseTree / DebugRender (Renderer.cpp:202-412) --
+
+def test_host_debug_mode_cornell_known_answers(oracle_mod):
+    """Config C1 (Cornell box, 256x256, serial host traversal): the host
+    twin's rules (a leaf child is tested unconditionally, the sibling internal
+    node is entered without an interval check, "both" pushes (far, tMin,
+    tMax); Renderer.cpp:202-349) reach the same pixels as the GPU walk and
+    brute force, with a different visit set.  Counters are known answers of
+    this restatement (regression pins, not reference-held data)."""
+    ot = oracle_mod.OracleTree(edge_scenes()["cornell"])
+    hd, s_hd = ot.render(256, 256, mode=oracle_mod.MODE_HOST_DEBUG, threads=1)
+    ref, s_ref = ot.render(256, 256, mode=oracle_mod.MODE_GPU_REF)
+    bf, _ = ot.render(256, 256, mode=oracle_mod.MODE_BRUTE)
+    assert np.array_equal(hd, ref) and np.array_equal(hd, bf)
+    assert np.array_equal(hd, np.load(os.path.join(GOLDEN, "cornell_256x256_f0.npy")))
+    assert s_hd.threads == 1
+    assert (s_hd.rays_hit, s_hd.slab_miss) == (s_ref.rays_hit, s_ref.slab_miss) == (96336, 165808)
+    assert (s_hd.node_visits, s_hd.leaf_visits, s_hd.tri_tests) == (962363, 875734, 1613103)
+    assert (s_ref.node_visits, s_ref.leaf_visits, s_ref.tri_tests) == (979811, 646310, 1135753)
+
+
+@pytest.mark.parametrize("scene", ["cornell", "soup", "torus"])
+def test_host_debug_hit_set_equals_brute_force(oracle_mod, bihrt_mod, scene):
+    """Per ray, over random rays from inside and outside the scene box: the
+    host twin reports a hit exactly when brute force over every triangle does
+    (and so does the GPU walk on these scenes)."""
+    S = bihrt_mod.scenes
+    tris = {"cornell": S.cornell, "soup": lambda: S.soup(5_000, seed=3), "torus": S.torus}[scene]()
+    ot = oracle_mod.OracleTree(tris)
+    rng = np.random.default_rng(11)
+    n = 20_000 if scene == "cornell" else 3_000
+    c = (ot.scene_lo + ot.scene_hi) / 2
+    ext = ot.scene_hi - ot.scene_lo
+    org = (c + rng.uniform(-1.5, 1.5, (n, 3)) * ext).astype(F32)
+    dirs = (c + rng.uniform(-0.5, 0.5, (n, 3)) * ext - org).astype(F32)
+    h_hd, n_hd, t_hd = ot.trace(org, dirs, oracle_mod.MODE_HOST_DEBUG)
+    h_bf, _, _ = ot.trace(org, dirs, oracle_mod.MODE_BRUTE)
+    h_ref, n_ref, _ = ot.trace(org, dirs, oracle_mod.MODE_GPU_REF)
+    assert h_hd.sum() > n // 20
+    assert np.array_equal(h_hd, h_bf)
+    assert np.array_equal(h_ref, h_bf)
+    # the host rules never prune a leaf child: they test at least as many triangles
+    assert t_hd.sum() >= h_hd.sum()
+
+
 def test_pixels_take_the_five_binary_shades(oracle_mod):
     """k of 4 samples hit -> R=G=floor((255k + 20(4-k))/4), B=10(4-k)
     (Color + rgbToInt, CUDAKernels.cu:370-389,74-88)."""
@@ -386,7 +431,7 @@ def test_pixels_take_the_five_binary_shades(oracle_mod):
 GOLDEN_CASES = [("cornell_256x256_f0.npy", "cornell", 256, 256, 0),
                 ("cornell_256x256_f7.npy", "cornell", 256, 256, 7),
                 ("dodeca_64x64_f0.npy", "dodeca", 64, 64, 0),
-         ("bih1_dodeca_640x480_f0.npy", "bih1_dodeca", 640, 480, 0)]
+                ("bih1_dodeca_640x480_f0.npy", "bih1_dodeca", 640, 480, 0)]
 
 
 @pytest.mark.parametrize("fname,scene,w,h,frame", GOLDEN_CASES)
