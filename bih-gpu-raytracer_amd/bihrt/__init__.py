@@ -158,6 +158,28 @@ class Renderer:
                                        C.c_void_p(out_ptr), C.c_void_p(stats_ptr or 0),
                                        C.c_void_p(stream or 0)), "bih_render_device")
 
+    def render_whitted(self, frame: int | None = None) -> np.ndarray:
+        """Config C4: one frame of 8-bounce mirror rays (bih_render_whitted) into a
+        host (h, w) uint32 image."""
+        f = self.frame if frame is None else frame
+        out = np.zeros((self.h, self.w), np.uint32)
+        fb = Framebuffer(self.w, self.h, self.spp, f, self.seed, out.ctypes.data)
+        sc = C.byref(self.arrays.scene) if self.arrays.scene is not None else None
+        check(load().bih_render_whitted(sc, self.arrays.handle, C.byref(self.camera), C.byref(fb)),
+              "bih_render_whitted")
+        self.frame = f + 1
+        return out
+
+    def render_whitted_device(self, out_ptr: int, frame: int, rows: Rows | None = None,
+                              hits_ptr: int | None = None, stream: int | None = None):
+        """Asynchronous C4 render into out_ptr (u32, nrows*w); hits_ptr (optional,
+        u32 per sample) receives each sample's hit count along its mirror path."""
+        check(load().bih_render_whitted_device(self.arrays.handle, C.byref(self.camera), self.w, self.h,
+                                               self.spp, frame, self.seed,
+                                               C.byref(rows) if rows is not None else None,
+                                               C.c_void_p(out_ptr), C.c_void_p(hits_ptr or 0),
+                                               C.c_void_p(stream or 0)), "bih_render_whitted_device")
+
     def sync(self, stream: int | None = None):
         check(load().bih_sync(self.arrays.handle, C.c_void_p(stream or 0)), "bih_sync")
 

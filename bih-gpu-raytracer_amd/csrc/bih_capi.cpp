@@ -112,6 +112,9 @@ struct bih_tree {
     uint32_t q_par[kSlots] = {};
     uint32_t *fb_mem = nullptr;      // per slot: fallback records of k_render_bins (8 words per tile)
     size_t fbq_cap = 0;              // tiles per slot
+    // config C4 (bih_whitted.hip): two ray queues, counters and per-sample hits
+    char *wh_mem = nullptr;
+    size_t wh_rays = 0;              // queue capacity (rays)
 };
 
 namespace {
@@ -406,6 +409,7 @@ void bih_free(bih_tree *tr) {
     if (tr->q_mem) (void)hipFree(tr->q_mem);
     if (tr->q_count) (void)hipFree(tr->q_count);
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
+    if (tr->wh_mem) (void)hipFree(tr->wh_mem);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
         if (tr->evd[k]) (void)hipEventDestroy(tr->evd[k]);
@@ -980,6 +984,111 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;                 // frame+1's state
     return BIH_OK;
+}
+
+int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h,
+                              uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows_in,
+                              uint32_t *d_out, uint32_t *d_hits, void *stream) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0) return BIH_ERR_INVALID;
+    bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
+    if (rows.nrows == 0) return BIH_OK;
+    if (rows.band_h == 0 || rows.band_step == 0) return BIH_ERR_INVALID;
+    uint64_t lr = rows.nrows - 1;
+    uint64_t ylast = rows.row0 + (lr / rows.band_h) * (uint64_t)rows.band_h * rows.band_step +
+                     (lr % rows.band_h);
+    if (ylast >= h) return BIH_ERR_INVALID;
+    if ((uint64_t)h * w * spp > 0xFFFFFFFFull) return BIH_ERR_TOO_LARGE;   // u32 ray ids
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+    resolve_bins(tr, false);
+    // the queues are shared by every Whitted render of this tree: order after
+    // every render in flight (and after the last writer of the RNG ring)
+    int rc = wait_renders(tr, st);
+    if (rc) return rc;
+    if (tr->rng_pending) {
+        hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
+    if (rc) return rc;
+    const size_t P = (size_t)rows.nrows * w;
+    const uint64_t rays = (uint64_t)P * spp;
+    const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, st));
+    if (rc) return rc;
+    if (tr->wh_rays < rays) {
+        hipError_t e = hipStreamSynchronize(st);   // the previous Whitted render's readers
+        if (e != hipSuccess) return map_hip((int)e);
+        if (tr->wh_mem) (void)hipFree(tr->wh_mem);
+        tr->wh_mem = nullptr;
+        tr->wh_rays = 0;
+        e = hipMalloc((void **)&tr->wh_mem, bih::whitted_bytes(rays));
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->wh_rays = rays;
+    }
+    hipError_t e = hipEventRecord(tr->ev_rng, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_pending = true;
+    bih::RenderArgs a;
+    memcpy(a.cam, cam, sizeof a.cam);
+    a.w = w;
+    a.h = h;
+    a.spp = spp;
+    a.row0 = rows.row0;
+    a.nrows = rows.nrows;
+    a.band_h = rows.band_h;
+    a.band_step = rows.band_step;
+    uint32_t v[5], d0;
+    bih::xorwow_seed(seed, v, &d0);
+    a.d_base = d0 + (uint32_t)((uint64_t)2 * spp * frame) * 362437u;
+    a.hdr = tr->t.hdr;
+    a.hdr_n_tris = tr->t.n;
+    a.n_nodes = tr->t.u > 0 ? tr->t.u - 1 : 0;
+    a.nodes = tr->t.nodes;
+    a.tris = tr->t.tris_s;
+    a.dup_cnt = tr->t.dup_cnt;
+    a.rng_in = rng_buf(tr, cur);
+    a.out = d_out;
+    const int slot = tr->slot;
+    rc = bih::launch_whitted(a, tr->wh_mem, rays, d_hits, st, tr->ev0[slot], tr->ev1[slot]);
+    if (rc) return map_hip(rc);
+    e = hipEventRecord(tr->evd[slot], st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->used[slot] = true;
+    tr->last_slot = slot;
+    tr->slot = (slot + 1) % kSlots;
+    tr->rng_cur = nxt;
+    return BIH_OK;
+}
+
+int bih_render_whitted(const bih_scene *scene, const bih_tree *ctr, const bih_camera *cam,
+                       bih_framebuffer *fb) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !cam || !fb || !fb->rgba) return BIH_ERR_INVALID;
+    if (scene && (scene->n_tris != tr->t.n || (tr->host_v && scene->v != tr->host_v)))
+        return BIH_ERR_MISMATCH;
+    if (fb->w == 0 || fb->h == 0 || fb->spp == 0) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    const size_t P = (size_t)fb->h * fb->w;
+    {
+        std::lock_guard<std::mutex> lk(tr->mu);
+        if (P > tr->fb_cap) {
+            if (tr->fb) (void)hipFree(tr->fb);
+            tr->fb = nullptr;
+            tr->fb_cap = 0;
+            hipError_t e = hipMalloc((void **)&tr->fb, P * 4);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->fb_cap = P;
+        }
+    }
+    int rc = bih_render_whitted_device(tr, cam, fb->w, fb->h, fb->spp, fb->frame, fb->seed, nullptr, tr->fb,
+                                       nullptr, nullptr);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(fb->rgba, tr->fb, P * 4, hipMemcpyDeviceToHost, tr->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(tr->stream);
+    return map_hip((int)e);
 }
 
 int bih_sync(const bih_tree *tr, void *stream) {

@@ -170,6 +170,13 @@ void free_tree_device(DeviceTree &t);
 // render (bih_render.hip)
 int upload_rng_tables(int device);
 const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host() on the device
+// config C4 (bih_whitted.hip): device bytes of the ray queues for `rays`
+// samples, and the frame's launches (k_wh_gen, 9 x k_wh_trace, k_wh_shade);
+// ev_k0/ev_k1 bracket the trace launches.  d_hits (optional): u32 hit count
+// per sample.
+size_t whitted_bytes(uint64_t rays);
+int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
+                   void *ev_k1);
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)

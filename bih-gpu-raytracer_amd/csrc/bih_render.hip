@@ -38,13 +38,19 @@
 #include "bih_internal.h"
 #include "bih_bound.h"
 #include "bih_packet_asm.h"
+#include "bih_device.h"
 
 namespace bih {
 namespace {
 
+using dev::camera_dir;
+using dev::global_row;
+using dev::kDetEps;
+using dev::kWeyl;
+using dev::rgb_to_int;
+using dev::xorwow_uniform;
+
 constexpr int kThreads = 256;
-constexpr float kDetEps = 9.99999997475242708e-07f;   // 0x358637bd: largest f32 < 1e-6
-constexpr uint32_t kWeyl = 362437u;
 constexpr uint32_t kDone = 0xFFFFFFFFu;
 
 #ifndef BIH_MT_EARLY_OUT
@@ -69,11 +75,6 @@ __device__ __forceinline__ void gf2_apply(const uint32_t *__restrict__ m, uint32
         }
     }
     x[0] = r0; x[1] = r1; x[2] = r2; x[3] = r3; x[4] = r4;
-}
-
-__device__ __forceinline__ uint32_t global_row(uint32_t lr, uint32_t row0, uint32_t band_h,
-                                               uint32_t band_step) {
-    return row0 + (lr / band_h) * band_h * band_step + (lr % band_h);
 }
 
 // Per-pixel curand_init(seed, pixel, 0) + skip (InitRandGPU,
@@ -141,22 +142,6 @@ __global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, u
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
-}
-
-__device__ __forceinline__ float xorwow_uniform(uint32_t v[5], uint32_t &d) {
-    uint32_t t = v[0] ^ (v[0] >> 2);
-    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
-    d += kWeyl;
-    uint32_t x = v[4] + d;
-    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);   // _curand_uniform
-}
-
-__device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
-    r = fmaxf(0.0f, fminf(255.0f, r));                             // clamp, :74-76
-    g = fmaxf(0.0f, fminf(255.0f, g));
-    b = fmaxf(0.0f, fminf(255.0f, b));
-    return ((uint32_t)(int)b << 16) | ((uint32_t)(int)g << 8) | (uint32_t)(int)r;
 }
 
 // Pixel of k hits out of spp samples.  Color() returns (255,255,0) or
@@ -413,13 +398,6 @@ struct Walker {
 };
 
 // Camera::GetRay(u, v) direction, Camera.cu:18-20 (glm order, no contraction).
-__device__ __forceinline__ void camera_dir(const RenderArgs &a, float u, float v, float &dx, float &dy,
-                                           float &dz) {
-    dx = ((a.cam[3] + u * a.cam[6]) + v * a.cam[9]) - a.cam[0];
-    dy = ((a.cam[4] + u * a.cam[7]) + v * a.cam[10]) - a.cam[1];
-    dz = ((a.cam[5] + u * a.cam[8]) + v * a.cam[11]) - a.cam[2];
-}
-
 template <int L>
 struct TileShape {   // TW x TH pixels, TW*TH = 64 >> log2(spp)
     static constexpr uint32_t LP = 6 - L;

@@ -1,0 +1,352 @@
+// bih_whitted.hip -- config C4 (BASELINE.json configs[3]): 8-bounce Whitted
+// mirror rays at 3840x2160 on gfx950, as a wavefront of compacted ray queues.
+//
+// The reference has primary rays only (cudaRender, CUDAKernels.cu:391-423;
+// Color :370-389 is binary).  C4's semantics are the build's own, defined in
+// the test oracle (ob_render_whitted) and DESIGN.md section 4.5:
+//   closest hit = min (t, sorted position) over the triangles the reference
+//   walk visits (TraverseTree's decisions, :227-368, RayTriangleIntersection
+//   :17-50), t_lo < t < FLT_MAX (t_lo = 0 for primary rays, 1e-4 after);
+//   P = O + t*D, n = cross(e1, e2), k = (2*dot(D, n)) / dot(n, n), R = D - k*n;
+//   shade(d) = miss ? (20,20,40) : d == 8 ? (255,255,0) : 0.5*Y + 0.5*shade(d+1).
+// The (t, i) rule is order-independent, so any walk order over the same visit
+// set gives the oracle's hit; every f32 expression is the oracle's, in its
+// order (-ffp-contract=off): bit-exact RGBA.
+//
+// Kernels (one frame, all on the caller's stream, no host round trip):
+//   k_wh_gen    one thread per sample: the XORWOW jitter (cudaRender's draws)
+//               and camera direction into ray queue 0; zeroes the counters.
+//   k_wh_trace  bounce d (9 launches): persistent waves drain queue d%2
+//               (length counts[d]); each lane walks its ray's BIH visit set
+//               for the closest hit; hits reflect and are appended to queue
+//               (d+1)%2 with one ballot + mbcnt per wave and one atomic per
+//               wave (wavefront compaction: the next bounce's waves are full).
+//   k_wh_shade  one thread per pixel: the samples' shades -> rgbToInt.
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+#include "bih_device.h"
+#include "bih_internal.h"
+
+namespace bih {
+namespace {
+
+using dev::camera_dir;
+using dev::global_row;
+using dev::kDetEps;
+using dev::rgb_to_int;
+using dev::xorwow_uniform;
+
+constexpr uint32_t kWT = 64;            // threads per block: one wave
+constexpr int kWStack = kStackDepth;    // Karras path length <= 30 (bih_internal.h)
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
+
+struct WScene {
+    const uint4 *nodes;
+    const float *tris;          // sorted {v0, e1, e2}
+    const uint32_t *dup;
+    float slo[3], shi[3];
+    uint32_t U, N;
+};
+
+__device__ __forceinline__ WScene load_wscene(const RenderArgs &a) {
+    WScene s;
+    s.nodes = a.nodes;
+    s.tris = a.tris;
+    s.dup = a.dup_cnt;
+    for (int k = 0; k < 3; ++k) {
+        s.slo[k] = a.hdr->scene_lo[k];
+        s.shi[k] = a.hdr->scene_hi[k];
+    }
+    s.U = a.hdr->n_unique;
+    s.N = a.hdr->n_tris;
+    return s;
+}
+
+__device__ __forceinline__ float pick3(uint32_t ax, float a, float b, float c) {
+    return ax == 0 ? a : (ax == 1 ? b : c);
+}
+
+// RayTriangleIntersection (CUDAKernels.cu:17-50) on a {v0, e1, e2} record,
+// returning t; with the C4 acceptance t_lo < t < FLT_MAX.
+__device__ __forceinline__ bool mt_t(const float *__restrict__ tp, float ox, float oy, float oz, float dx,
+                                     float dy, float dz, float t_lo, float &t) {
+    const float v0x = tp[0], v0y = tp[1], v0z = tp[2];
+    const float e1x = tp[3], e1y = tp[4], e1z = tp[5];
+    const float e2x = tp[6], e2y = tp[7], e2z = tp[8];
+    const float px = dy * e2z - e2y * dz;                  // pvec = cross(D, e2)
+    const float py = dz * e2x - e2z * dx;
+    const float pz = dx * e2y - e2x * dy;
+    const float det = (e1x * px + e1y * py) + e1z * pz;
+    if (det <= kDetEps) return false;                      // det < 0.000001 (double); NaN passes
+    const float inv = 1.0f / det;
+    const float sx = ox - v0x, sy = oy - v0y, sz = oz - v0z;
+    const float u = ((sx * px + sy * py) + sz * pz) * inv;
+    if (u < 0.0f || u > 1.0f) return false;
+    const float qx = sy * e1z - e1y * sz;                  // qvec = cross(tvec, e1)
+    const float qy = sz * e1x - e1z * sx;
+    const float qz = sx * e1y - e1x * sy;
+    const float v = ((dx * qx + dy * qy) + dz * qz) * inv;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    return t > t_lo && t < FLT_MAX;
+}
+
+// The C4 closest hit over the reference walk's visit set (the oracle's
+// traverse_closest): bt/bi = min (t, i), bi = kNoHit on a miss.  Stack slot
+// k of this lane at stk[k * kWT] (LDS).
+__device__ void closest_walk(const WScene &s, float ox, float oy, float oz, float dx, float dy, float dz,
+                             float t_lo, float &bt, uint32_t &bi, uint32_t *sn, float *smin, float *smax) {
+    bt = FLT_MAX;
+    bi = kNoHit;
+    const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+    const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+    // scene-AABB slab test, CUDAKernels.cu:237-262 (tMin may be negative)
+    float tMin = (((sg & 1) ? s.shi[0] : s.slo[0]) - ox) * ix;
+    float tMax = (((sg & 1) ? s.slo[0] : s.shi[0]) - ox) * ix;
+    const float tymin = (((sg & 2) ? s.shi[1] : s.slo[1]) - oy) * iy;
+    const float tymax = (((sg & 2) ? s.slo[1] : s.shi[1]) - oy) * iy;
+    if ((tMin > tymax) || (tymin > tMax)) return;
+    if (tymin > tMin) tMin = tymin;
+    if (tymax < tMax) tMax = tymax;
+    const float tzmin = (((sg & 4) ? s.shi[2] : s.slo[2]) - oz) * iz;
+    const float tzmax = (((sg & 4) ? s.slo[2] : s.shi[2]) - oz) * iz;
+    if ((tMin > tzmax) || (tzmin > tMax)) return;
+    if (tzmin > tMin) tMin = tzmin;
+    if (tzmax < tMax) tMax = tzmax;
+    if (s.U == 0) return;
+    auto leaf = [&](uint32_t b, uint32_t e) {
+        for (uint32_t i = b; i < e; ++i) {
+            float t;
+            if (mt_t(s.tris + 9ull * i, ox, oy, oz, dx, dy, dz, t_lo, t) && (t < bt || (t == bt && i < bi))) {
+                bt = t;
+                bi = i;
+            }
+        }
+    };
+    if (s.U == 1) {   // single leaf (reference: UB; defined as the oracle's)
+        leaf(0, s.N);
+        return;
+    }
+    uint32_t cur = 0, sp = 0;
+    for (;;) {
+        const uint4 nd = s.nodes[cur];
+        const uint32_t ax = (nd.z >> 27) & 3u;
+        const float org = pick3(ax, ox, oy, oz), inv = pick3(ax, ix, iy, iz);
+        const uint32_t nr = (sg >> ax) & 1u;
+        const float t0 = (__uint_as_float(nd.x) - org) * inv;
+        const float t1 = (__uint_as_float(nd.y) - org) * inv;
+        const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
+        const bool A = tMin < tn, B = tMax < tf;
+        const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
+        const bool leafL = (nd.z >> 29) & 1u, leafR = (nd.z >> 30) & 1u;
+        const bool leafN = nr ? leafR : leafL, leafF = nr ? leafL : leafR;
+        uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
+        if (leafL && cL == 0) cL = s.dup[split];
+        if (leafR && cR == 0) cR = s.dup[split + 1];
+        const uint32_t nb = nr ? mid : mid - cL, ne = nr ? mid + cR : mid;
+        const uint32_t fb = nr ? mid - cL : mid, fe = nr ? mid : mid + cR;
+        const uint32_t nearc = split + nr, farc = split + 1u - nr;
+        bool pop = false;
+        if (!A && B) {
+            pop = true;
+        } else if (A && B) {
+            if (leafN) { leaf(nb, ne); pop = true; }
+            else { cur = nearc; tMax = tn; }
+        } else if (!A && !B) {
+            if (leafF) { leaf(fb, fe); pop = true; }
+            else { cur = farc; tMin = tf; }
+        } else {
+            if (leafN && leafF) {
+                leaf(nb, ne);
+                leaf(fb, fe);
+                pop = true;
+            } else if (!leafN && leafF) {
+                leaf(fb, fe);
+                cur = nearc; tMax = tn;
+            } else if (leafN && !leafF) {
+                leaf(nb, ne);
+                cur = farc; tMin = tf;
+            } else {
+                sn[sp * kWT] = farc;
+                smin[sp * kWT] = tf;
+                smax[sp * kWT] = tMax;
+                ++sp;
+                cur = nearc; tMax = tn;
+            }
+        }
+        if (pop) {
+            if (sp == 0) return;
+            --sp;
+            cur = sn[sp * kWT];
+            tMin = smin[sp * kWT];
+            tMax = smax[sp * kWT];
+        }
+    }
+}
+
+// Ray queue: 7 planes of `cap` words {ox, oy, oz, dx, dy, dz, sample}.
+struct WQueue {
+    float *p;
+    uint64_t cap;
+    __device__ __forceinline__ void put(uint64_t i, const float o[3], const float d[3], uint32_t sid) const {
+        for (int k = 0; k < 3; ++k) {
+            p[k * cap + i] = o[k];
+            p[(3 + k) * cap + i] = d[k];
+        }
+        reinterpret_cast<uint32_t *>(p)[6 * cap + i] = sid;
+    }
+};
+
+// counts[0..9]: rays in queue d (d = bounce depth)
+__global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, uint32_t *counts,
+                                                uint8_t *hits) {
+    const uint64_t P = (uint64_t)a.nrows * a.w;
+    const uint64_t rays = P * a.spp;
+    const uint64_t gid = (uint64_t)blockIdx.x * kWT + threadIdx.x;
+    if (gid == 0) {
+        counts[0] = (uint32_t)rays;
+        for (int k = 1; k < 16; ++k) counts[k] = 0u;
+    }
+    if (gid >= rays) return;
+    const uint64_t lp = gid / a.spp;
+    const uint32_t s = (uint32_t)(gid % a.spp);
+    // draws 2s, 2s+1 of this pixel's frame (cudaRender :413-415)
+    uint32_t v[5];
+    for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
+    uint32_t d = a.d_base;
+    float ru = 0.f, rv = 0.f;
+    for (uint32_t k = 0; k <= s; ++k) {
+        ru = xorwow_uniform(v, d);
+        rv = xorwow_uniform(v, d);
+    }
+    const uint32_t lr = (uint32_t)(lp / a.w), x = (uint32_t)(lp % a.w);
+    const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+    float dir[3];
+    camera_dir(a, ((float)x + ru) / (float)a.w, ((float)y + rv) / (float)a.h, dir[0], dir[1], dir[2]);
+    q.put(gid, a.cam, dir, (uint32_t)gid);
+    hits[gid] = 0;
+}
+
+__global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
+                                                  uint32_t *counts, uint8_t *hits) {
+    __shared__ uint32_t s_node[kWStack * kWT];
+    __shared__ float s_min[kWStack * kWT];
+    __shared__ float s_max[kWStack * kWT];
+    const uint32_t lane = threadIdx.x;
+    const WScene sc = load_wscene(a);
+    const uint32_t n = counts[depth];
+    const float t_lo = depth ? kBounceTLo : 0.0f;
+    const uint32_t *sid_in = reinterpret_cast<const uint32_t *>(qin.p) + 6 * qin.cap;
+    // wave-uniform loop over the queue (every lane takes part in the ballot)
+    for (uint64_t base = (uint64_t)blockIdx.x * kWT; base < n; base += (uint64_t)gridDim.x * kWT) {
+        const uint64_t i = base + lane;
+        const bool valid = i < n;
+        float o[3] = {0.f, 0.f, 0.f}, d[3] = {0.f, 0.f, 1.f};
+        uint32_t sid = 0;
+        float bt = FLT_MAX;
+        uint32_t bi = kNoHit;
+        if (valid) {
+            for (int k = 0; k < 3; ++k) {
+                o[k] = qin.p[k * qin.cap + i];
+                d[k] = qin.p[(3 + k) * qin.cap + i];
+            }
+            sid = sid_in[i];
+            closest_walk(sc, o[0], o[1], o[2], d[0], d[1], d[2], t_lo, bt, bi, s_node + lane, s_min + lane,
+                         s_max + lane);
+        }
+        const bool hit = valid && bi != kNoHit;
+        if (hit) hits[sid] = (uint8_t)(depth + 1);
+        // the mirror ray (oracle whitted_path), then compaction into qout
+        const bool next = hit && depth < 8u;
+        float po[3], rd[3];
+        if (next) {
+            const float *v = sc.tris + 9ull * bi;
+            const float e1x = v[3], e1y = v[4], e1z = v[5], e2x = v[6], e2y = v[7], e2z = v[8];
+            const float nx = e1y * e2z - e2y * e1z;        // n = cross(e1, e2), glm order
+            const float ny = e1z * e2x - e2z * e1x;
+            const float nz = e1x * e2y - e2x * e1y;
+            const float dn = (d[0] * nx + d[1] * ny) + d[2] * nz;
+            const float nn = (nx * nx + ny * ny) + nz * nz;
+            const float kk = (2.0f * dn) / nn;
+            const float nv[3] = {nx, ny, nz};
+            for (int k = 0; k < 3; ++k) {
+                const float td = bt * d[k];
+                po[k] = o[k] + td;
+                const float kn = kk * nv[k];
+                rd[k] = d[k] - kn;
+            }
+        }
+        const unsigned long long m = __ballot(next);
+        if (m) {
+            uint32_t first = 0;
+            if (lane == 0) first = atomicAdd(counts + depth + 1, (uint32_t)__popcll(m));
+            first = __builtin_amdgcn_readfirstlane(first);
+            if (next) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                qout.put((uint64_t)first + r, po, rd, sid);
+            }
+        }
+    }
+}
+
+// shade of a sample with h hits (oracle whitted_shade), f32
+__device__ __forceinline__ void wh_shade(uint32_t h, float &r, float &g, float &b) {
+    if (h > 8u) { r = 255.0f; g = 255.0f; b = 0.0f; h = 8u; }
+    else { r = 20.0f; g = 20.0f; b = 40.0f; }
+    for (uint32_t k = 0; k < h; ++k) {
+        r = 0.5f * 255.0f + 0.5f * r;
+        g = 0.5f * 255.0f + 0.5f * g;
+        b = 0.5f * 0.0f + 0.5f * b;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_wh_shade(const RenderArgs a, const uint8_t *hits, uint32_t *d_hits) {
+    const uint64_t P = (uint64_t)a.nrows * a.w;
+    const uint64_t lp = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (lp >= P) return;
+    float cr = 0.f, cg = 0.f, cb = 0.f;
+    for (uint32_t s = 0; s < a.spp; ++s) {
+        const uint32_t h = hits[lp * a.spp + s];
+        if (d_hits) d_hits[lp * a.spp + s] = h;
+        float r, g, b;
+        wh_shade(h, r, g, b);
+        cr += r; cg += g; cb += b;                     // col += Color(...), sample order
+    }
+    const float fs = (float)a.spp;
+    a.out[lp] = rgb_to_int(cr / fs, cg / fs, cb / fs);
+}
+
+}  // namespace
+
+size_t whitted_bytes(uint64_t rays) { return 2 * (7 * rays * 4) + rays + 64; }
+
+int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
+                   void *ev_k1) {
+    const hipStream_t st = (hipStream_t)stream;
+    if (rays == 0) return 0;
+    float *base = reinterpret_cast<float *>(mem);
+    WQueue q0{base, rays}, q1{base + 7 * rays, rays};
+    uint32_t *counts = reinterpret_cast<uint32_t *>(base + 14 * rays);
+    uint8_t *hits = reinterpret_cast<uint8_t *>(counts + 16);
+    hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits);
+    hipError_t e = ev_k0 ? hipEventRecord((hipEvent_t)ev_k0, st) : hipSuccess;
+    if (e != hipSuccess) return (int)e;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t need = (rays + kWT - 1) / kWT;
+    const uint32_t grid = (uint32_t)(need < (uint64_t)cus * 16 ? need : (uint64_t)cus * 16);
+    for (uint32_t d = 0; d <= 8; ++d)
+        hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1,
+                           counts, hits);
+    e = ev_k1 ? hipEventRecord((hipEvent_t)ev_k1, st) : hipSuccess;
+    if (e != hipSuccess) return (int)e;
+    const uint64_t P = (uint64_t)a.nrows * a.w;
+    hipLaunchKernelGGL(k_wh_shade, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, a, hits, d_hits);
+    return (int)hipGetLastError();
+}
+
+}  // namespace bih

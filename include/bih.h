@@ -169,6 +169,24 @@ int bih_render_device(const bih_tree *tree, const bih_camera *camera, uint32_t w
                       uint32_t traverse, uint32_t *d_out, uint32_t *d_ray_stats, void *stream);
 int bih_sync(const bih_tree *tree, void *stream);
 
+/* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)
+ * reflection per primary ray.  The reference has primary rays only
+ * (Color, src/CUDAKernels.cu:370-389), so these semantics are this
+ * library's own, stated in DESIGN.md section 4.5 and restated by the oracle
+ * (ob_render_whitted): closest hit = min (t, sorted index) over the reference
+ * walk's visit set; P = O + tD, n = cross(e1, e2), R = D - (2 D.n / n.n) n;
+ * secondary hits need t > 1e-4; a sample's shade halves towards (255,255,0)
+ * per hit and ends at (20,20,40) on a miss (or (255,255,0) after 8 bounces).
+ * Same primary rays, RNG draws and framebuffer format as bih_render.
+ * d_hits (optional, device u32[rays]): hits along each sample's mirror path
+ * (0..9), ray = local pixel * spp + sample. */
+#define BIH_WHITTED_BOUNCES 8
+int bih_render_whitted_device(const bih_tree *tree, const bih_camera *camera, uint32_t w, uint32_t h,
+                              uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows,
+                              uint32_t *d_out, uint32_t *d_hits, void *stream);
+int bih_render_whitted(const bih_scene *scene, const bih_tree *tree, const bih_camera *camera,
+                       bih_framebuffer *fb);
+
 /* Device time (ms, HIP events on the render stream, recorded right before
  * and after the main render kernel) of the last render launched through this
  * tree. */

@@ -79,6 +79,14 @@ def lib():
         L.ob_trace_rays.restype = C.c_int
         L.ob_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ob_mt.restype = C.c_int
+        L.ob_render_whitted.argtypes = [C.POINTER(_Tree), C.c_void_p, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_void_p, C.c_int, C.POINTER(Stats),
+                                        C.c_void_p]
+        L.ob_render_whitted.restype = C.c_int
+        L.ob_closest.argtypes = [C.POINTER(_Tree), C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                 C.c_void_p]
+        L.ob_closest.restype = C.c_int
         L.ob_morton3d.argtypes = [C.c_float, C.c_float, C.c_float]
         L.ob_morton3d.restype = C.c_uint32
         _lib = L
@@ -149,6 +157,33 @@ class OracleTree:
         if ray_stats:
             return out, st, rc_arr
         return out, st
+
+    def render_whitted(self, w, h, spp=4, frame=0, seed=1984, cam=None, rows=None, threads=0,
+                       depths=False):
+        """Config C4 (bih_oracle.h ob_render_whitted): (uint32 image rows, Stats[,
+        uint8 per-sample hit counts (rays, )]).  Stats.slab_miss = rays traced."""
+        if cam is None:
+            cam = camera_reference(w, h)
+        cam = np.ascontiguousarray(cam, np.float32).reshape(12)
+        row0, nrows, step = rows if rows is not None else (0, h, 1)
+        out = np.zeros((nrows, w), np.uint32)
+        st = Stats()
+        dep = np.zeros(nrows * w * spp, np.uint8) if depths else None
+        rc = lib().ob_render_whitted(self._p, cam.ctypes.data, w, h, spp, frame, seed, row0, nrows,
+                                     step, out.ctypes.data, threads, C.byref(st),
+                                     dep.ctypes.data if depths else None)
+        if rc != 0:
+            raise RuntimeError(f"ob_render_whitted failed: {rc}")
+        return (out, st, dep) if depths else (out, st)
+
+    def closest(self, o, d, t_lo=0.0):
+        """C4 closest hit: (t, sorted index) or (FLT_MAX, -1)."""
+        o = np.ascontiguousarray(o, np.float32).reshape(3)
+        d = np.ascontiguousarray(d, np.float32).reshape(3)
+        t = np.zeros(1, np.float32)
+        i = np.zeros(1, np.int32)
+        lib().ob_closest(self._p, o.ctypes.data, d.ctypes.data, t_lo, t.ctypes.data, i.ctypes.data)
+        return float(t[0]), int(i[0])
 
     def trace(self, orig, dirs, mode=MODE_GPU_REF):
         orig = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
