@@ -72,6 +72,8 @@ def parse():
                          "(child processes, before this process touches the GPU)")
     ap.add_argument("--kernel-samples", type=int, default=20,
                     help="isolated launches timed with the library's kernel events (roofline launch_ms)")
+    ap.add_argument("--whitted-frames", type=int, default=3,
+                    help="N=1: frames of config C4 (8-bounce Whitted, 3840x2160, same soup) to time; 0 = skip")
     ap.add_argument("--no-reference-leg", action="store_true")
     ap.add_argument("--no-rebuild-leg", action="store_true",
                     help="skip the leg that rebuilds the BIH every frame (as the reference does)")
@@ -242,6 +244,34 @@ def main():
                              "on this GPU, frames in flight as the headline; efficiency = full ms / "
                              f"({Q} x slowest share ms); excludes the gather to rank 0 "
                              f"({H * W * 4 * (Q - 1) // Q / 1e6:.1f} MB over xGMI per frame)"}
+
+    # config C4 (BASELINE.json configs[3]): 8-bounce Whitted mirror rays at
+    # 3840x2160 on the same soup and tree (bih_render_whitted_device)
+    whitted_leg = None
+    if world == 1 and args.whitted_frames > 0 and not args.headline_only:
+        WW, WH = 3840, 2160
+        rw = bihrt.Renderer(arrays, WW, WH, spp=SPP, seed=1984)
+        wout = torch.zeros(WW * WH, dtype=torch.int32, device="cuda")
+        whits = torch.zeros(WW * WH * SPP, dtype=torch.int32, device="cuda")
+        rw.render_whitted_device(wout.data_ptr(), 0, hits_ptr=whits.data_ptr(), stream=sptr)
+        torch.cuda.synchronize()
+        traced = int(torch.clamp(whits.to(torch.int64) + 1, max=9).sum())
+        hist = torch.bincount(whits.view(-1), minlength=10).tolist()
+        del whits
+        t0 = time.perf_counter()
+        for k in range(args.whitted_frames):
+            rw.render_whitted_device(wout.data_ptr(), 1 + k, stream=sptr)
+        torch.cuda.synchronize()
+        wel = (time.perf_counter() - t0) / args.whitted_frames
+        wk, _ = rw.last_render_times()
+        whitted_leg = {"config": "C4: 1M soup, 3840x2160, 4 spp, 8 bounces of mirror rays",
+                       "ms_per_frame": 1e3 * wel, "primary_rays_per_s": WW * WH * SPP / wel,
+                       "rays_traced_per_frame": traced, "rays_traced_per_s": traced / wel,
+                       "trace_kernels_ms": wk, "hit_histogram": hist, "frames": args.whitted_frames,
+                       "note": "k_wh_gen + 9 x k_wh_trace (closest hit, per-lane walk, ballot/mbcnt "
+                               "compaction of live rays between bounces) + k_wh_shade; bit-exact vs the "
+                               "oracle (tests/test_whitted.py)"}
+        del wout
 
     # N > 1: the other decomposition, informational
     side_leg = None
@@ -429,6 +459,7 @@ def main():
             "one_in_flight": serial_leg,
             "other_decomposition": side_leg,
             "band_share": share_leg,
+            "whitted_c4": whitted_leg,
         }
         if parity_rows is not None:
             res["parity_sample_rows_equal"] = parity_rows

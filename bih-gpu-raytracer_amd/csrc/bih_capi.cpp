@@ -252,7 +252,7 @@ int create_tree(int device, void *stream, bih_tree **out) {
     for (int k = 0; k < kSlots && e == hipSuccess; ++k) {
         e = hipEventCreate(&tr->ev0[k]);
         if (e == hipSuccess) e = hipEventCreate(&tr->ev1[k]);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->evd[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreate(&tr->evd[k]);   // timed: bih_last_render_times
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_bins, hipEventDisableTiming);

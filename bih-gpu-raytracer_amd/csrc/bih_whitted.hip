@@ -39,6 +39,8 @@ using dev::xorwow_uniform;
 
 constexpr uint32_t kWT = 64;            // threads per block: one wave
 constexpr int kWStack = kStackDepth;    // Karras path length <= 30 (bih_internal.h)
+constexpr int kWLds = 8;                // stack slots per lane in LDS; deeper ones in HBM
+constexpr uint32_t kWBlocksPerCU = 32;  // persistent grid of k_wh_trace
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
 
@@ -93,11 +95,37 @@ __device__ __forceinline__ bool mt_t(const float *__restrict__ tp, float ox, flo
     return t > t_lo && t < FLT_MAX;
 }
 
-// The C4 closest hit over the reference walk's visit set (the oracle's
-// traverse_closest): bt/bi = min (t, i), bi = kNoHit on a miss.  Stack slot
-// k of this lane at stk[k * kWT] (LDS).
+// Per-lane stack: slots [0, kWLds) in LDS at [slot * kWT] from this lane's
+// base, deeper slots in this thread's HBM area (slot-major, grid-interleaved).
+struct WStack {
+    uint32_t *sn;
+    float *smin, *smax;
+    uint32_t *spill;           // + gtid; slot k >= kWLds at ((k - kWLds) * 3) * gthreads
+    uint64_t gthreads;
+    __device__ __forceinline__ void push(uint32_t sp, uint32_t n, float lo, float hi) const {
+        if (sp < (uint32_t)kWLds) {
+            sn[sp * kWT] = n; smin[sp * kWT] = lo; smax[sp * kWT] = hi;
+        } else {
+            uint32_t *q = spill + (uint64_t)(sp - kWLds) * 3 * gthreads;
+            q[0] = n; q[gthreads] = __float_as_uint(lo); q[2 * gthreads] = __float_as_uint(hi);
+        }
+    }
+    __device__ __forceinline__ void pop(uint32_t sp, uint32_t &n, float &lo, float &hi) const {
+        if (sp < (uint32_t)kWLds) {
+            n = sn[sp * kWT]; lo = smin[sp * kWT]; hi = smax[sp * kWT];
+        } else {
+            const uint32_t *q = spill + (uint64_t)(sp - kWLds) * 3 * gthreads;
+            n = q[0]; lo = __uint_as_float(q[gthreads]); hi = __uint_as_float(q[2 * gthreads]);
+        }
+    }
+};
+
+// The C4 closest hit (the oracle's traverse_closest): the reference walk's
+// decisions and order, min (t, i) at its leaves, and once a hit is known a
+// node entered beyond it is popped and tMax is clamped to it.  bi = kNoHit on
+// a miss.
 __device__ void closest_walk(const WScene &s, float ox, float oy, float oz, float dx, float dy, float dz,
-                             float t_lo, float &bt, uint32_t &bi, uint32_t *sn, float *smin, float *smax) {
+                             float t_lo, float &bt, uint32_t &bi, const WStack &stk) {
     bt = FLT_MAX;
     bi = kNoHit;
     const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
@@ -131,6 +159,14 @@ __device__ void closest_walk(const WScene &s, float ox, float oy, float oz, floa
     }
     uint32_t cur = 0, sp = 0;
     for (;;) {
+        const float best = bi != kNoHit ? bt : __builtin_inff();
+        if (tMin > best) {                           // entered beyond the best hit: skip
+            if (sp == 0) return;
+            --sp;
+            stk.pop(sp, cur, tMin, tMax);
+            continue;
+        }
+        if (best < tMax) tMax = best;
         const uint4 nd = s.nodes[cur];
         const uint32_t ax = (nd.z >> 27) & 3u;
         const float org = pick3(ax, ox, oy, oz), inv = pick3(ax, ix, iy, iz);
@@ -169,9 +205,7 @@ __device__ void closest_walk(const WScene &s, float ox, float oy, float oz, floa
                 leaf(nb, ne);
                 cur = farc; tMin = tf;
             } else {
-                sn[sp * kWT] = farc;
-                smin[sp * kWT] = tf;
-                smax[sp * kWT] = tMax;
+                stk.push(sp, farc, tf, tMax);
                 ++sp;
                 cur = nearc; tMax = tn;
             }
@@ -179,9 +213,7 @@ __device__ void closest_walk(const WScene &s, float ox, float oy, float oz, floa
         if (pop) {
             if (sp == 0) return;
             --sp;
-            cur = sn[sp * kWT];
-            tMin = smin[sp * kWT];
-            tMax = smax[sp * kWT];
+            stk.pop(sp, cur, tMin, tMax);
         }
     }
 }
@@ -230,11 +262,17 @@ __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, ui
 }
 
 __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
-                                                  uint32_t *counts, uint8_t *hits) {
-    __shared__ uint32_t s_node[kWStack * kWT];
-    __shared__ float s_min[kWStack * kWT];
-    __shared__ float s_max[kWStack * kWT];
+                                                  uint32_t *counts, uint8_t *hits, uint32_t *spill) {
+    __shared__ uint32_t s_node[kWLds * kWT];
+    __shared__ float s_min[kWLds * kWT];
+    __shared__ float s_max[kWLds * kWT];
     const uint32_t lane = threadIdx.x;
+    WStack stk;
+    stk.sn = s_node + lane;
+    stk.smin = s_min + lane;
+    stk.smax = s_max + lane;
+    stk.gthreads = (uint64_t)gridDim.x * kWT;
+    stk.spill = spill + (uint64_t)blockIdx.x * kWT + lane;
     const WScene sc = load_wscene(a);
     const uint32_t n = counts[depth];
     const float t_lo = depth ? kBounceTLo : 0.0f;
@@ -253,8 +291,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
                 d[k] = qin.p[(3 + k) * qin.cap + i];
             }
             sid = sid_in[i];
-            closest_walk(sc, o[0], o[1], o[2], d[0], d[1], d[2], t_lo, bt, bi, s_node + lane, s_min + lane,
-                         s_max + lane);
+            closest_walk(sc, o[0], o[1], o[2], d[0], d[1], d[2], t_lo, bt, bi, stk);
         }
         const bool hit = valid && bi != kNoHit;
         if (hit) hits[sid] = (uint8_t)(depth + 1);
@@ -321,7 +358,19 @@ __global__ void __launch_bounds__(256) k_wh_shade(const RenderArgs a, const uint
 
 }  // namespace
 
-size_t whitted_bytes(uint64_t rays) { return 2 * (7 * rays * 4) + rays + 64; }
+static uint32_t whitted_grid(uint64_t rays) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t need = (rays + kWT - 1) / kWT, cap = (uint64_t)(cus > 0 ? cus : 256) * kWBlocksPerCU;
+    return (uint32_t)(need < cap ? need : cap);
+}
+
+// two queues of 7 planes, 16 counters, per-sample hits (u8), the stack spill
+size_t whitted_bytes(uint64_t rays) {
+    const uint64_t q = 2 * 7 * rays * 4, hits = (rays + 255) & ~255ull;
+    return q + 64 + hits + (uint64_t)whitted_grid(rays) * kWT * (kWStack - kWLds) * 3 * 4;
+}
 
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
                    void *ev_k1) {
@@ -331,17 +380,14 @@ int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hi
     WQueue q0{base, rays}, q1{base + 7 * rays, rays};
     uint32_t *counts = reinterpret_cast<uint32_t *>(base + 14 * rays);
     uint8_t *hits = reinterpret_cast<uint8_t *>(counts + 16);
+    uint32_t *spill = reinterpret_cast<uint32_t *>(hits + ((rays + 255) & ~255ull));
     hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits);
     hipError_t e = ev_k0 ? hipEventRecord((hipEvent_t)ev_k0, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t need = (rays + kWT - 1) / kWT;
-    const uint32_t grid = (uint32_t)(need < (uint64_t)cus * 16 ? need : (uint64_t)cus * 16);
+    const uint32_t grid = whitted_grid(rays);
     for (uint32_t d = 0; d <= 8; ++d)
         hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1,
-                           counts, hits);
+                           counts, hits, spill);
     e = ev_k1 ? hipEventRecord((hipEvent_t)ev_k1, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
     const uint64_t P = (uint64_t)a.nrows * a.w;

@@ -517,8 +517,11 @@ static int traverse_gpu_ref(const ob_tree *T, const ray_t *r, cnt_t *c, int anyh
     return rec.idx >= 0;
 }
 
-/* The reference walk's visit set (traverse_gpu_ref's decisions, no early
- * exit) with the C4 closest-hit rule at its leaves. */
+/* The reference walk (traverse_gpu_ref's decisions and order) with the C4
+ * closest-hit rule at its leaves and front-to-back culling: before each node
+ * a node entered beyond the best hit so far (tMin > best) is popped, and tMax
+ * is clamped to the best hit (tMax = min(tMax, best), best = +inf until the
+ * first hit, so the walk is the reference's until then). */
 static void traverse_closest(const ob_tree *T, const ray_t *r, float t_lo, float *bt, int32_t *bi,
                              cnt_t *c) {
     *bt = FLT_MAX; *bi = -1;
@@ -532,6 +535,13 @@ static void traverse_closest(const ob_tree *T, const ray_t *r, float t_lo, float
     stack[sp].node = -1; sp++;
     int cur = 0;
     while (cur != -1) {
+        const float best = *bi >= 0 ? *bt : INFINITY;
+        if (tMin > best) {                       /* entered beyond the best hit: skip */
+            sp--;
+            cur = stack[sp].node; tMin = stack[sp].tmin; tMax = stack[sp].tmax;
+            continue;
+        }
+        if (best < tMax) tMax = best;
         c->nodes++;
         int ax = T->axis[cur];
         float org = r->o[ax], inv = r->inv[ax];

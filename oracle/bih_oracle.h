@@ -88,9 +88,11 @@ int ob_render(const ob_tree *t, const float cam[12], uint32_t w, uint32_t h,
  * build-defined extension (the reference has no secondary rays,
  * CUDAKernels.cu:370-389); semantics, all f32 without contraction:
  *   closest hit of a ray = min (t, sorted position i) over the triangles the
- *     reference walk visits (TraverseTree's visit set, CUDAKernels.cu:227-368;
- *     RayTriangleIntersection :17-50) with OB_WHITTED_TMIN[depth] < t < FLT_MAX
- *     (depth 0: t > 0 as FindNearestTriangle :212; bounces: t > 1e-4);
+ *     reference walk tests (TraverseTree's decisions and order,
+ *     CUDAKernels.cu:227-368; RayTriangleIntersection :17-50) with
+ *     t_lo < t < FLT_MAX (depth 0: t > 0 as FindNearestTriangle :212;
+ *     bounces: t > 1e-4), where the walk culls front to back once it has a
+ *     hit: before each node, pop if tMin > best, else tMax = min(tMax, best);
  *   hit point P = O + t*D; n = cross(e1, e2) (glm order, e = v - v0 of the
  *     original triangle); k = (2*dot(D, n)) / dot(n, n); R = D - k*n;
  *   shade(d) = miss ? (20,20,40) : d == 8 ? (255,255,0)

@@ -10,11 +10,12 @@ print("value %.4g rays/s  ms/step %.4f  n_gpus %s  scaling %s" % (d["value"], d[
 print("roofline frac %s  frac_algorithmic %s  launch_ms %s" % (rf.get("frac"), rf.get("frac_algorithmic"),
                                                                rf.get("launch_ms")))
 for k in ("one_in_flight", "moving_camera", "with_rebuild", "other_traversal", "band_share",
-          "other_decomposition"):
+          "other_decomposition", "whitted_c4"):
     v = d.get(k)
     if v:
         print(k, {kk: v[kk] for kk in v if kk in ("value", "ms_per_step", "projected_efficiency",
-                                                  "share_ms_per_step", "build_ms", "kernel_ms")})
+                                                  "share_ms_per_step", "build_ms", "kernel_ms",
+                                                  "ms_per_frame", "rays_traced_per_s")})
 c = d.get("cpu_baseline")
 if c:
     print("cpu", c["value"], c["cores"], c.get("cpu_model"), c.get("affinity_cpus"))
