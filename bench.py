@@ -72,6 +72,8 @@ def parse():
                          "(child processes, before this process touches the GPU)")
     ap.add_argument("--kernel-samples", type=int, default=20,
                     help="isolated launches timed with the library's kernel events (roofline launch_ms)")
+    ap.add_argument("--step-events", type=int, default=0,
+                    help="record torch events around every timed render (kernel_ms per leg)")
     ap.add_argument("--whitted-frames", type=int, default=3,
                     help="N=1: frames of config C4 (8-bounce Whitted, 3840x2160, same soup) to time; 0 = skip")
     ap.add_argument("--no-reference-leg", action="store_true")
@@ -152,6 +154,11 @@ def main():
     def step(mode, rows, k, frame, traverse, ev=None, rebuild=False, nf=F):
         j = k % nf
         s = streams[j]
+        if ev is None and not rebuild and not (mode == "strong" and world > 1):
+            # the render alone: no torch work on the stream, no stream context
+            r.render_device(outs[j].data_ptr(), frame, rows=rows, traverse=traverse,
+                            stream=s.cuda_stream)
+            return
         with torch.cuda.stream(s):
             if rebuild:
                 arrays.rebuild()
@@ -181,16 +188,18 @@ def main():
         for k in range(args.warmup):
             step(mode, rows, k, frame_of(base, k), traverse, rebuild=rebuild, nf=nf)
         sync_all()
+        # per-step torch events only when asked (--step-events): recording them
+        # costs host time per frame, which the row-band shares feel
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
+               for _ in range(args.steps)] if args.step_events else []
         t0 = time.perf_counter()
         for k in range(args.steps):
-            step(mode, rows, args.warmup + k, frame_of(base, args.warmup + k), traverse, evs[k],
-                 rebuild=rebuild, nf=nf)
+            step(mode, rows, args.warmup + k, frame_of(base, args.warmup + k), traverse,
+                 evs[k] if evs else None, rebuild=rebuild, nf=nf)
         sync_all()
         el = max_over_ranks(time.perf_counter() - t0)
-        kms = [a.elapsed_time(b) for a, b in evs]
-        return el, sum(kms) / len(kms), fps
+        kms = [a.elapsed_time(b) for a, b in evs] if evs else []
+        return el, (sum(kms) / len(kms) if kms else None), fps
 
     mode = args.mode if world > 1 else "weak"
     rows, frame_of, _ = plan(mode)
@@ -258,12 +267,14 @@ def main():
         traced = int(torch.clamp(whits.to(torch.int64) + 1, max=9).sum())
         hist = torch.bincount(whits.view(-1), minlength=10).tolist()
         del whits
+        rw.set_timing(True)
         t0 = time.perf_counter()
         for k in range(args.whitted_frames):
             rw.render_whitted_device(wout.data_ptr(), 1 + k, stream=sptr)
         torch.cuda.synchronize()
         wel = (time.perf_counter() - t0) / args.whitted_frames
         wk, _ = rw.last_render_times()
+        rw.set_timing(False)
         whitted_leg = {"config": "C4: 1M soup, 3840x2160, 4 spp, 8 bounces of mirror rays",
                        "ms_per_frame": 1e3 * wel, "primary_rays_per_s": WW * WH * SPP / wel,
                        "rays_traced_per_frame": traced, "rays_traced_per_s": traced / wel,
@@ -330,11 +341,15 @@ def main():
     # on the render stream right around the render kernel (bih_last_render_ms),
     # over isolated launches (each frame synchronised before the next) -- the
     # figure rocprofv3's kernel trace reports for the same kernel
-    kms_iso = []
+    kms_iso, tails_iso = [], []
+    r.set_timing(True)
     for k in range(args.kernel_samples):
         step(mode, rows, k, frame_of(5000, k), trav, nf=1)
         torch.cuda.synchronize()
-        kms_iso.append(r.last_render_ms())
+        km, tm = r.last_render_times()
+        kms_iso.append(km)
+        tails_iso.append(tm)
+    r.set_timing(False)
     kernel_launch_ms = sum(kms_iso) / len(kms_iso) if kms_iso else None
 
     # per-ray work counters of one frame (untimed): exact integers, equal to
@@ -428,6 +443,7 @@ def main():
                 "algorithmic": alg,
                 "frac_algorithmic": alg["gbs"] / HBM_PEAK_GBS if alg else None,
                 "launch_ms": launch_ms,
+                "fallback_ms": (sum(tails_iso) / len(tails_iso)) if tails_iso else None,
                 "launch_ms_source": (f"HIP events around the render kernel on its stream "
                                      f"(bih_last_render_ms), mean of {len(kms_iso)} isolated launches")
                                     if kernel_launch_ms else "headline leg",

@@ -183,6 +183,10 @@ class Renderer:
     def sync(self, stream: int | None = None):
         check(load().bih_sync(self.arrays.handle, C.c_void_p(stream or 0)), "bih_sync")
 
+    def set_timing(self, on: bool = True):
+        """Record device-time events around every render (bih_set_timing)."""
+        check(load().bih_set_timing(self.arrays.handle, 1 if on else 0), "bih_set_timing")
+
     def last_render_ms(self) -> float:
         ms = C.c_double(0.0)
         check(load().bih_last_render_ms(self.arrays.handle, C.byref(ms)), "bih_last_render_ms")

@@ -129,11 +129,12 @@ def load():
                                             C.POINTER(Rows), vp, vp, vp]
     L.bih_render_whitted.argtypes = [C.POINTER(Scene), vp, C.POINTER(Camera), C.POINTER(Framebuffer)]
     L.bih_last_render_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.bih_set_timing.argtypes = [vp, i32]
     L.bih_last_render_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.bih_bins_get_stats.argtypes = [vp, C.POINTER(BinsStats)]
     for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
-                 "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_last_render_times",
+                 "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_last_render_times", "bih_set_timing",
                  "bih_render_whitted_device", "bih_render_whitted",
                  "bih_bins_get_stats"):
         getattr(L, name).restype = i32

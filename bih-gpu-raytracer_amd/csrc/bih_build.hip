@@ -128,7 +128,27 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
         hdr->n_unique = 0;
         hdr->nonfinite = 0;
         hdr->pad0 = 0;
+        hdr->content = 0ull;
     }
+}
+
+// Hash of the input soup: XOR over words of splitmix64(index << 32 | bits).
+// The build is a deterministic function of the soup, so an unchanged hash
+// after a rebuild means an unchanged tree, and the per-camera structures
+// derived from it (bih_capi.cpp finish_build) stay valid.
+__global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__restrict__ v, uint64_t words,
+                                                           TreeHeader *hdr) {
+    unsigned long long x = 0ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < words;
+         i += (uint64_t)gridDim.x * kThreads) {
+        unsigned long long z = (i << 32) ^ v[i];
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        x ^= z ^ (z >> 31);
+    }
+    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+    if ((threadIdx.x & 63) == 0 && x) atomicXor(&hdr->content, x);
 }
 
 __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
@@ -791,6 +811,10 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
         hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.v, t.vals, n,
                            t.tris_s);
+        const uint64_t words = 9ull * n;
+        const uint64_t hb = (words + kThreads - 1) / kThreads;
+        hipLaunchKernelGGL(k_content_hash, dim3((uint32_t)(hb < 2048 ? hb : 2048)), dim3(kThreads), 0, st,
+                           reinterpret_cast<const uint32_t *>(t.v), words, t.hdr);
         BIH_TRY(hipGetLastError());
     }
     BIH_TRY(hipEventRecord(e1, st));
@@ -803,6 +827,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     (void)hipEventDestroy(e1);
     if (ms_out) *ms_out = ms;
     t.u = h.n_unique;
+    t.content = h.content;
     if (h.nonfinite) return -1000;   // mapped to BIH_ERR_NONFINITE by the C ABI
     return 0;
 }

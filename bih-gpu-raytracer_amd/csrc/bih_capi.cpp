@@ -39,7 +39,11 @@ struct bih_tree {
     // ev0/ev1: the render kernel's start and end (bih_last_render_ms); evd:
     // everything the render issued is done (ordering of slot reuse, rebuilds)
     hipEvent_t ev0[kSlots] = {}, ev1[kSlots] = {}, evd[kSlots] = {};
+    hipEvent_t ev2[kSlots] = {};     // end of the render's device work (timed renders only)
     bool used[kSlots] = {};
+    bool timing = false;             // bih_set_timing: record ev0/ev1/ev2 around each render
+    bool last_timed = false;
+    bool built = false;              // a build completed (t.content is its soup's hash)
     int slot = 0;                    // slot of the next render
     int last_slot = -1;              // slot of the last render
     // After the last write to state every render reads, whichever stream
@@ -223,12 +227,23 @@ int finish_build(bih_tree *tr) {
     int rc = wait_renders(tr, tr->stream);
     if (rc) return rc;
     float ms = 0.f;
+    const bool had = tr->built;
+    const uint64_t old_content = tr->t.content;
+    const uint32_t old_n = tr->t.n, old_u = tr->t.u;
     int e = bih::build_tree_device(tr->t, tr->stream, &ms);
     tr->build_ms = ms;
+    tr->built = e == 0;
     // the per-pixel RNG state does not depend on the geometry: a rebuild (the
-    // reference rebuilds every frame) keeps the frame sequence going
-    tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
-    tr->bins_valid = false;
+    // reference rebuilds every frame) keeps the frame sequence going.  The
+    // per-camera structures (triangle and node records, shortcut boxes,
+    // frustum bins, tile queues) are functions of the tree, and the tree of
+    // the soup: a rebuild of an unchanged soup (same content hash, N and U;
+    // the tree is bit-identical) keeps them
+    const bool same = had && e == 0 && tr->t.content == old_content && tr->t.n == old_n && tr->t.u == old_u;
+    if (!same) {
+        tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
+        tr->bins_valid = false;
+    }
     if (e) return map_hip(e);
     // renders issued on other streams order after the (re)build; tr->stream
     // waited for every render above, so this also follows the last advance
@@ -252,7 +267,8 @@ int create_tree(int device, void *stream, bih_tree **out) {
     for (int k = 0; k < kSlots && e == hipSuccess; ++k) {
         e = hipEventCreate(&tr->ev0[k]);
         if (e == hipSuccess) e = hipEventCreate(&tr->ev1[k]);
-        if (e == hipSuccess) e = hipEventCreate(&tr->evd[k]);   // timed: bih_last_render_times
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->evd[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreate(&tr->ev2[k]);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_bins, hipEventDisableTiming);
@@ -414,6 +430,7 @@ void bih_free(bih_tree *tr) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
         if (tr->evd[k]) (void)hipEventDestroy(tr->evd[k]);
         if (tr->ev1[k]) (void)hipEventDestroy(tr->ev1[k]);
+        if (tr->ev2[k]) (void)hipEventDestroy(tr->ev2[k]);
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
     if (tr->ev_bins) (void)hipEventDestroy(tr->ev_bins);
@@ -974,9 +991,15 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     a.ray_stats = d_ray_stats;
     a.work = tr->work + (size_t)slot * bih::kWorkWords;
     a.spill = tr->spill + (size_t)slot * tr->spill_per_slot;
-    rc = bih::launch_render(a, traverse, st, tr->ev0[slot], tr->ev1[slot]);
+    rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
+                            tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
     if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
+    if (tr->timing) {
+        e = hipEventRecord(tr->ev2[slot], st);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    tr->last_timed = tr->timing;
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
@@ -1052,8 +1075,14 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     a.rng_in = rng_buf(tr, cur);
     a.out = d_out;
     const int slot = tr->slot;
-    rc = bih::launch_whitted(a, tr->wh_mem, rays, d_hits, st, tr->ev0[slot], tr->ev1[slot]);
+    rc = bih::launch_whitted(a, tr->wh_mem, rays, d_hits, st, tr->timing ? tr->ev0[slot] : nullptr,
+                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
+    if (tr->timing) {
+        e = hipEventRecord(tr->ev2[slot], st);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    tr->last_timed = tr->timing;
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
@@ -1224,8 +1253,15 @@ int bih_sync(const bih_tree *tr, void *stream) {
     return map_hip((int)hipStreamSynchronize(st));
 }
 
+int bih_set_timing(bih_tree *tr, int on) {
+    if (!tr) return BIH_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(tr->mu);
+    tr->timing = on != 0;
+    return BIH_OK;
+}
+
 int bih_last_render_ms(const bih_tree *tr, double *ms) {
-    if (!tr || !ms || tr->last_slot < 0) return BIH_ERR_INVALID;
+    if (!tr || !ms || tr->last_slot < 0 || !tr->last_timed) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     const int k = tr->last_slot;
     hipError_t e = hipEventSynchronize(tr->evd[k]);
@@ -1238,14 +1274,14 @@ int bih_last_render_ms(const bih_tree *tr, double *ms) {
 }
 
 int bih_last_render_times(const bih_tree *tr, double *kernel_ms, double *tail_ms) {
-    if (!tr || !kernel_ms || !tail_ms || tr->last_slot < 0) return BIH_ERR_INVALID;
+    if (!tr || !kernel_ms || !tail_ms || tr->last_slot < 0 || !tr->last_timed) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     const int k = tr->last_slot;
     hipError_t e = hipEventSynchronize(tr->evd[k]);
     if (e != hipSuccess) return map_hip((int)e);
     float f0 = 0.f, f1 = 0.f;
     e = hipEventElapsedTime(&f0, tr->ev0[k], tr->ev1[k]);
-    if (e == hipSuccess) e = hipEventElapsedTime(&f1, tr->ev1[k], tr->evd[k]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&f1, tr->ev1[k], tr->ev2[k]);
     if (e != hipSuccess) return map_hip((int)e);
     *kernel_ms = f0;
     *tail_ms = f1;

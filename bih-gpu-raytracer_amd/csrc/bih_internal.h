@@ -58,6 +58,7 @@ struct TreeHeader {
     uint32_t pad0;
     unsigned long long lo_key[3];   // argmin keys (App.cpp:133-137 tie rules)
     unsigned long long hi_key[3];   // argmax keys
+    unsigned long long content;     // hash of the input soup (k_content_hash): the tree is a function of it
 };
 
 // Render parameters, passed by value.
@@ -140,6 +141,7 @@ struct BinBuffers {
 struct DeviceTree {
     int device = 0;
     uint32_t n = 0, u = 0;
+    uint64_t content = 0;          // TreeHeader::content of the last build
     size_t bytes = 0;
     float *v = nullptr;            // input soup f32[9N] (device copy)
     bool owns_v = false;

@@ -187,9 +187,12 @@ int bih_render_whitted_device(const bih_tree *tree, const bih_camera *camera, ui
 int bih_render_whitted(const bih_scene *scene, const bih_tree *tree, const bih_camera *camera,
                        bih_framebuffer *fb);
 
-/* Device time (ms, HIP events on the render stream, recorded right before
- * and after the main render kernel) of the last render launched through this
- * tree. */
+/* Per-render device timing (HIP events on the render stream around the main
+ * render kernel and at the end of the render's device work), off by default:
+ * the events cost host time on every render call.  bih_last_render_ms gives
+ * the main kernel's device time (ms) of the last render, which must have been
+ * issued with timing on (else BIH_ERR_INVALID). */
+int bih_set_timing(bih_tree *tree, int on);
 int bih_last_render_ms(const bih_tree *tree, double *ms);
 /* The same render split in two: *kernel_ms as bih_last_render_ms (the main
  * render kernel, the figure rocprofv3 reports for it) and *tail_ms from its

@@ -26,6 +26,7 @@ def main():
     d = torch.from_numpy(tris).cuda()
     g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=s.cuda_stream)
     r = bihrt.Renderer(g, a.width, a.height)
+    r.set_timing(True)
     P = a.width * a.height
     out = torch.zeros(P, dtype=torch.int32, device="cuda")
     hits = torch.zeros(P * 4, dtype=torch.int32, device="cuda")
