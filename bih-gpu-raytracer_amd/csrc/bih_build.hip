@@ -15,6 +15,8 @@
 // Everything is integer/byte work or exact f32 compares; all arithmetic is
 // compiled with -ffp-contract=off so it matches the strict-IEEE oracle.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <float.h>
 
 #include "bih_internal.h"
@@ -132,23 +134,33 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
     }
 }
 
-// Hash of the input soup: XOR over words of splitmix64(index << 32 | bits).
-// The build is a deterministic function of the soup, so an unchanged hash
-// after a rebuild means an unchanged tree, and the per-camera structures
-// derived from it (bih_capi.cpp finish_build) stay valid.
-__global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__restrict__ v, uint64_t words,
+// Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
+// (32-bit arithmetic: HBM-bound).  The build is a deterministic function of
+// the soup, so an unchanged hash after a rebuild means an unchanged tree, and
+// the per-camera structures derived from it (bih_capi.cpp finish_build) stay
+// valid.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+__global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__restrict__ v, uint32_t words,
                                                            TreeHeader *hdr) {
-    unsigned long long x = 0ull;
-    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < words;
-         i += (uint64_t)gridDim.x * kThreads) {
-        unsigned long long z = (i << 32) ^ v[i];
-        z += 0x9E3779B97F4A7C15ull;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        x ^= z ^ (z >> 31);
+    uint32_t x = 0u, y = 0u;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < words; i += gridDim.x * kThreads) {
+        const uint32_t w = v[i];
+        x ^= fmix32(w ^ (i * 0x9E3779B1u));
+        y ^= fmix32((w + 0x165667B1u) ^ fmix32(i + 0x27D4EB2Fu));
     }
-    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
-    if ((threadIdx.x & 63) == 0 && x) atomicXor(&hdr->content, x);
+    for (int o = 32; o > 0; o >>= 1) {
+        x ^= __shfl_xor(x, o);
+        y ^= __shfl_xor(y, o);
+    }
+    if ((threadIdx.x & 63) == 0 && (x | y))
+        atomicXor(&hdr->content, ((unsigned long long)y << 32) | x);
 }
 
 __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
@@ -227,7 +239,7 @@ __global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ l
 }
 
 // ---------------------------------------------------------------------------
-// Device-wide exclusive scan of u32 (reduce-then-scan, 3 launches).
+// Device-wide exclusive scan of u32 (one launch, decoupled look-back).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *lds, uint32_t *total) {
     // 256 threads = 4 waves
@@ -252,65 +264,80 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *l
     return wbase + inc - x;
 }
 
-__global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t *__restrict__ in, uint32_t n,
-                                                          uint32_t *__restrict__ partials) {
-    __shared__ uint32_t lds[4];
-    uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        uint64_t i = base + (uint64_t)k * kThreads + threadIdx.x;
-        s += (i < n) ? in[i] : 0u;
-    }
-    uint32_t tot;
-    block_exclusive_scan(s, lds, &tot);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+// Single-pass scan with decoupled look-back: tile t publishes its aggregate,
+// adds its predecessors' published values walking back until one carries an
+// inclusive prefix, then publishes its own inclusive prefix.  A status word is
+// {tag:30 | flag:2 | value:32}, flag 1 = aggregate, 2 = inclusive prefix; the
+// tag is unique per scan call (host counter), so no status memset is needed
+// between calls.  Tiles are blockIdx.x: workgroups dispatch in id order, so
+// every tile a block waits for is resident or done.
+constexpr uint32_t kScanAgg = 1u, kScanPre = 2u;
+__device__ __forceinline__ unsigned long long scan_word(uint32_t tag, uint32_t flag, uint32_t v) {
+    return ((unsigned long long)((tag << 2) | flag) << 32) | v;
 }
 
-__global__ void __launch_bounds__(kThreads) k_scan_partials(uint32_t *partials, uint32_t nparts,
-                                                            uint32_t *total_out) {
+__global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, uint32_t *out, uint32_t n,
+                                                           unsigned long long *status, uint32_t tag,
+                                                           uint32_t *total_out) {
     __shared__ uint32_t lds[4];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nparts; base += kThreads) {
-        uint32_t i = base + threadIdx.x;
-        uint32_t x = i < nparts ? partials[i] : 0u;
-        uint32_t tot;
-        uint32_t ex = block_exclusive_scan(x, lds, &tot);
-        if (i < nparts) partials[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0 && total_out) *total_out = carry;
-}
-
-__global__ void __launch_bounds__(kThreads) k_scan_down(const uint32_t *in, uint32_t *out, uint32_t n,
-                                                        const uint32_t *__restrict__ partials) {
-    __shared__ uint32_t lds[4];
-    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    __shared__ uint32_t s_prefix;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     uint32_t x[kScanItems];
-    uint32_t s = 0;
+    uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
-        uint64_t i = base + k;
+        const uint64_t i = base + k;
         x[k] = (i < n) ? in[i] : 0u;
-        s += x[k];
+        sum += x[k];
     }
     uint32_t tot;
-    uint32_t run = block_exclusive_scan(s, lds, &tot) + partials[blockIdx.x];
+    const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
+    if (threadIdx.x == 0) {
+        uint32_t prefix = 0;
+        if (tile == 0) {
+            __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t j = tile - 1;;) {
+                const unsigned long long w =
+                    __hip_atomic_load(status + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t hi = (uint32_t)(w >> 32);
+                if ((hi >> 2) != tag || (hi & 3u) == 0u) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                prefix += (uint32_t)w;
+                if ((hi & 3u) == kScanPre) break;
+                --j;
+            }
+            __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_prefix = prefix;
+        if (tile == gridDim.x - 1 && total_out) *total_out = prefix + tot;
+    }
+    __syncthreads();
+    uint32_t run = s_prefix + ex;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
-        uint64_t i = base + k;
+        const uint64_t i = base + k;
         if (i < n) out[i] = run;
         run += x[k];
     }
 }
 
+std::atomic<uint32_t> g_scan_tag{0};
+
+// `partials`: scan_partials_words(n) u32 words, 8-byte aligned (status words)
 hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                           uint32_t *total_dev, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    uint32_t nb = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kThreads), 0, st, in, n, partials);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kThreads), 0, st, partials, nb, total_dev);
-    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(kThreads), 0, st, in, out, n, partials);
+    const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+    const uint32_t tag = ((g_scan_tag.fetch_add(1) % 0x3FFFFFFFu) + 1u);   // 1 .. 2^30-1
+    hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kThreads), 0, st, in, out, n,
+                       reinterpret_cast<unsigned long long *>(partials), tag, total_dev);
     return hipGetLastError();
 }
 
@@ -705,7 +732,7 @@ int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *part
                    uint32_t *total_dev, void *stream) {
     return (int)exclusive_scan(in, out, n, partials, total_dev, (hipStream_t)stream);
 }
-size_t scan_partials_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+size_t scan_partials_words(uint32_t n) { return 2 * (size_t)((n + kScanTile - 1) / kScanTile) + 2; }
 
 void free_tree_device(DeviceTree &t) {
     void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
@@ -756,7 +783,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.nodes, nn, b));
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
         BIH_TRY(dalloc(&t.hist, hist_n, b));
-        BIH_TRY(dalloc(&t.partials, (uint64_t)max_parts + 1, b));
+        BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, b));   // k_scan_onepass status words
         BIH_TRY(dalloc(&t.prep_part, 6ull * kPrepBlocks, b));
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -811,9 +838,9 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
         hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.v, t.vals, n,
                            t.tris_s);
-        const uint64_t words = 9ull * n;
-        const uint64_t hb = (words + kThreads - 1) / kThreads;
-        hipLaunchKernelGGL(k_content_hash, dim3((uint32_t)(hb < 2048 ? hb : 2048)), dim3(kThreads), 0, st,
+        const uint32_t words = 9u * n;     // n <= BIH_MAX_TRIS = 2^27
+        const uint32_t hb = (words + kThreads - 1) / kThreads;
+        hipLaunchKernelGGL(k_content_hash, dim3(hb < 4096u ? hb : 4096u), dim3(kThreads), 0, st,
                            reinterpret_cast<const uint32_t *>(t.v), words, t.hdr);
         BIH_TRY(hipGetLastError());
     }
