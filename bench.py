@@ -54,6 +54,13 @@ def parse():
                     help="N > 1: row bands of every frame + RCCL gather to rank 0 (strong, the "
                          "north star's decomposition) or whole frames per rank (weak) as the "
                          "headline; the other runs as a side leg")
+    ap.add_argument("--gather-packed", type=int, default=1,
+                    help="N > 1 strong: send the bands as 4-bit hit counts (8x fewer bytes over "
+                         "xGMI; rank 0 expands them to the same RGBA words); needs spp 4")
+    ap.add_argument("--group", type=int, default=8,
+                    help="consecutive frames per render call (bih_render_device_frames: one launch "
+                         "of each kernel for the group; each frame is still the reference's frame "
+                         "at its index); the with_rebuild and moving_camera legs use 1")
     ap.add_argument("--share-world", type=int, default=8,
                     help="N=1: time each of the bands one of this many GPUs would render (the "
                          "strong decomposition's per-rank work) -> projected per-GPU efficiency")
@@ -133,43 +140,62 @@ def main():
     info = arrays.info()
     cam = bihrt.camera_reference(W, H)
     r = bihrt.Renderer(arrays, W, H, spp=SPP, seed=1984, camera=cam)
-    # weak: this rank renders whole frames; strong: its bands of every frame
+    # weak: this rank renders whole frames; strong: its bands of every frame.
+    # A render call covers G consecutive frames (--group, bih_render_device_frames):
+    # frame f of a call at out + f * stride, stride = the rank's padded rows.
+    G = max(1, args.group)
     mrows = max_rows(H, args.band, world)
-    outs = [torch.zeros(H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
+    outs = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
     out = outs[0]
     if world > 1:
-        # one gather (and receive buffer on rank 0) per frame in flight
-        gathers = [BandGather(dist, H, W, args.band, rank, world, torch.device("cuda", local))
+        # one gather (and receive buffer on rank 0) per call in flight; a call's
+        # G frames travel as one message
+        packed = bool(args.gather_packed) and SPP == 4 and W % 8 == 0
+        gathers = [BandGather(dist, H, W, args.band, rank, world, torch.device("cuda", local), frames=G,
+                              packed=packed)
                    for _ in range(F)]
-        frame_img = [torch.zeros(H * W, dtype=torch.int32, device="cuda") if rank == 0 else None
+        frame_img = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") if rank == 0 else None
                      for _ in range(F)]
     trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 
-    def plan(mode):
-        """(rows of this rank, frame index of step k from `base`, frames per step job-wide)"""
+    def plan(mode, g=G):
+        """(rows of this rank, first frame of the call at step k from `base`, frames per step job-wide)"""
         if mode == "weak" or world == 1:
-            return band_rows(H, args.band, 0, 1), (lambda base, k: frame_of_step(base, k, rank, world)), world
+            return (band_rows(H, args.band, 0, 1),
+                    (lambda base, k: frame_of_step(base, k, rank, world, g)), world)
         return band_rows(H, args.band, rank, world), (lambda base, k: base + k), 1
 
-    def step(mode, rows, k, frame, traverse, ev=None, rebuild=False, nf=F):
+    def step(mode, rows, k, frame, traverse, ev=None, rebuild=False, nf=F, m=1):
+        """One render call: frames frame .. frame+m-1 (call index k)."""
         j = k % nf
         s = streams[j]
+        o = outs[j].data_ptr()
+        # frames of a call packed at the rank's padded rows (the gather sends them as one block)
+        stride = (mrows if (mode == "strong" and world > 1) else H) * W
+
+        def render():
+            if m == 1:
+                r.render_device(o, frame, rows=rows, traverse=traverse, stream=s.cuda_stream)
+            elif traverse == bihrt.TRAVERSE_ANYHIT:
+                r.render_device_frames(o, frame, m, stride, rows=rows, stream=s.cuda_stream)
+            else:
+                for f in range(m):
+                    r.render_device(o + 4 * f * stride, frame + f, rows=rows, traverse=traverse,
+                                    stream=s.cuda_stream)
+
         if ev is None and not rebuild and not (mode == "strong" and world > 1):
-            # the render alone: no torch work on the stream, no stream context
-            r.render_device(outs[j].data_ptr(), frame, rows=rows, traverse=traverse,
-                            stream=s.cuda_stream)
+            render()     # the render alone: no torch work on the stream, no stream context
             return
         with torch.cuda.stream(s):
             if rebuild:
                 arrays.rebuild()
             if ev is not None:
                 ev[0].record(s)
-            r.render_device(outs[j].data_ptr(), frame, rows=rows, traverse=traverse,
-                            stream=s.cuda_stream)
+            render()
             if ev is not None:
                 ev[1].record(s)
             if mode == "strong" and world > 1:
-                # frame k's gather runs on stream j while frame k+1 renders on j+1
+                # call k's gather runs on stream j while call k+1 renders on j+1
                 gathers[j](outs[j], frame_img[j])
 
     def sync_all():
@@ -183,22 +209,27 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def timed(mode, traverse, base, rebuild=False, nf=F):
-        rows, frame_of, fps = plan(mode)
-        for k in range(args.warmup):
-            step(mode, rows, k, frame_of(base, k), traverse, rebuild=rebuild, nf=nf)
+    def timed(mode, traverse, base, rebuild=False, nf=F, g=G):
+        """Times exactly args.steps frames per rank (calls of g frames; the
+        last call takes the remainder)."""
+        rows, frame_of, fps = plan(mode, g)
+        for k in range(0, args.warmup, g):
+            step(mode, rows, k // g, frame_of(base, k), traverse, rebuild=rebuild, nf=nf,
+                 m=min(g, args.warmup - k))
         sync_all()
-        # per-step torch events only when asked (--step-events): recording them
-        # costs host time per frame, which the row-band shares feel
+        # per-call torch events only when asked (--step-events): recording them
+        # costs host time per call, which the row-band shares feel
+        ncalls = (args.steps + g - 1) // g
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)] if args.step_events else []
+               for _ in range(ncalls)] if args.step_events else []
+        k0 = ((args.warmup + g - 1) // g) * g
         t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(mode, rows, args.warmup + k, frame_of(base, args.warmup + k), traverse,
-                 evs[k] if evs else None, rebuild=rebuild, nf=nf)
+        for c, k in enumerate(range(0, args.steps, g)):
+            step(mode, rows, (k0 + k) // g, frame_of(base, k0 + k), traverse,
+                 evs[c] if evs else None, rebuild=rebuild, nf=nf, m=min(g, args.steps - k))
         sync_all()
         el = max_over_ranks(time.perf_counter() - t0)
-        kms = [a.elapsed_time(b) for a, b in evs] if evs else []
+        kms = [a.elapsed_time(b) / g for a, b in evs] if evs else []
         return el, (sum(kms) / len(kms) if kms else None), fps
 
     mode = args.mode if world > 1 else "weak"
@@ -238,12 +269,13 @@ def main():
         shares = []
         for q in range(Q):
             rows_q = band_rows(H, args.band, q, Q)
-            for k in range(args.warmup):
-                step("weak", rows_q, k, 7000 + k, trav)
+            for k in range(0, args.warmup, G):
+                step("weak", rows_q, k // G, 7000 + k, trav, m=min(G, args.warmup - k))
             sync_all()
+            k0 = ((args.warmup + G - 1) // G) * G
             t0 = time.perf_counter()
-            for k in range(args.steps):
-                step("weak", rows_q, args.warmup + k, 7000 + args.warmup + k, trav)
+            for k in range(0, args.steps, G):
+                step("weak", rows_q, (k0 + k) // G, 7000 + k0 + k, trav, m=min(G, args.steps - k))
             sync_all()
             shares.append(1e3 * (time.perf_counter() - t0) / args.steps)
         share_leg = {"world": Q, "band": args.band, "share_ms_per_step": shares,
@@ -330,7 +362,7 @@ def main():
     # Renderer.cpp:415-503): time rebuild + render per step as well
     rebuild_leg = None
     if not args.no_rebuild_leg:
-        el3, _, fps3 = timed(mode, trav, 2000, rebuild=True)
+        el3, _, fps3 = timed(mode, trav, 2000, rebuild=True, g=1)
         rebuild_leg = {"value": fps3 * rays_per_frame * args.steps / el3, "unit": "rays/s",
                        "ms_per_step": 1e3 * el3 / args.steps,
                        "build_ms": arrays.info().build_ms,
@@ -424,6 +456,7 @@ def main():
                 "spp": SPP, "traverse": args.traverse,
                 "parallelism": parallelism(mode, args.band, world),
                 "frames_in_flight": F,
+                "frames_per_call": G,
             },
             "kernel_ms": kernel_ms,
             "build_ms": info.build_ms,
@@ -489,9 +522,9 @@ def parallelism(mode, band, world):
     if world == 1:
         return "1 GPU, whole frames"
     if mode == "weak":
-        return f"whole frames round-robin over {world} GPUs (rank r: frames r, r+{world}, ...), no collective"
+        return f"whole frames in groups of consecutive frames, round-robin over {world} GPUs, no collective"
     return (f"row bands of {band} rows interleaved over {world} GPUs + one RCCL gather of the bands "
-            "to rank 0 per frame")
+            "to rank 0 per render call")
 
 
 def cpu_model():

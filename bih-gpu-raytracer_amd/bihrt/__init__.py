@@ -158,6 +158,16 @@ class Renderer:
                                        C.c_void_p(out_ptr), C.c_void_p(stats_ptr or 0),
                                        C.c_void_p(stream or 0)), "bih_render_device")
 
+    def render_device_frames(self, out_ptr: int, frame0: int, nframes: int, out_stride: int,
+                             rows: Rows | None = None, stream: int | None = None):
+        """Frames frame0 .. frame0+nframes-1 (any-hit) in one call
+        (bih_render_device_frames); frame j at out_ptr + 4*j*out_stride bytes."""
+        check(load().bih_render_device_frames(self.arrays.handle, C.byref(self.camera), self.w, self.h,
+                                              self.spp, frame0, nframes, self.seed,
+                                              C.byref(rows) if rows is not None else None,
+                                              C.c_void_p(out_ptr), out_stride, C.c_void_p(stream or 0)),
+              "bih_render_device_frames")
+
     def render_whitted(self, frame: int | None = None) -> np.ndarray:
         """Config C4: one frame of 8-bounce mirror rays (bih_render_whitted) into a
         host (h, w) uint32 image."""

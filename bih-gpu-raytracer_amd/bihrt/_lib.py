@@ -125,6 +125,8 @@ def load():
     L.bih_render_device.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, u32, u64,
                                     C.POINTER(Rows), u32, vp, vp, vp]
     L.bih_sync.argtypes = [vp, vp]
+    L.bih_render_device_frames.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, u32, u32, u64,
+                                           C.POINTER(Rows), vp, u64, vp]
     L.bih_render_whitted_device.argtypes = [vp, C.POINTER(Camera), u32, u32, u32, u32, u64,
                                             C.POINTER(Rows), vp, vp, vp]
     L.bih_render_whitted.argtypes = [C.POINTER(Scene), vp, C.POINTER(Camera), C.POINTER(Framebuffer)]
@@ -135,7 +137,7 @@ def load():
     for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
                  "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_last_render_times", "bih_set_timing",
-                 "bih_render_whitted_device", "bih_render_whitted",
+                 "bih_render_whitted_device", "bih_render_whitted", "bih_render_device_frames",
                  "bih_bins_get_stats"):
         getattr(L, name).restype = i32
     _lib = L

@@ -149,6 +149,7 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 }
 __global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__restrict__ v, uint32_t words,
                                                            TreeHeader *hdr) {
+    __shared__ uint32_t s_x[kThreads / 64], s_y[kThreads / 64];
     uint32_t x = 0u, y = 0u;
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < words; i += gridDim.x * kThreads) {
         const uint32_t w = v[i];
@@ -159,8 +160,18 @@ __global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__res
         x ^= __shfl_xor(x, o);
         y ^= __shfl_xor(y, o);
     }
-    if ((threadIdx.x & 63) == 0 && (x | y))
-        atomicXor(&hdr->content, ((unsigned long long)y << 32) | x);
+    if ((threadIdx.x & 63) == 0) {
+        s_x[threadIdx.x >> 6] = x;
+        s_y[threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // one atomic per block (a single address: few blocks)
+        for (int k = 1; k < kThreads / 64; ++k) {
+            x ^= s_x[k];
+            y ^= s_y[k];
+        }
+        if (x | y) atomicXor(&hdr->content, ((unsigned long long)y << 32) | x);
+    }
 }
 
 __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
@@ -270,7 +281,9 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *l
 // {tag:30 | flag:2 | value:32}, flag 1 = aggregate, 2 = inclusive prefix; the
 // tag is unique per scan call (host counter), so no status memset is needed
 // between calls.  Tiles are blockIdx.x: workgroups dispatch in id order, so
-// every tile a block waits for is resident or done.
+// every tile a block waits for is resident or done.  The flag and the value
+// share one 64-bit word, so relaxed device-scope atomics suffice (no L2
+// writeback/invalidate fences: each block's output is its own).
 constexpr uint32_t kScanAgg = 1u, kScanPre = 2u;
 __device__ __forceinline__ unsigned long long scan_word(uint32_t tag, uint32_t flag, uint32_t v) {
     return ((unsigned long long)((tag << 2) | flag) << 32) | v;
@@ -296,13 +309,13 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     if (threadIdx.x == 0) {
         uint32_t prefix = 0;
         if (tile == 0) {
-            __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELEASE,
+            __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             for (uint32_t j = tile - 1;;) {
                 const unsigned long long w =
-                    __hip_atomic_load(status + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t hi = (uint32_t)(w >> 32);
                 if ((hi >> 2) != tag || (hi & 3u) == 0u) {
                     __builtin_amdgcn_s_sleep(1);
@@ -312,7 +325,7 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
                 if ((hi & 3u) == kScanPre) break;
                 --j;
             }
-            __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELEASE,
+            __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         s_prefix = prefix;
@@ -840,7 +853,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.tris_s);
         const uint32_t words = 9u * n;     // n <= BIH_MAX_TRIS = 2^27
         const uint32_t hb = (words + kThreads - 1) / kThreads;
-        hipLaunchKernelGGL(k_content_hash, dim3(hb < 4096u ? hb : 4096u), dim3(kThreads), 0, st,
+        hipLaunchKernelGGL(k_content_hash, dim3(hb < 512u ? hb : 512u), dim3(kThreads), 0, st,
                            reinterpret_cast<const uint32_t *>(t.v), words, t.hdr);
         BIH_TRY(hipGetLastError());
     }

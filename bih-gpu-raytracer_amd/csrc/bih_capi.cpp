@@ -734,11 +734,12 @@ static void resolve_bins(bih_tree *tr, bool block) {
 // rebuilt when the bins or the rows change, after every render that may
 // still read the old one.
 static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_rows &rows,
-                             int slot, hipStream_t st, bih::RenderArgs &a) {
+                             int slot, hipStream_t st, bih::RenderArgs &a, uint32_t nframes) {
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     const uint32_t tiles_x = (w + tw - 1) / tw;
     const uint32_t ntiles = tiles_x * ((rows.nrows + th - 1) / th);
+    const size_t nrec = (size_t)ntiles * nframes;   // fallback records: one per packet at most
     const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, tr->bins_gen};
     if (!tr->q_count) {
         hipError_t e = hipMalloc((void **)&tr->q_count, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
@@ -768,15 +769,15 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
         memcpy(tr->q_key, key, sizeof key);
         tr->q_valid = true;
     }
-    if (tr->fbq_cap < ntiles) {
+    if (tr->fbq_cap < nrec) {
         for (int k = 0; k < kSlots; ++k)
             if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
         if (tr->fb_mem) (void)hipFree(tr->fb_mem);
         tr->fb_mem = nullptr;
         tr->fbq_cap = 0;
-        hipError_t e = hipMalloc((void **)&tr->fb_mem, (size_t)kSlots * ntiles * 8 * sizeof(uint32_t));
+        hipError_t e = hipMalloc((void **)&tr->fb_mem, (size_t)kSlots * nrec * 8 * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip((int)e);
-        tr->fbq_cap = ntiles;
+        tr->fbq_cap = nrec;
     }
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
     a.bin_queue = tr->q_list;
@@ -796,10 +797,15 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
     return BIH_OK;
 }
 
-int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
-                      uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
-                      uint32_t *d_out, uint32_t *d_ray_stats, void *stream) {
-    bih_tree *tr = const_cast<bih_tree *>(ctr);
+// nframes > 1 (bih_render_device_frames): frames frame .. frame+nframes-1 in
+// one frustum-bin launch, frame j at d_out + j * out_stride.  Returns
+// kRenderPerFrame, before any RNG work, when this render does not go
+// through the bins (the caller then renders the frames one by one).
+constexpr int kRenderPerFrame = 1;
+static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
+                              uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
+                              uint32_t *d_out, uint32_t *d_ray_stats, void *stream, uint32_t nframes,
+                              uint64_t out_stride) {
     if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0 || traverse > 1) return BIH_ERR_INVALID;
     bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
     if (rows.nrows == 0) return BIH_OK;
@@ -837,13 +843,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
-    int rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
-    if (rc) return rc;
-    const size_t P = (size_t)rows.nrows * w;
-    const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
-    // the state cudaRender leaves behind for frame+1 (CUDAKernels.cu:419)
-    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, st));
-    if (rc) return rc;
+    int rc = BIH_OK;
     hipError_t e = hipSuccess;
     // primary-ray records follow the camera (the origin; the miss-proof boxes
     // also the direction bounds)
@@ -914,6 +914,19 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         // a packet's rows are one bin row when tiles and bands align
         use_bins = rows.row0 % th == 0 && rows.band_h % th == 0;
     }
+    if (nframes > 1 && !use_bins) return kRenderPerFrame;
+    // the frame's per-pixel XORWOW state (InitRandGPU / the state earlier
+    // frames left), and the state cudaRender leaves behind for the frame
+    // after this launch's last (CUDAKernels.cu:419)
+    rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
+    if (rc) return rc;
+    const size_t P = (size_t)rows.nrows * w;
+    const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st));
+    if (rc) return rc;
+    tr->next_frame = frame + nframes;
+    a.nframes = nframes;
+    a.out_stride = out_stride;
     if (use_bins) {
         a.bin_off = tr->bins.off;
         a.bin_list = tr->bin_list;
@@ -921,7 +934,7 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
         a.bin_path = tr->bins.path;
         a.bins_x = tr->bins.bins_x;
         a.bin_gstat = tr->bins.gcount + 1;
-        rc = prepare_bin_queue(tr, w, h, spp, rows, slot, st, a);
+        rc = prepare_bin_queue(tr, w, h, spp, rows, slot, st, a, nframes);
         if (rc) return rc;
     } else {
         // the cost order pays off for the long BIH walks; with the bins the
@@ -1006,6 +1019,36 @@ int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, ui
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;                 // frame+1's state
+    return BIH_OK;
+}
+
+int bih_render_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
+                      uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
+                      uint32_t *d_out, uint32_t *d_ray_stats, void *stream) {
+    return render_device_impl(const_cast<bih_tree *>(ctr), cam, w, h, spp, frame, seed, rows_in, traverse,
+                              d_out, d_ray_stats, stream, 1, 0);
+}
+
+int bih_render_device_frames(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
+                             uint32_t frame0, uint32_t nframes, uint64_t seed, const bih_rows *rows_in,
+                             uint32_t *d_out, uint64_t out_stride, void *stream) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0 || nframes == 0 || nframes > 64)
+        return BIH_ERR_INVALID;
+    const uint64_t nrows = rows_in ? rows_in->nrows : h;
+    if (nframes > 1 && out_stride < nrows * w) return BIH_ERR_INVALID;
+    // one launch: items (<= tiles per band x nframes) and records stay far below 2^31
+    const bool one_launch = nframes > 1 && (uint64_t)((w + 7) / 4) * ((nrows + 3) / 4 + 1) * nframes < (1ull << 28);
+    if (one_launch) {
+        const int rc = render_device_impl(tr, cam, w, h, spp, frame0, seed, rows_in, BIH_TRAVERSE_ANYHIT, d_out,
+                                          nullptr, stream, nframes, out_stride);
+        if (rc != kRenderPerFrame) return rc;
+    }
+    for (uint32_t j = 0; j < nframes; ++j) {
+        const int rc = render_device_impl(tr, cam, w, h, spp, frame0 + j, seed, rows_in, BIH_TRAVERSE_ANYHIT,
+                                          d_out + (uint64_t)j * out_stride, nullptr, stream, 1, 0);
+        if (rc) return rc;
+    }
     return BIH_OK;
 }
 

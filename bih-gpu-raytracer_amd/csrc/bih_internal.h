@@ -105,6 +105,11 @@ struct RenderArgs {
     uint32_t *bin_heads_next = nullptr;
     uint32_t *bin_fb = nullptr;             // fallback records of the slot (k_render_bins), 8 words each
     uint32_t dbg = 0;                       // timing experiments only (BIH_DBG): 1 skip background, 2 skip live
+    // k_render_bins / k_render_fallback: frames d_base's frame .. + nframes - 1
+    // in one launch (bih_render_device_frames); frame j's pixels at
+    // out + j * out_stride, its XORWOW draws 2*spp*j past rng_in's
+    uint32_t nframes = 1;
+    uint64_t out_stride = 0;
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,

@@ -424,12 +424,19 @@ __device__ __forceinline__ void ray_coords(uint64_t rid, uint32_t tiles_x, uint3
 // its frame's state, so consecutive frames can be in flight together.
 template <uint32_t SPP>
 __device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uint32_t s, float &ru,
-                                           float &rv) {
+                                           float &rv, uint32_t fj = 0) {
     const uint64_t P = (uint64_t)a.nrows * a.w;
     uint32_t v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
     uint32_t d = a.d_base;
+    // frame j of a multi-frame launch: its draws start 2*spp*j past rng_in's
+    for (uint32_t k = 0; k < 2 * SPP * fj; ++k) {
+        const uint32_t t = v[0] ^ (v[0] >> 2);
+        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+    }
+    d += 2 * SPP * fj * kWeyl;
     for (uint32_t k = 0; k <= s; ++k) {
         ru = xorwow_uniform(v, d);
         rv = xorwow_uniform(v, d);
@@ -1815,6 +1822,7 @@ struct BinQueue {
     uint4 hb;                          // header of the band of the item next() returned
     unsigned long long pending;        // a position claimed ahead (claim()), lane 0
     bool has_pending;
+    uint32_t nf;                       // frames per launch: a band holds hb.w * nf items
 
     // Claims the slot position next() will use, so that its round trip
     // overlaps the current item's loads (BIH_QUEUE_AHEAD).
@@ -1840,7 +1848,7 @@ struct BinQueue {
             if (hi != 0 && lo < kBinBatch) {
                 const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch;
                 hb = hdr[b];
-                if (start + lo < hb.w) {
+                if (start + lo < hb.w * nf) {
                     item = start + lo;
                     band = b;
                     return true;
@@ -1853,7 +1861,7 @@ struct BinQueue {
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    if (c < h.w) {
+                    if (c < h.w * nf) {
                         if (lane == 0)
                             atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
                         hb = h;
@@ -1895,6 +1903,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.band = xcc_id();
     q.left = 8;
     q.has_pending = false;
+    q.nf = a.nframes;
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
     // timing experiment: items dealt round-robin over the waves (no atomics)
@@ -1929,6 +1938,10 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
 #endif
         BIH_PH(0);
         const uint4 hb = q.hb;
+        // multi-frame launch: a band's items repeat per frame
+        const uint32_t fj = a.nframes > 1 ? it / hb.w : 0u;
+        it -= fj * hb.w;
+        uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
         if (BIH_QUEUE_AHEAD && it < hb.y) q.claim(lane);   // a live tile: claim the next item now
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
@@ -1940,7 +1953,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 for (uint32_t r = 0; r < TH; ++r) {
                     const uint32_t lr = ty * TH + r;
                     if (lr >= a.nrows) break;
-                    uint32_t *o = a.out + (uint64_t)lr * a.w + x0;
+                    uint32_t *o = fout + (uint64_t)lr * a.w + x0;
                     if (TW == 4 && x0 + 4 <= a.w && ((uintptr_t)o & 15u) == 0) {
                         *reinterpret_cast<uint4 *>(o) = make_uint4(bgpix, bgpix, bgpix, bgpix);
                     } else {
@@ -1962,7 +1975,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
         if (valid) {
             float ru = 0.f, rv = 0.f;
-            ray_jitter<SPP>(a, lp, s, ru, rv);
+            ray_jitter<SPP>(a, lp, s, ru, rv, fj);
             const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
             uf = ((float)x + ru) / fw;       // CUDAKernels.cu:414-415
             vf = ((float)y + rv) / fh;
@@ -2031,16 +2044,16 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             uint32_t r = 0;
             if (lane == 0) r = atomicAdd(a.bin_heads + 8 * 32, 1u);
             r = __builtin_amdgcn_readfirstlane(r);
-            if (lane < 5) {
-                const uint32_t v[5] = {tile, (uint32_t)undecided, (uint32_t)(undecided >> 32), (uint32_t)hits,
-                                       (uint32_t)(hits >> 32)};
+            if (lane < 6) {
+                const uint32_t v[6] = {tile, (uint32_t)undecided, (uint32_t)(undecided >> 32), (uint32_t)hits,
+                                       (uint32_t)(hits >> 32), fj};
                 a.bin_fb[(uint64_t)r * kFbWords + lane] = v[lane];
             }
             continue;
         }
         if (valid && s == SPP - 1) {
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
-            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+            fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
         BIH_PH(5);
     }
@@ -2080,6 +2093,8 @@ __global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a
         const uint32_t tile = rec[0];
         const unsigned long long und = ((unsigned long long)rec[2] << 32) | rec[1];
         unsigned long long hits = ((unsigned long long)rec[4] << 32) | rec[3];
+        const uint32_t fj = rec[5];                      // frame of a multi-frame launch
+        uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
         uint32_t x, lr, s;
         ray_coords<LOG2SPP>((uint64_t)tile * 64 + lane, tiles_x, x, lr, s);
         const bool valid = x < a.w && lr < a.nrows;
@@ -2088,7 +2103,7 @@ __global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a
         float dx = 0.f, dy = 0.f, dz = 1.f;
         if (mine) {
             float ru = 0.f, rv = 0.f;
-            ray_jitter<SPP>(a, lp, s, ru, rv);
+            ray_jitter<SPP>(a, lp, s, ru, rv, fj);
             const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
             camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
         }
@@ -2098,7 +2113,7 @@ __global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a
         hits |= __ballot(mine && w.hit);
         if (valid && s == SPP - 1) {
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
-            a.out[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+            fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
     }
 }

@@ -167,6 +167,16 @@ int bih_render_rows(const bih_scene *scene, const bih_tree *tree, const bih_came
 int bih_render_device(const bih_tree *tree, const bih_camera *camera, uint32_t w, uint32_t h,
                       uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows,
                       uint32_t traverse, uint32_t *d_out, uint32_t *d_ray_stats, void *stream);
+/* nframes consecutive frames (frame0 .. frame0+nframes-1, any-hit) in one
+ * call: frame j's nrows*w pixels at d_out + j*out_stride (out_stride >=
+ * nrows*w pixels; 1 <= nframes <= 64).  Each frame is exactly the frame
+ * bih_render_device renders at that index; through the frustum bins the
+ * frames share one launch of each kernel (the host issue cost and the
+ * render's drain are paid once per call -- DESIGN.md section 5), otherwise
+ * they are rendered one by one. */
+int bih_render_device_frames(const bih_tree *tree, const bih_camera *camera, uint32_t w, uint32_t h,
+                             uint32_t spp, uint32_t frame0, uint32_t nframes, uint64_t seed,
+                             const bih_rows *rows, uint32_t *d_out, uint64_t out_stride, void *stream);
 int bih_sync(const bih_tree *tree, void *stream);
 
 /* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)

@@ -549,3 +549,47 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
         assert np.array_equal(a, b), (f, c, cap, int((a != b).sum()))
     monkeypatch.delenv("BIH_BINS_CAP", raising=False)
     g.close()
+
+
+@pytest.mark.parametrize("case", ["bins", "bands", "force_fallback", "spp3_per_frame"])
+def test_render_device_frames_equals_single_frames(case, gpu, bihrt_mod, oracle_mod, monkeypatch):
+    """bih_render_device_frames: nframes consecutive frames in one call
+    (one launch of each kernel through the frustum bins; frame j's jitter
+    2*spp*j draws past the launch's RNG state) equal the frames rendered one
+    by one, then the frame sequence continues; through the exact-walk
+    fallback (every packet undecided) and the per-frame path (spp 3: no bins)
+    as well."""
+    import torch
+    from bihrt.tiling import band_rows
+    S = bihrt_mod.scenes
+    tris = S.soup(200_000, seed=11)
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 480, 270
+    spp = 3 if case == "spp3_per_frame" else 4
+    rows = band_rows(h, 8, 1, 3) if case == "bands" else None
+    nrows = rows.nrows if rows is not None else h
+    if case == "force_fallback":
+        monkeypatch.setenv("BIH_BINS_FORCE_FALLBACK", "1")
+    r = bihrt_mod.Renderer(g, w, h, spp=spp)
+    ref = []
+    for f in range(7):
+        o = torch.zeros(nrows * w, dtype=torch.int32, device="cuda")
+        r.render_device(o.data_ptr(), f, rows=rows)
+        r.sync()
+        ref.append(o.cpu().numpy().view(np.uint32))
+    stride = nrows * w + 64
+    buf = torch.full((6 * stride,), -1, dtype=torch.int32, device="cuda")
+    r.render_device_frames(buf.data_ptr(), 0, 5, stride, rows=rows)
+    o6 = torch.zeros(nrows * w, dtype=torch.int32, device="cuda")
+    r.render_device(o6.data_ptr(), 5, rows=rows)          # the sequence continues
+    r.render_device_frames(buf.data_ptr() + 4 * 5 * stride, 6, 1, stride, rows=rows)
+    r.sync()
+    b = buf.cpu().numpy().view(np.uint32)
+    for f in range(5):
+        assert np.array_equal(b[f * stride: f * stride + nrows * w], ref[f]), (case, f)
+        assert (b[f * stride + nrows * w: (f + 1) * stride] == 0xFFFFFFFF).all()   # stride gap untouched
+    assert np.array_equal(o6.cpu().numpy().view(np.uint32), ref[5])
+    assert np.array_equal(b[5 * stride: 5 * stride + nrows * w], ref[6])
+    if rows is None and spp == 4:
+        img, _ = oracle_mod.OracleTree(tris).render(w, h, frame=3)
+        assert np.array_equal(b[3 * stride: 3 * stride + h * w].reshape(h, w), img)

@@ -43,7 +43,8 @@ def _worker(rank, world, port, w, h, band, out_dir):
     local = np.zeros((mrows, w), np.uint32)
     for k, y in enumerate(ys):
         local[k], _ = ot.render(w, h, rows=(int(y), 1, 1))
-    # the exchange step bench.py runs for N > 1 (gather to rank 0 + reassembly)
+    # the exchange step bench.py runs for N > 1 (gather to rank 0 + reassembly):
+    # one frame, then a group of 3 frames (frames 0, 1, 2) in one message
     t = torch.from_numpy(local.view(np.int32).reshape(-1))
     gather = BandGather(dist, h, w, band, rank, world, "cpu")
     frame = torch.full((h * w,), -1, dtype=torch.int32) if rank == 0 else None
@@ -52,6 +53,21 @@ def _worker(rank, world, port, w, h, band, out_dir):
         np.save(os.path.join(out_dir, "frame.npy"), frame.numpy().view(np.uint32).reshape(h, w))
     else:
         assert gather.recv is None     # nothing lands on non-root ranks
+    group = np.zeros((3, mrows, w), np.uint32)
+    for f in range(3):
+        for k, y in enumerate(ys):
+            group[f, k], _ = ot.render(w, h, frame=f, rows=(int(y), 1, 1))
+    g3 = BandGather(dist, h, w, band, rank, world, "cpu", frames=3)
+    frames = torch.full((3 * h * w,), -1, dtype=torch.int32) if rank == 0 else None
+    g3(torch.from_numpy(group.view(np.int32).reshape(-1)), frames)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "frames3.npy"), frames.numpy().view(np.uint32).reshape(3, h, w))
+    # the same group as 4-bit hit counts (bench.py's strong leg)
+    gp = BandGather(dist, h, w, band, rank, world, "cpu", frames=3, packed=True)
+    framesp = torch.full((3 * h * w,), -1, dtype=torch.int32) if rank == 0 else None
+    gp(torch.from_numpy(group.view(np.int32).reshape(-1)), framesp)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "frames3p.npy"), framesp.numpy().view(np.uint32).reshape(3, h, w))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,9 +79,15 @@ def test_band_tiling_gather_equals_single_render(tmp_path, world, band, oracle_m
                        nprocs=world, join=True, start_method="spawn")
     ref, _ = oracle_mod.OracleTree(edge_scenes()["cornell"]).render(w, h)
     assert np.array_equal(np.load(tmp_path / "frame.npy"), ref)
+    f3 = np.load(tmp_path / "frames3.npy")
+    f3p = np.load(tmp_path / "frames3p.npy")
+    for f in range(3):
+        ref_f = oracle_mod.OracleTree(edge_scenes()["cornell"]).render(w, h, frame=f)[0]
+        assert np.array_equal(f3[f], ref_f)
+        assert np.array_equal(f3p[f], ref_f)
 
 
-def _frames_worker(rank, world, port, w, h, steps, out_dir):
+def _frames_worker(rank, world, port, w, h, steps, out_dir, group=1):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "bih-gpu-raytracer_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -78,7 +100,7 @@ def _frames_worker(rank, world, port, w, h, steps, out_dir):
     # the step itself has no collective: each rank renders its own frames
     mine = {}
     for k in range(steps):
-        f = frame_of_step(5, k, rank, world)
+        f = frame_of_step(5, k, rank, world, group)
         mine[f], _ = ot.render(w, h, frame=f)
     # checking only: collect every rank's frames
     got = [None] * world
@@ -90,13 +112,14 @@ def _frames_worker(rank, world, port, w, h, steps, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_frame_round_robin_covers_sequence(tmp_path, world, oracle_mod):
-    """Weak-scaling decomposition (bench.py default for N > 1): the ranks'
-    frames are exactly frames 5 .. 5 + N*steps - 1, each equal to the frame a
-    single process renders at that index."""
+@pytest.mark.parametrize("world,group", [(2, 1), (3, 1), (2, 3)])
+def test_frame_round_robin_covers_sequence(tmp_path, world, group, oracle_mod):
+    """Weak-scaling decomposition (bench.py's side leg for N > 1): the ranks'
+    frames (groups of `group` consecutive frames dealt round-robin) are
+    exactly frames 5 .. 5 + N*steps - 1, each equal to the frame a single
+    process renders at that index."""
     w, h, steps = 24, 16, 3
-    mp.start_processes(_frames_worker, args=(world, _free_port(), w, h, steps, str(tmp_path)),
+    mp.start_processes(_frames_worker, args=(world, _free_port(), w, h, steps, str(tmp_path), group),
                        nprocs=world, join=True, start_method="spawn")
     z = np.load(tmp_path / "frames.npz")
     assert sorted(int(k) for k in z.files) == list(range(5, 5 + world * steps))
