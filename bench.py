@@ -373,10 +373,11 @@ def main():
     # on the render stream right around the render kernel (bih_last_render_ms),
     # over isolated launches (each frame synchronised before the next) -- the
     # figure rocprofv3's kernel trace reports for the same kernel
+    # (the headline's launches: a call of G frames, one k_render_bins launch)
     kms_iso, tails_iso = [], []
     r.set_timing(True)
     for k in range(args.kernel_samples):
-        step(mode, rows, k, frame_of(5000, k), trav, nf=1)
+        step(mode, rows, k, frame_of(5000, k * G), trav, nf=1, m=G)
         torch.cuda.synchronize()
         km, tm = r.last_render_times()
         kms_iso.append(km)
@@ -398,7 +399,7 @@ def main():
     n_node, n_leaf, n_tri = [int(x) for x in sums.tolist()]
     rays_all = rays_per_frame
     b_ray = (NODE_B * n_node + LEAF_B * n_leaf + TRI_B * n_tri) / rays_all + (FB_B + RNG_B) / SPP
-    launch_rays = rows.nrows * W * SPP
+    launch_rays = rows.nrows * W * SPP * (G if trav == 0 else 1)   # rays of one headline launch
     # per-launch duration of the kernel: with frames in flight a launch's
     # events also count the time it queues behind the other stream's frame,
     # so the isolated launches of the one-in-flight leg give the duration
@@ -416,12 +417,14 @@ def main():
     bc = (traffic or {}).get("bin_counters")
     if bc and trav == 0 and bst.usable and launch_ms:
         pix = rows.nrows * W
-        alg_bytes = 48 * int(bst.list_entries) + 64 * bc["mt"] + 24 * pix
-        alg = {"bytes_per_launch": alg_bytes,
+        gl = G if trav == 0 else 1       # frames per k_render_bins launch
+        alg_bytes = gl * (48 * int(bst.list_entries) + 64 * bc["mt"] + 24 * pix)
+        alg = {"bytes_per_launch": alg_bytes, "frames_per_launch": gl,
                "terms": {"list_entries": int(bst.list_entries), "intersector_calls": bc["mt"],
                          "pixels": pix, "entries_pretested": bc["entries"], "live_lanes": bc["lanes"],
                          "live_packets": bc["packets"]},
-               "formula": "48 x list entries + 64 x intersector calls + (20 + 4) x pixels",
+               "formula": "frames per launch x (48 x list entries + 64 x intersector calls + "
+                          "(20 + 4) x pixels), per-frame terms of one frame (tools/fast_counters.py)",
                "gbs": alg_bytes / (launch_ms * 1e-3) / 1e9}
     bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
             "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
@@ -477,8 +480,10 @@ def main():
                 "frac_algorithmic": alg["gbs"] / HBM_PEAK_GBS if alg else None,
                 "launch_ms": launch_ms,
                 "fallback_ms": (sum(tails_iso) / len(tails_iso)) if tails_iso else None,
+                "frames_per_launch": G if trav == 0 else 1,
                 "launch_ms_source": (f"HIP events around the render kernel on its stream "
-                                     f"(bih_last_render_ms), mean of {len(kms_iso)} isolated launches")
+                                     f"(bih_last_render_times), mean of {len(kms_iso)} isolated launches "
+                                     f"of the headline's calls ({G if trav == 0 else 1} frames each)")
                                     if kernel_launch_ms else "headline leg",
                 "limiter": "scalar-unit issue and memory latency of the packet walk, not HBM "
                            "(DESIGN.md section 4: SQ counters)",
@@ -624,7 +629,7 @@ def measure_traffic(args):
         cmd = [prof, "--pmc", ctr, "-d", out, "-o", ctr, "--output-format", "csv", "--",
                sys.executable, os.path.join(ROOT, "tools", "prof_render.py"), "--frames", "3",
                "--tris", str(args.tris), "--width", str(args.width), "--height", str(args.height),
-               "--spp", str(args.spp), "--traverse", traverse]
+               "--spp", str(args.spp), "--traverse", traverse, "--group", str(max(1, args.group))]
         try:
             p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=300)
         except (OSError, subprocess.TimeoutExpired):

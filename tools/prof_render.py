@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
+    ap.add_argument("--group", type=int, default=1,
+                    help="frames per render call (bih_render_device_frames; any-hit only)")
     a = ap.parse_args()
     import torch
     import bihrt
@@ -26,10 +28,14 @@ def main():
     d = torch.from_numpy(tris).cuda()
     g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=s.cuda_stream)
     r = bihrt.Renderer(g, a.width, a.height, spp=a.spp)
-    out = torch.zeros(a.width * a.height, dtype=torch.int32, device="cuda")
+    P = a.width * a.height
+    out = torch.zeros(a.group * P, dtype=torch.int32, device="cuda")
     trav = bihrt.TRAVERSE_ANYHIT if a.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
-    for f in range(a.frames):
-        r.render_device(out.data_ptr(), f, traverse=trav, stream=s.cuda_stream)
+    for f in range(a.frames):     # --frames render calls
+        if a.group > 1 and trav == bihrt.TRAVERSE_ANYHIT:
+            r.render_device_frames(out.data_ptr(), f * a.group, a.group, P, stream=s.cuda_stream)
+        else:
+            r.render_device(out.data_ptr(), f, traverse=trav, stream=s.cuda_stream)
     torch.cuda.synchronize()
     print("frames", a.frames, "done")
 
