@@ -255,8 +255,8 @@ void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);
 const uint32_t *xorwow_tables_host();   // [32 seq][160][5] ++ [64 step][160][5]
 // v = M^skip v (skip draws ahead, host)
 void xorwow_skip(uint32_t v[5], uint64_t skip);
-// k_rng_init's device tables: jump bytes [4][256][160][5] ++ J by nibbles [40][16][5]
-constexpr size_t kRngInitWords = (size_t)4 * 256 * 800 + 40 * 16 * 5;
+// k_rng_init's device tables: jump bytes [4][256][160][5] ++ J, J^64 by nibbles [2][40][16][5]
+constexpr size_t kRngInitWords = (size_t)4 * 256 * 800 + 2 * 40 * 16 * 5;
 const uint32_t *xorwow_init_tables_host();
 
 }  // namespace bih

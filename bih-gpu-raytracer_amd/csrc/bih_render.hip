@@ -78,13 +78,18 @@ __device__ __forceinline__ void gf2_apply(const uint32_t *__restrict__ m, uint32
 }
 
 // Per-pixel curand_init(seed, pixel, 0) + skip (InitRandGPU,
-// CUDAKernels.cu:450-459): a thread seeds a run of kRngRun consecutive pixels
-// of one row.  The host applied M^skip to the seed state (powers of M
-// commute); the run's first pixel jumps to its subsequence with at most 4
-// byte-table applies (J^(b << 8k)), each next pixel is one J step through the
-// nibble table in LDS.
-constexpr uint32_t kRngRun = 16;
-__device__ __forceinline__ void jump1_lds(const uint32_t *__restrict__ nib, uint32_t x[5]) {
+// CUDAKernels.cu:450-459).  The host applied M^skip to the seed state
+// (powers of M commute).  A wave seeds a segment of 64 x kRngRun consecutive
+// pixels of one row: lane l's first pixel jumps to its subsequence with at
+// most 4 byte-table applies (J^(b << 8k)), its next ones (64 pixels further
+// each) are one J^64 step through the nibble table in LDS, and the 64 lanes
+// store 64 consecutive words per plane (coalesced: a lane-per-run layout
+// spread each store over 64 lines and was store-bound at 0.18 ms / 1080p).
+#ifndef BIH_RNG_RUN
+#define BIH_RNG_RUN 32
+#endif
+constexpr uint32_t kRngRun = BIH_RNG_RUN;
+__device__ __forceinline__ void jump_lds(const uint32_t *__restrict__ nib, uint32_t x[5]) {
     uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
 #pragma unroll
     for (int g = 0; g < 40; ++g) {
@@ -101,13 +106,16 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
                                                        uint32_t s2, uint32_t s3, uint32_t s4,
                                                        const uint32_t *__restrict__ tables) {
     __shared__ uint32_t s_nib[40 * 16 * 5];
-    const uint32_t *nib = tables + 4 * 256 * 800;
-    for (uint32_t k = threadIdx.x; k < 40 * 16 * 5; k += kThreads) s_nib[k] = nib[k];
+    const uint32_t *nib64 = tables + 4 * 256 * 800 + 40 * 16 * 5;   // J^64
+    for (uint32_t k = threadIdx.x; k < 40 * 16 * 5; k += kThreads) s_nib[k] = nib64[k];
     __syncthreads();
-    const uint32_t runs = (w + kRngRun - 1) / kRngRun;
-    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (t >= (uint64_t)nrows * runs) return;
-    const uint32_t lr = (uint32_t)(t / runs), x0 = (uint32_t)(t % runs) * kRngRun;
+    constexpr uint32_t kSeg = 64 * kRngRun;
+    const uint32_t segs = (w + kSeg - 1) / kSeg;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+    if (wave >= (uint64_t)nrows * segs) return;
+    const uint32_t lr = (uint32_t)(wave / segs), x0 = (uint32_t)(wave % segs) * kSeg + lane;
+    if (x0 >= w) return;
     const uint64_t pix = (uint64_t)global_row(lr, row0, band_h, band_step) * w + x0;
     uint32_t v[5] = {s0, s1, s2, s3, s4};
 #pragma unroll
@@ -116,11 +124,10 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
         if (b) gf2_apply(tables + ((uint32_t)k * 256 + b) * 800, v);
     }
     const uint64_t P = (uint64_t)nrows * w, lp0 = (uint64_t)lr * w + x0;
-    const uint32_t n = w - x0 < kRngRun ? w - x0 : kRngRun;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (i) jump1_lds(s_nib, v);
+    for (uint32_t i = 0; i < kRngRun && x0 + 64 * i < w; ++i) {
+        if (i) jump_lds(s_nib, v);
 #pragma unroll
-        for (int j = 0; j < 5; ++j) rng[(uint64_t)j * P + lp0 + i] = v[j];
+        for (int j = 0; j < 5; ++j) rng[(uint64_t)j * P + lp0 + 64 * i] = v[j];
     }
 }
 
@@ -2782,7 +2789,7 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     uint32_t v[5], d;
     xorwow_seed(seed, v, &d);
     xorwow_skip(v, skip);   // M^skip commutes with the subsequence jumps
-    const uint64_t threads = (uint64_t)nrows * ((w + kRngRun - 1) / kRngRun);
+    const uint64_t threads = (uint64_t)nrows * ((w + 64 * kRngRun - 1) / (64 * kRngRun)) * 64;
     if (threads == 0) return 0;
     const uint32_t blocks = (uint32_t)((threads + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_rng_init, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, rng, w, row0,

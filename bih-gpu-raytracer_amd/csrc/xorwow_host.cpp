@@ -120,9 +120,9 @@ void xorwow_skip(uint32_t v[5], uint64_t skip) {
 
 // k_rng_init's tables: jump bytes [4][256][160][5], entry (k, b) = J^(b << 8k)
 // with J = M^(2^67) (one subsequence), so a pixel's subsequence start is at
-// most 4 matrix applies; then J itself by 4-bit input groups [40][16][5]
-// (entry (g, n) = XOR of J's columns 4g + set bits of n), the step from one
-// pixel to the next from LDS.
+// most 4 matrix applies; then J and J^64 by 4-bit input groups [2][40][16][5]
+// (entry (g, n) = XOR of the matrix's columns 4g + set bits of n), a lane's
+// step to its next pixel from LDS.
 static void build_init_tables() {
     const uint32_t *seqt = xorwow_tables_host();
     std::vector<Gf2> seq(32);
@@ -137,12 +137,17 @@ static void build_init_tables() {
         for (int b = 1; b < 256; ++b) mul(lvl[b & (b - 1)], seq[8 * k + __builtin_ctz(b)], lvl[b]);
         for (int b = 0; b < 256; ++b) memcpy(bytes + ((size_t)k * 256 + b) * 800, lvl[b].c, 800 * 4);
     }
-    uint32_t *nib = bytes + 4 * 256 * 800;
-    for (int g = 0; g < 40; ++g)
-        for (int n = 0; n < 16; ++n)
-            for (int j = 0; j < 4; ++j)
-                if ((n >> j) & 1)
-                    for (int w = 0; w < 5; ++w) nib[(g * 16 + n) * 5 + w] ^= seq[0].c[4 * g + j][w];
+    // nibble tables of J (k_rng_init's per-pixel step) and of J^64 (a lane's
+    // step when the 64 lanes of a wave seed 64 consecutive pixels at a time)
+    const Gf2 *steps[2] = {&seq[0], &seq[6]};
+    for (int t = 0; t < 2; ++t) {
+        uint32_t *nib = bytes + 4 * 256 * 800 + t * 40 * 16 * 5;
+        for (int g = 0; g < 40; ++g)
+            for (int n = 0; n < 16; ++n)
+                for (int j = 0; j < 4; ++j)
+                    if ((n >> j) & 1)
+                        for (int w = 0; w < 5; ++w) nib[(g * 16 + n) * 5 + w] ^= steps[t]->c[4 * g + j][w];
+    }
 }
 
 const uint32_t *xorwow_init_tables_host() {
