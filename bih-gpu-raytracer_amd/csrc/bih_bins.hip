@@ -56,25 +56,74 @@
 
 #include "bih_internal.h"
 #include "bih_bound.h"
+#include "bih_device.h"
 
 namespace bih {
 namespace {
 
 constexpr int kThreads = 256;
 
-__device__ __forceinline__ bool alive(const float *prim, uint32_t k) {
-    const uint32_t b = __float_as_uint(prim[16ull * k + 12]);
-    return b - 1u < 0x7f7fffffu;                 // 0 < tnum < +inf (tri_alive)
+
+// The camera's primary-ray records and its alive triangles (a thread per
+// Morton-ordered triangle i and per internal node i):
+//   - the triangle record (dev::tri_prim_record; bih_render.hip's k_tri_prim)
+//     and the camera-relative node record (k_node_prim's, no culled set);
+//   - which triangles a primary ray from the camera can hit (tnum_alive:
+//     about half of a soup, the other half faces away): per block a 256-bit
+//     mask and its count, for k_live_compact;
+//   - zeroes the per-tile counters (zero[0 .. zero_words)) and the bins'
+//     status words (gcount[0..2], [4..5]).
+// (A decoupled look-back here made the kernel 0.08 ms instead of 0.03: 3900
+// blocks waiting on their predecessors' status words.)
+__global__ void __launch_bounds__(kThreads) k_cam_tris(const float *__restrict__ tris, uint32_t n,
+                                                       float ox, float oy, float oz,
+                                                       float *__restrict__ prim,
+                                                       const uint4 *__restrict__ nodes, uint32_t m,
+                                                       uint4 *__restrict__ node_out,
+                                                       unsigned long long *__restrict__ bmask,
+                                                       uint32_t *__restrict__ bcnt,
+                                                       uint32_t *__restrict__ zero, uint32_t zero_words,
+                                                       uint32_t *__restrict__ gcount) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    bool al = false;
+    if (i < n) al = dev::tnum_alive(dev::tri_prim_record(tris + 9ull * i, ox, oy, oz, prim + 16ull * i));
+    if (i < m) {
+        const uint4 nd = nodes[i];
+        const uint32_t ax = (nd.z >> 27) & 3u;
+        const float org = ax == 0u ? ox : (ax == 1u ? oy : oz);
+        const uint32_t split = nd.z & 0x7ffffffu;
+        const uint32_t wd = nd.w | (((nd.z >> 29) & 1u) << 26) | (((nd.z >> 30) & 1u) << 31);
+        node_out[i] = make_uint4(__float_as_uint(__uint_as_float(nd.x) - org),
+                                 __float_as_uint(__uint_as_float(nd.y) - org), (split << 8) | ax, wd);
+    }
+    for (uint32_t k = i; k < zero_words; k += gridDim.x * kThreads) zero[k] = 0u;
+    if (i == 0) {
+        gcount[0] = gcount[1] = gcount[2] = 0u;
+        gcount[4] = gcount[5] = 0u;
+    }
+    const unsigned long long mk = __ballot(al);
+    if (lane == 0) {
+        s_w[w] = (uint32_t)__popcll(mk);
+        bmask[4ull * blockIdx.x + w] = mk;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-// r[13] = leaf of each Morton-ordered triangle (the leaf fast_verify checks)
-__global__ void __launch_bounds__(kThreads) k_bin_leaf(const int32_t *__restrict__ first,
-                                                       const uint32_t *__restrict__ cnt, uint32_t U,
-                                                       float *__restrict__ prim) {
-    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-    if (k >= U) return;
-    const uint32_t b = (uint32_t)first[k], c = cnt[k];
-    for (uint32_t i = b; i < b + c; ++i) prim[16ull * i + 13] = __uint_as_float(k);
+// live[] = the alive triangles in Morton order (boff = exclusive scan of
+// k_cam_tris' block counts), so that k_bin_fp, k_bin_count and k_bin_fill
+// run over whole waves of them.
+__global__ void __launch_bounds__(kThreads) k_live_compact(const unsigned long long *__restrict__ bmask,
+                                                           const uint32_t *__restrict__ boff,
+                                                           uint32_t *__restrict__ live) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const unsigned long long *bm = bmask + 4ull * blockIdx.x;
+    const unsigned long long mk = bm[w];
+    if (!((mk >> lane) & 1ull)) return;
+    uint32_t off = boff[blockIdx.x];
+    for (uint32_t k = 0; k < w; ++k) off += (uint32_t)__popcll(bm[k]);
+    live[off + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = blockIdx.x * kThreads + threadIdx.x;
 }
 
 __device__ __forceinline__ double dot3(const double *a, const double *b) {
@@ -170,30 +219,48 @@ __device__ __forceinline__ void edge_pretest(const float *rr, float a, float b, 
 struct PlanL {
     double L[3];
 };
+// m(h) of plane_l: h / max|X[a]| (h >= 0) or h / min|X[a]| (h < 0), NaN -> -inf;
+// nondecreasing in h
+__device__ __forceinline__ double plane_m(double h, double ramin, double ramax) {
+    double m;
+    if (h >= 0.0) m = ramax > 0.0 ? h * ramax : INFINITY;
+    else m = ramin > 0.0 ? h * ramin : -INFINITY;
+    return (m == m) ? m : -INFINITY;
+}
 // ramin / ramax: 1 / min|X[a]|, 1 / max|X[a]| over the hull (0: that bound
 // is 0; the f64 reciprocal's rounding is far below the 4e margins)
 __device__ __forceinline__ PlanL plane_l(const double (*X)[3], int ax, double val, bool le, double ramin,
                                          double ramax) {
     PlanL o;
     const double r = 4.0 * 0x1p-24 * fabs(val);
-    for (int j = 0; j < 3; ++j) {
-        const double h = (le ? val - X[j][ax] : X[j][ax] - val) - r;
-        double m;
-        if (h >= 0.0) m = ramax > 0.0 ? h * ramax : INFINITY;
-        else m = ramin > 0.0 ? h * ramin : -INFINITY;
-        o.L[j] = (m == m) ? m : -INFINITY;
-    }
+    for (int j = 0; j < 3; ++j) o.L[j] = plane_m((le ? val - X[j][ax] : X[j][ax] - val) - r, ramin, ramax);
     return o;
+}
+// The smallest of plane_l's three values: the same expression at the corner
+// with the extreme coordinate (xmax for le, xmin otherwise; fmax / fmin return
+// one of the corners' own values), and fl and plane_m are monotone, so it is
+// <= every corner's value.  With no NaN among the corners, lmin_p + lmin_q > 0
+// (rounded: fl(a + b) is monotone too) implies every corner's
+// L_p + L_q > 0, so triangle_plan tests the three corners only when this
+// one-value test fails -- with the same outcome as testing them always.
+__device__ __forceinline__ double plane_lmin(double xmin, double xmax, double val, bool le, double ramin,
+                                             double ramax) {
+    const double r = 4.0 * 0x1p-24 * fabs(val);
+    return plane_m((le ? val - xmax : xmin - val) - r, ramin, ramax);
 }
 __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const TreeHeader *hdr,
                                   const float *o, const uint4 *node_prim, const int32_t *leaf_parent,
                                   const int32_t *parent, float *vals) {
     constexpr uint32_t kFull = 3u;
-    double amin[3], amax[3];
+    double amin[3], amax[3], xlo[3], xhi[3];
     int sgn[3];
+    bool finite_ok = true;   // no NaN corner coordinate: the one-value test is exact
     for (int ax = 0; ax < 3; ++ax) {
         const double lo = fmin(fmin(X[0][ax], X[1][ax]), X[2][ax]);
         const double hi = fmax(fmax(X[0][ax], X[1][ax]), X[2][ax]);
+        finite_ok = finite_ok && X[0][ax] == X[0][ax] && X[1][ax] == X[1][ax] && X[2][ax] == X[2][ax];
+        xlo[ax] = lo;
+        xhi[ax] = hi;
         const double mn = lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0);
         const double mx = fmax(fabs(lo), fabs(hi));
         amin[ax] = mn > 0.0 ? 1.0 / mn : 0.0;   // reciprocals (plane_l)
@@ -218,8 +285,12 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
         }
     // the root path, root first (Karras: leaf k lies left of node n iff
     // k <= split(n); every thread reads the top levels from cache), each
-    // plane against the last plane of the other kind
-    PlanL lastE = slabE, lastX = slabX;
+    // plane against the last plane of the other kind.  The last planes are
+    // kept as {value, axis} plus their smallest L (plane_lmin); their three
+    // corner values are recomputed (plane_l, the same values) only for a
+    // comparison the one-value test does not settle.
+    double lastEmin = fmin(fmin(slabE.L[0], slabE.L[1]), slabE.L[2]);
+    double lastXmin = fmin(fmin(slabX.L[0], slabX.L[1]), slabX.L[2]);
     float lastEv = 0.0f, lastXv = 0.0f;
     uint32_t lastEa = 0, lastXa = 0;
     bool lastEslab = true, lastXslab = true;
@@ -234,26 +305,40 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
         const float val = __uint_as_float(le ? r.x : r.y);
         if (sgn[ax] == 0 || val == 0.0f || !(val == val)) return kFull;
         const bool is_exit = le == (sgn[ax] > 0);
-        const PlanL l = plane_l(X, ax, (double)val, le, amin[ax], amax[ax]);
-        const PlanL &q = is_exit ? lastE : lastX;
-        bool ok = true;
-        for (int j = 0; j < 3; ++j) ok = ok && (l.L[j] + q.L[j] > 0.0);
+        const double lmin = plane_lmin(xlo[ax], xhi[ax], (double)val, le, amin[ax], amax[ax]);
+        bool ok = finite_ok && lmin + (is_exit ? lastEmin : lastXmin) > 0.0;
         if (!ok) {
-            if (nc == 2) return kFull;
+            // the three corners: this plane and the partner (the last plane
+            // of the other kind: an entry plane has le = sgn < 0, an exit
+            // plane le = sgn > 0)
+            const PlanL l = plane_l(X, ax, (double)val, le, amin[ax], amax[ax]);
             const bool qslab = is_exit ? lastEslab : lastXslab;
             const uint32_t qa = is_exit ? lastEa : lastXa;
-            meta |= (ax | (is_exit ? 4u : 0u) | ((qslab ? 0u : qa) << 3) | (qslab ? 32u : 0u)) << (2 + 6 * nc);
-            vals[2 * nc] = val;
-            vals[2 * nc + 1] = qslab ? 0.0f : (is_exit ? lastEv : lastXv);
-            ++nc;
+            PlanL q;
+            if (qslab) {
+                q = is_exit ? slabE : slabX;
+            } else {
+                const float qv = is_exit ? lastEv : lastXv;
+                const bool qle = is_exit ? sgn[qa] < 0 : sgn[qa] > 0;
+                q = plane_l(X, qa, (double)qv, qle, amin[qa], amax[qa]);
+            }
+            ok = true;
+            for (int j = 0; j < 3; ++j) ok = ok && (l.L[j] + q.L[j] > 0.0);
+            if (!ok) {
+                if (nc == 2) return kFull;
+                meta |= (ax | (is_exit ? 4u : 0u) | ((qslab ? 0u : qa) << 3) | (qslab ? 32u : 0u)) << (2 + 6 * nc);
+                vals[2 * nc] = val;
+                vals[2 * nc + 1] = qslab ? 0.0f : (is_exit ? lastEv : lastXv);
+                ++nc;
+            }
         }
         if (is_exit) {
-            lastX = l;
+            lastXmin = lmin;
             lastXv = val;
             lastXa = ax;
             lastXslab = false;
         } else {
-            lastE = l;
+            lastEmin = lmin;
             lastEv = val;
             lastEa = ax;
             lastEslab = false;
@@ -293,60 +378,14 @@ __device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint
     }
 }
 
-// The triangles a primary ray from the camera can hit (alive: 0 < tnum <
-// inf; about half of a soup, the other half faces away), compacted in
-// Morton order: k_bin_fp, k_bin_count and k_bin_fill run over this list, so
-// their waves are not half idle.  Per-block counts (k_bin_alive_count), an
-// exclusive scan, then the writes (k_bin_compact): one atomic per wave on a
-// single counter cost 0.18 ms (the head-word limit of k_render_bins' queue).
-// A dead triangle gets the empty footprint here.
-__device__ __forceinline__ uint32_t block_alive(const float *prim, uint32_t n, uint32_t *s_w,
-                                                unsigned long long &m, uint32_t &wave_off) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const bool al = i < n && alive(prim, i);
-    m = __ballot(al);
-    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t tot = 0;
-    wave_off = 0;
-    for (uint32_t k = 0; k < kThreads / 64; ++k) {
-        if (k == w) wave_off = tot;
-        tot += s_w[k];
-    }
-    return tot;
-}
-__global__ void __launch_bounds__(kThreads) k_bin_alive_count(float *__restrict__ prim, uint32_t n,
-                                                              uint2 *__restrict__ brect,
-                                                              uint32_t *__restrict__ bcnt) {
-    __shared__ uint32_t s_w[kThreads / 64];
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i < n && !alive(prim, i)) {
-        brect[i] = make_uint2(1u, 0u);
-        prim[16ull * i + 14] = __uint_as_float(1u);   // empty pixel range
-        prim[16ull * i + 15] = __uint_as_float(1u);
-    }
-    unsigned long long m;
-    uint32_t wo;
-    const uint32_t tot = block_alive(prim, n, s_w, m, wo);
-    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
-}
-__global__ void __launch_bounds__(kThreads) k_bin_compact(const float *__restrict__ prim, uint32_t n,
-                                                          const uint32_t *__restrict__ boff,
-                                                          uint32_t *__restrict__ live) {
-    __shared__ uint32_t s_w[kThreads / 64];
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
-    unsigned long long m;
-    uint32_t wo;
-    (void)block_alive(prim, n, s_w, m, wo);
-    if ((m >> lane) & 1ull) live[boff[blockIdx.x] + wo + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
-}
-
-// Footprint of triangle i: bin rectangle brect[i] (bx0 | bx1 << 16,
-// by0 | by1 << 16; empty = bx0 > bx1), the pixel rectangle in r[14..15] and
-// its list entry binrec[i]; the global list takes the rest.
-__global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, uint32_t n,
+// Footprint of alive triangle i = live[j]: bin rectangle brect[i] (bx0 |
+// bx1 << 16, by0 | by1 << 16; empty = bx0 > bx1) and its list entry
+// binrec[i]; the global list takes the rest.  leaf = the leaf of each sorted
+// triangle (DeviceTree::tri_leaf).
+__global__ void __launch_bounds__(kThreads) k_bin_fp(const float *__restrict__ prim, uint32_t n,
                                                      BinCamera c, const TreeHeader *__restrict__ hdr,
                                                      const uint4 *__restrict__ node_prim,
+                                                     const uint32_t *__restrict__ tri_leaf,
                                                      const int32_t *__restrict__ leaf_parent,
                                                      const int32_t *__restrict__ parent,
                                                      uint2 *__restrict__ path, uint2 *__restrict__ brect,
@@ -357,15 +396,10 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
                                                      const uint32_t *__restrict__ live_count) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= *live_count) return;
-    const uint32_t i = live[j];   // k_bin_compact
-    float *r = prim + 16ull * i;
+    const uint32_t i = live[j];   // k_cam_tris
+    const float *r = prim + 16ull * i;
+    const uint32_t leaf = tri_leaf[i];
     const uint2 none = make_uint2(1u, 0u);
-    if (!alive(prim, i)) {
-        brect[i] = none;
-        r[14] = __uint_as_float(1u);   // empty pixel range
-        r[15] = __uint_as_float(1u);
-        return;
-    }
     float rr[13];
 #pragma unroll
     for (int k = 0; k < 13; ++k) rr[k] = r[k];
@@ -375,6 +409,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
     uint32_t plan = 3u;                // triangle_plan: 3 = full root-path check
     float plan_vals[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+    float rec[16];
     if (ok) {
         // corners of the inflated triangle: depth and image (u, v)
         int front = 0, back = 0;
@@ -429,8 +464,6 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
         }
         if (front == 3) {
             side = 1;
-            plan = triangle_plan(cx, __float_as_uint(r[13]), hdr, c.o, node_prim, leaf_parent, parent,
-                                 plan_vals);
         } else if (back == 3) {
             // exact t* = tnum* / det* with det* > 0 (miss_bary's den); tnum_c
             // errs by at most 5e |e2|.Q (q_c = cross(s, e1): 2e Q, the dot
@@ -445,149 +478,168 @@ __global__ void __launch_bounds__(kThreads) k_bin_fp(float *__restrict__ prim, u
                                                fabs((double)rr[5]) * Q[2]);
             if ((double)rr[12] > et) side = -1;
         }
-    }
-    if (side == -1) {
-        brect[i] = none;
-        r[14] = __uint_as_float(1u);
-        r[15] = __uint_as_float(1u);
-        return;
-    }
-    // the list entry: edge pre-test (or the always-passing one), triangle, leaf
-    {
-        float rec[16];
-        if (ok) {
-            edge_pretest(rr, a, b, cc, c, rec);
-        } else {
-            for (int j = 0; j < 3; ++j) {
-                rec[3 * j] = INFINITY;
-                rec[3 * j + 1] = 0.0f;
-                rec[3 * j + 2] = 0.0f;
-            }
+        if (side == -1) {
+            brect[i] = none;
+            return;
         }
-        rec[9] = __uint_as_float(i);
-        rec[10] = __uint_as_float(__float_as_uint(r[13]) | (plan == 0u ? 0x80000000u : 0u));
-        rec[11] = __uint_as_float(plan);
+        uint2 rect = none;
+        if (side == 1) {
+            // pixel x holds the samples u in (x / W, (x + 1) / W]: pixels
+            // [floor(W umin - 1/2) - 1, floor(W umax + 1/2)], clipped to the image
+            const double W = (double)c.w, H = (double)c.h;
+            const double fx0 = floor(fmax(fmin(umin * W - 0.5, 1e9), -1e9)) - 1.0;
+            const double fx1 = floor(fmax(fmin(umax * W + 0.5, 1e9), -1e9));
+            const double fy0 = floor(fmax(fmin(vmin * H - 0.5, 1e9), -1e9)) - 1.0;
+            const double fy1 = floor(fmax(fmin(vmax * H + 0.5, 1e9), -1e9));
+            if (!(fx1 >= 0.0 && fy1 >= 0.0 && fx0 <= W - 1.0 && fy0 <= H - 1.0)) {
+                brect[i] = none;       // off the image: never listed (no entry, no plan)
+                return;
+            }
+            const uint32_t x0 = (uint32_t)fmax(fx0, 0.0), x1 = (uint32_t)fmin(fx1, W - 1.0);
+            const uint32_t y0 = (uint32_t)fmax(fy0, 0.0), y1 = (uint32_t)fmin(fy1, H - 1.0);
+            rect = make_uint2((x0 / c.tw) | ((x1 / c.tw) << 16), (y0 / c.th) | ((y1 / c.th) << 16));
+        }
+        // the edge pre-test now (rr, a, b, cc end here), the plan after
+        edge_pretest(rr, a, b, cc, c, rec);
+#ifndef BIH_FP_EXP
+#define BIH_FP_EXP 0   // timing experiments only (wrong plans): 1 no plan walk, no paths
+#endif
+#if BIH_FP_EXP & 1
+        plan = 1u;
+#else
+        if (side == 1) plan = triangle_plan(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, plan_vals);
+#endif
+        brect[i] = rect;
+    } else {
+        // no bound: the always-passing pre-test, every packet tests it
+        for (int j = 0; j < 3; ++j) {
+            rec[3 * j] = INFINITY;
+            rec[3 * j + 1] = 0.0f;
+            rec[3 * j + 2] = 0.0f;
+        }
+        brect[i] = none;
+    }
+    // the list entry: edge pre-test, triangle, leaf, plan
+    rec[9] = __uint_as_float(i);
+    rec[10] = __uint_as_float(leaf | (plan == 0u ? 0x80000000u : 0u));
+    rec[11] = __uint_as_float(plan);
 #ifndef BIH_FAST_COUNTERS
 #define BIH_FAST_COUNTERS 0
 #endif
-        // counter builds check every plan against the root-path check: all paths
-        if (plan == 3u || BIH_FAST_COUNTERS) write_path(node_prim, __float_as_uint(r[13]), path);
-        for (int k = 0; k < 4; ++k) rec[12 + k] = plan_vals[k];
-        float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
-        for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
-    }
-    if (side == 0) {                   // every packet tests it
-        brect[i] = none;
-        r[14] = __uint_as_float(0xffff0000u);
-        r[15] = __uint_as_float(0xffff0000u);
-        glist[atomicAdd(gcount, 1u)] = i;
-        return;
-    }
-    // pixel x holds the samples u in (x / W, (x + 1) / W]: pixels
-    // [floor(W umin - 1/2) - 1, floor(W umax + 1/2)], clipped to the image
-    const double W = (double)c.w, H = (double)c.h;
-    const double fx0 = floor(fmax(fmin(umin * W - 0.5, 1e9), -1e9)) - 1.0;
-    const double fx1 = floor(fmax(fmin(umax * W + 0.5, 1e9), -1e9));
-    const double fy0 = floor(fmax(fmin(vmin * H - 0.5, 1e9), -1e9)) - 1.0;
-    const double fy1 = floor(fmax(fmin(vmax * H + 0.5, 1e9), -1e9));
-    if (!(fx1 >= 0.0 && fy1 >= 0.0 && fx0 <= W - 1.0 && fy0 <= H - 1.0)) {
-        brect[i] = none;               // off the image
-        r[14] = __uint_as_float(1u);
-        r[15] = __uint_as_float(1u);
-        return;
-    }
-    const uint32_t x0 = (uint32_t)fmax(fx0, 0.0), x1 = (uint32_t)fmin(fx1, W - 1.0);
-    const uint32_t y0 = (uint32_t)fmax(fy0, 0.0), y1 = (uint32_t)fmin(fy1, H - 1.0);
-    r[14] = __uint_as_float(x0 | ((x1 - x0) << 16));
-    r[15] = __uint_as_float(y0 | ((y1 - y0) << 16));
-    brect[i] = make_uint2((x0 / c.tw) | ((x1 / c.tw) << 16), (y0 / c.th) | ((y1 / c.th) << 16));
+    // counter builds check every plan against the root-path check: all paths
+    if (plan == 3u || BIH_FAST_COUNTERS) write_path(node_prim, leaf, path);
+    for (int k = 0; k < 4; ++k) rec[12 + k] = plan_vals[k];
+    float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
+    for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+    if (side == 0) glist[atomicAdd(gcount, 1u)] = i;   // every packet tests it
 }
 
 // Tile (bx, by) against a triangle's edge pre-test (k0..k8 = 3 x {K0', Ku,
 // Kv}, the kernel evaluates fmaf(Kv, v, fmaf(Ku, u, K0'))): 0 = no sample of
 // the tile passes all three edges (the triangle stays off the tile's list),
 // 2 = every sample passes (listed first: it most likely hits every lane),
-// 1 = otherwise.  A sample of pixel x has u = fl(fl(x + r) / W), r in (0, 1]:
-// u in [x / W, (x + 1) / W] up to 2 roundings (|u| <= 1; padded 2^-20).  Over
-// the tile's (u, v) rectangle the affine function ranges over [lo, hi]
-// (f64, exact enough); the kernel's two fmaf roundings err by at most
-// 2e (|K0'| + |Ku| + |Kv|), taken 4e (sl).  NaN / inf coefficients never
-// exclude a tile.
+// 1 = otherwise.  In f32 with margins (tests/test_bin_pretest.py mirrors it
+// op for op and checks it on kernel-rounded samples):
+//   - a sample of pixel x has u = fl(fl(x + r) / W), r in (0, 1], so
+//     u in [x / W - e, (x + 1) / W + e] (e = 2^-24); the rectangle's
+//     u0 = fl(fl(X * fl(1 / W)) - 2^-20) and u1 = fl(fl(XE * fl(1 / W)) +
+//     2^-20) lie outside that by more than 12e (X <= W: |fl(X fl(1/W)) -
+//     X / W| <= 2e, the pad's rounding e);
+//   - hi = fl(fl(K0 + max(fl(Ku u0), fl(Ku u1))) + max(fl(Kv v0), fl(Kv v1)))
+//     errs from the affine function's largest value over the rectangle by
+//     at most 3e S (S = |K0| + |Ku| + |Kv|: three roundings of terms bounded
+//     by S; fl is monotone, so the max of rounded products is the rounded
+//     max), lo likewise from its smallest, and the kernel's two fmaf roundings
+//     by 2e S more;
+//   - the threshold T = 2^-21 fl(S) + 2^-125 >= 8e S (1 - 3e) covers the 5e S
+//     and, through the absolute term, subnormal roundings.
+// hi < -T: every sample's f < 0 (the kernel rejects it); lo > T: f > 0.
+// NaN / inf coefficients never exclude a tile (T = inf or NaN compares false).
+__device__ __forceinline__ float edge_margin(float K0, float Ku, float Kv) {
+    return 0x1p-21f * ((fabsf(K0) + fabsf(Ku)) + fabsf(Kv)) + 0x1p-125f;
+}
 __device__ __forceinline__ int tile_class(const float4 r0, const float4 r1, const float4 r2,
                                           uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
                                           uint32_t tw, uint32_t th) {
-    const double pad = 0x1p-20;
-    // x / W as x * (1 / W): off by ~1e-16, far inside the pad
-    const double iw = 1.0 / (double)w, ih = 1.0 / (double)h;
+    const float pad = 0x1p-20f;
+    const float iw = 1.0f / (float)w, ih = 1.0f / (float)h;
     const uint32_t xe = (bx + 1) * tw < w ? (bx + 1) * tw : w;
     const uint32_t ye = (by + 1) * th < h ? (by + 1) * th : h;
-    const double u0 = (double)(bx * tw) * iw - pad, u1 = (double)xe * iw + pad;
-    const double v0 = (double)(by * th) * ih - pad, v1 = (double)ye * ih + pad;
+    const float u0 = (float)(bx * tw) * iw - pad, u1 = (float)xe * iw + pad;
+    const float v0 = (float)(by * th) * ih - pad, v1 = (float)ye * ih + pad;
     const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
     bool all = true;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const double K0 = k[3 * j], Ku = k[3 * j + 1], Kv = k[3 * j + 2];
-        const double sl = 0x1p-22 * (fabs(K0) + fabs(Ku) + fabs(Kv));
-        const double hi = K0 + fmax(Ku * u0, Ku * u1) + fmax(Kv * v0, Kv * v1);
-        const double lo = K0 + fmin(Ku * u0, Ku * u1) + fmin(Kv * v0, Kv * v1);
-        if (hi < -sl) return 0;
-        if (!(lo > sl)) all = false;
+        const float K0 = k[3 * j], Ku = k[3 * j + 1], Kv = k[3 * j + 2];
+        const float T = edge_margin(K0, Ku, Kv);
+        const float au0 = Ku * u0, au1 = Ku * u1, bv0 = Kv * v0, bv1 = Kv * v1;
+        const float hi = (K0 + fmaxf(au0, au1)) + fmaxf(bv0, bv1);
+        const float lo = (K0 + fminf(au0, au1)) + fminf(bv0, bv1);
+        if (hi < -T) return 0;
+        if (!(lo > T)) all = false;
     }
     return all ? 2 : 1;
 }
 
 // Pixel mask of a 4 x 4-pixel tile against a triangle's edge pre-test: bit
 // 4 * row + col is clear only when no sample of that pixel can pass all
-// three edges (tile_class's test on the pixel's own rectangle).  The list
-// walk skips an entry for a packet whose remaining lanes all sit in pixels
-// outside its mask.  Other tile shapes: all ones.
+// three edges (tile_class's hi test on the pixel's own rectangle: the
+// largest value is K0 + cu[px] + cv[py], 8 products per edge instead of 16
+// rectangles).  The list walk skips an entry for a packet whose remaining
+// lanes all sit in pixels outside its mask.  Other tile shapes: all ones.
 __device__ __forceinline__ uint32_t pixel_mask(const float4 r0, const float4 r1, const float4 r2,
                                                uint32_t bx, uint32_t by, uint32_t w, uint32_t h,
                                                uint32_t tw, uint32_t th) {
     if (tw != 4u || th != 4u) return 0xFFFFu;
     const float k[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
-    // NaN coefficients never exclude a pixel
-    if (!(k[0] == k[0] && k[3] == k[3] && k[6] == k[6])) return 0xFFFFu;
-    const double pad = 0x1p-20;
-    const double iw = 1.0 / (double)w, ih = 1.0 / (double)h;
-    // the affine edge function's largest value over pixel (px, py)'s (u, v)
-    // rectangle is K0 + cu[px] + cv[py] (the same f64 expressions, in the
-    // same order, as tile_class on the pixel's rectangle): 8 products per edge
-    // instead of 16 rectangles
+    const float pad = 0x1p-20f;
+    const float iw = 1.0f / (float)w, ih = 1.0f / (float)h;
+    float ua[4], ub[4], va[4], vb[4];   // each pixel's u0, u1 / row's v0, v1
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t x = bx * 4u + j, y = by * 4u + j;
+        ua[j] = (float)x * iw - pad;
+        ub[j] = (float)(x + 1u) * iw + pad;
+        va[j] = (float)y * ih - pad;
+        vb[j] = (float)(y + 1u) * ih + pad;
+    }
     uint32_t m = 0xFFFFu;
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
-        const double K0 = k[3 * e], Ku = k[3 * e + 1], Kv = k[3 * e + 2];
-        const double sl = 0x1p-22 * (fabs(K0) + fabs(Ku) + fabs(Kv));
-        double cu[4], cv[4];
+        const float K0 = k[3 * e], Ku = k[3 * e + 1], Kv = k[3 * e + 2];
+        const float T = edge_margin(K0, Ku, Kv);
+        float cu[4], cv[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t x = bx * 4u + j, y = by * 4u + j;
-            const double u0 = (double)x * iw - pad, u1 = (double)(x + 1u) * iw + pad;
-            const double v0 = (double)y * ih - pad, v1 = (double)(y + 1u) * ih + pad;
-            cu[j] = fmax(Ku * u0, Ku * u1);
-            cv[j] = fmax(Kv * v0, Kv * v1);
+            cu[j] = K0 + fmaxf(Ku * ua[j], Ku * ub[j]);
+            cv[j] = fmaxf(Kv * va[j], Kv * vb[j]);
         }
 #pragma unroll
         for (uint32_t py = 0; py < 4u; ++py)
 #pragma unroll
             for (uint32_t px = 0; px < 4u; ++px)
-                if (K0 + cu[px] + cv[py] < -sl) m &= ~(1u << (4u * py + px));
+                if (cu[px] + cv[py] < -T) m &= ~(1u << (4u * py + px));
     }
     return m;
 }
 
-// A lane walks its own triangle's tile rectangle when it has at most
-// kBigRect tiles; larger rectangles (triangles close to the camera or seen
-// edge-on) are walked by the whole wave afterwards, 64 tiles at a time, so
-// one big footprint does not hold up its wave.
-constexpr uint32_t kBigRect = 32;
-// Lane j takes the j-th alive triangle (k_bin_compact's list).
+// The (triangle, tile) pairs of a block's alive triangles (k_cam_tris' list,
+// entries blockIdx.x * kThreads ..): the tile rectangles' areas are scanned in
+// LDS and the block's threads take the pairs in turn (pair p: the triangle
+// whose area range holds p, tile p - its start in row-major order), so a
+// large rectangle (a triangle close to the camera or seen edge-on) is spread
+// over the whole block and every lane runs the same `visit` code.
+struct PairLds {
+    uint32_t off[kThreads + 1];   // exclusive scan of the areas; off[kThreads] = the block's pairs
+    uint32_t tri[kThreads];
+    uint2 rect[kThreads];
+    uint32_t wsum[kThreads / 64];
+};
 template <typename F>
-__device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, const uint32_t *__restrict__ live,
-                                               const uint32_t *__restrict__ live_count, F &&visit) {
-    const uint32_t j0 = blockIdx.x * kThreads + threadIdx.x, lane = threadIdx.x & 63u;
+__device__ __forceinline__ void for_block_pairs(const uint2 *__restrict__ brect, const uint32_t *__restrict__ live,
+                                                const uint32_t *__restrict__ live_count, PairLds &L, F &&visit) {
+    const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid, lane = tid & 63u, w = tid >> 6;
     const uint32_t nl = *live_count;
     uint2 q = make_uint2(1u, 0u);
     uint32_t i = 0;
@@ -595,40 +647,82 @@ __device__ __forceinline__ void for_rect_tiles(const uint2 *__restrict__ brect, 
         i = live[j0];
         q = brect[i];
     }
-    uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-    const bool any = j0 < nl && bx0 <= bx1;
-    const uint32_t area = any ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0u;
-    if (any && area <= kBigRect)
-        for (uint32_t by = by0; by <= by1; ++by)
-            for (uint32_t bx = bx0; bx <= bx1; ++bx) visit(i, bx, by);
-    unsigned long long big = __ballot(area > kBigRect);
-    while (big) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(big);
-        big &= big - 1ull;
-        const uint32_t t = __builtin_amdgcn_readlane(i, j);
-        const uint2 r = brect[t];
-        const uint32_t x0 = r.x & 0xffffu, x1 = r.x >> 16, y0 = r.y & 0xffffu, y1 = r.y >> 16;
-        const uint32_t wx = x1 - x0 + 1, na = wx * (y1 - y0 + 1);
-        for (uint32_t k = lane; k < na; k += 64u) visit(t, x0 + k % wx, y0 + k / wx);
+    const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+    const uint32_t area = (j0 < nl && bx0 <= bx1) ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0u;
+    // inclusive wave scan of the areas, then the waves' totals
+    uint32_t x = area;
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63u) L.wsum[w] = x;
+    L.tri[tid] = i;
+    L.rect[tid] = make_uint2(bx0 | (by0 << 16), bx1 - bx0 + 1);
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t k = 0; k < kThreads / 64; ++k) {
+        base += k < w ? L.wsum[k] : 0u;
+        tot += L.wsum[k];
+    }
+    L.off[tid] = base + x - area;
+    if (tid == 0) L.off[kThreads] = tot;
+    __syncthreads();
+    for (uint32_t p = tid; p < tot; p += kThreads) {
+        // the last triangle t with off[t] <= p (zero areas repeat an offset)
+        uint32_t lo = 0, hi = kThreads;   // off[lo] <= p < off[hi]
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.off[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        const uint2 r = L.rect[lo];
+        const uint32_t k = p - L.off[lo], wx = r.y;
+        const uint32_t ty = k / wx;
+        visit(L.tri[lo], (r.x & 0xffffu) + (k - ty * wx), (r.x >> 16) + ty);
     }
 }
 
-// Counts per tile.  A block's alive triangles are Morton neighbours, so
-// their footprints share tiles (bench: ~10 visits per tile per block): the
-// block counts in LDS over the bounding rectangle of its footprints and
-// adds each non-zero count to the tile's global counter once.  Blocks whose
-// rectangle exceeds kCountLds tiles count with global atomics directly.
-constexpr uint32_t kCountLds = 4096;
+// List order.  A tile's list is walked front to back until every lane of
+// the packet has a verified hit (or the list ends), so triangles that cover
+// more of the tile go first: bucket 0 = every sample passes the pre-test
+// (tile_class 2), then the others by the pixel mask's population, most
+// pixels first (other tile shapes: all in bucket 1).  The order never
+// changes a pixel (any verified hit of a lane is the same bit); on the bench
+// frame it halves the entries walked against arrival order.  Per (tile,
+// bucket) counts are packed kBucketBits each in a u64 (a block adds at most
+// 256 per field).
+constexpr uint32_t kBuckets = kBinBuckets;    // 4: {2}, 12..16, 6..11, <6 px; 6: {2}, 16, 13..15, 10..12, 7..9, <7
+constexpr uint32_t kBucketBits = 64 / kBuckets >= 16 ? 16 : 64 / kBuckets;
+constexpr unsigned long long kBucketMask = (1ull << kBucketBits) - 1ull;
+static_assert(kBuckets * kBucketBits <= 64 && (1u << kBucketBits) > kThreads, "bucket fields");
+__device__ __forceinline__ uint32_t entry_bucket(int cls, uint32_t pm) {
+    if (cls == 2) return 0u;
+    const uint32_t pc = (uint32_t)__popc(pm);
+    if (kBuckets == 4) return pc >= 12u ? 1u : (pc >= 6u ? 2u : 3u);
+    const uint32_t q = kBuckets >= 7u ? 1u + (16u - pc + 1u) / 2u : 1u + (16u - pc + 2u) / 3u;
+    return q < kBuckets - 1u ? q : kBuckets - 1u;
+}
+
+// Counts per tile (cnt: all entries, for the offsets) and per tile and
+// bucket 0 .. kBuckets-2 (cntq[(kBuckets - 1) * b + q]; the last bucket is
+// the rest).  A block's alive
+// triangles are Morton neighbours, so their footprints share tiles: the block
+// counts in LDS over the bounding rectangle of its footprints and adds each
+// non-zero count to the global counters once.  Blocks whose rectangle exceeds
+// kCountLds tiles count with global atomics directly.
+constexpr uint32_t kCountLds = 2048;
 __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect,
                                                         const uint32_t *__restrict__ live,
                                                         const uint32_t *__restrict__ live_count,
                                                         uint32_t bins_x, const float4 *__restrict__ binrec,
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
-                                                        uint32_t *__restrict__ cnt,
+                                                        uint32_t *__restrict__ cnt, uint32_t *__restrict__ cntq,
                                                         unsigned long long *__restrict__ total64) {
-    __shared__ uint32_t s_cnt[kCountLds];
+    __shared__ unsigned long long s_cnt[kCountLds];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
     __shared__ unsigned long long s_tot;   // the block's entries (64-bit: the list total may pass 2^32)
+    __shared__ PairLds L;
     const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid;
     if (tid == 0) {
         s_rect[0] = s_rect[2] = 0xffffu;
@@ -636,17 +730,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
         s_tot = 0ull;
     }
     __syncthreads();
-    {
-        const uint32_t nl = *live_count;
-        if (j0 < nl) {
-            const uint2 q = brect[live[j0]];
-            const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
-            if (bx0 <= bx1) {
-                atomicMin(&s_rect[0], bx0);
-                atomicMax(&s_rect[1], bx1);
-                atomicMin(&s_rect[2], by0);
-                atomicMax(&s_rect[3], by1);
-            }
+    if (j0 < *live_count) {
+        const uint2 q = brect[live[j0]];
+        const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+        if (bx0 <= bx1) {
+            atomicMin(&s_rect[0], bx0);
+            atomicMax(&s_rect[1], bx1);
+            atomicMin(&s_rect[2], by0);
+            atomicMax(&s_rect[3], by1);
         }
     }
     __syncthreads();
@@ -654,58 +745,142 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     const uint32_t rw = rx1 - rx0 + 1;
     const bool use_lds = rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kCountLds;   // block-uniform
     const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
-    for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0u;
+    for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0ull;
     __syncthreads();
     unsigned long long mine = 0ull;
-    for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
-        if (!tile_class(r0, r1, r2, bx, by, w, h, tw, th)) return;
+        const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+        if (!cls) return;
+        const uint32_t q = entry_bucket(cls, cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th));
         ++mine;
-        if (use_lds) atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1u);
-        else atomicAdd(cnt + by * bins_x + bx, 1u);
+        if (use_lds) {
+            atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1ull << (kBucketBits * q));
+        } else {
+            const uint32_t b = by * bins_x + bx;
+            atomicAdd(cnt + b, 1u);
+            if (q < kBuckets - 1u) atomicAdd(cntq + (kBuckets - 1ull) * b + q, 1u);
+        }
     });
     if (mine) atomicAdd(&s_tot, mine);
     __syncthreads();
     for (uint32_t k = tid; k < rarea; k += kThreads) {
-        const uint32_t c = s_cnt[k];
-        if (c) atomicAdd(cnt + (ry0 + k / rw) * bins_x + rx0 + k % rw, c);
+        const unsigned long long c = s_cnt[k];
+        if (!c) continue;
+        const uint32_t b = (ry0 + k / rw) * bins_x + rx0 + k % rw;
+        uint32_t all = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kBuckets; ++q) {
+            const uint32_t cq = (uint32_t)((c >> (kBucketBits * q)) & kBucketMask);
+            all += cq;
+            if (q < kBuckets - 1u && cq) atomicAdd(cntq + (kBuckets - 1ull) * b + q, cq);
+        }
+        atomicAdd(cnt + b, all);
     }
     if (tid == 0 && s_tot) atomicAdd(total64, s_tot);
 }
 
-// A thread per triangle copies its 64-byte entry into each of its tiles'
-// lists: every-sample entries from the front (fill), the others from the
-// back (fill2, the per-tile counts, counted down: no second memset), so a
-// packet meets the triangles that cover its whole tile first.  The order
-// within each part follows the atomics (it can change which candidate a
-// lane verifies, never a pixel).  Positions stay per-entry global atomics:
-// taking them from per-block LDS cursors (as k_bin_count counts) made the
-// fill 0.20 -> 0.13 ms but the render 1 % slower (A/B on one box,
-// 0.0938 vs 0.0929 ms/frame): the block-grouped list order costs more per
-// frame than it saves per camera.
+// The lists: each (triangle, tile) pair k_bin_count counted copies the
+// triangle's 64-byte entry into the tile's list, in its bucket's range
+// (off[b] + the counts of the buckets before it) at a position from the
+// bucket's cursor cur[kBuckets * b + q] (zeroed).  When the block's tile rectangle
+// fits kFillLds tiles, a first pass counts the block's entries per (tile,
+// bucket) in LDS, one global atomic per (tile, bucket) reserves their range,
+// and a second pass ranks them through LDS atomics; larger rectangles take one
+// global atomic per entry.  (Per-entry global atomics throughout cost 0.10 of
+// this kernel's 0.15 ms.)  Within a bucket the order is the blocks' (Morton
+// order, roughly) -- it can change which candidate a lane verifies, never a
+// pixel.
+#ifndef BIH_FILL_LDS
+#define BIH_FILL_LDS 512
+#endif
+constexpr uint32_t kFillLds = BIH_FILL_LDS;
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect,
                                                        const uint32_t *__restrict__ live,
                                                        const uint32_t *__restrict__ live_count,
                                                        uint32_t bins_x, uint32_t w, uint32_t h,
                                                        uint32_t tw, uint32_t th,
                                                        const uint32_t *__restrict__ off,
-                                                       uint32_t *__restrict__ fill,
-                                                       uint32_t *__restrict__ fill2,
+                                                       const uint32_t *__restrict__ cntq,
+                                                       uint32_t *__restrict__ cur,
                                                        const float4 *__restrict__ binrec,
                                                        const uint32_t *__restrict__ gstat,
                                                        float4 *__restrict__ list) {
     if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
-    for_rect_tiles(brect, live, live_count, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    constexpr uint32_t kS = kFillLds > 0 ? kFillLds : 1u;
+    __shared__ unsigned long long s_cnt[kS];
+    __shared__ uint32_t s_base[kBuckets][kS];
+    __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
+    __shared__ PairLds L;
+    const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid;
+    if (tid == 0) {
+        s_rect[0] = s_rect[2] = 0xffffu;
+        s_rect[1] = s_rect[3] = 0u;
+    }
+    __syncthreads();
+    if (j0 < *live_count) {
+        const uint2 q = brect[live[j0]];
+        const uint32_t bx0 = q.x & 0xffffu, bx1 = q.x >> 16, by0 = q.y & 0xffffu, by1 = q.y >> 16;
+        if (bx0 <= bx1) {
+            atomicMin(&s_rect[0], bx0);
+            atomicMax(&s_rect[1], bx1);
+            atomicMin(&s_rect[2], by0);
+            atomicMax(&s_rect[3], by1);
+        }
+    }
+    __syncthreads();
+    const uint32_t rx0 = s_rect[0], rx1 = s_rect[1], ry0 = s_rect[2], ry1 = s_rect[3];
+    const uint32_t rw = rx1 - rx0 + 1;
+    const bool use_lds = kFillLds > 0 && rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kFillLds;   // block-uniform
+    const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
+    // bucket q of tile b starts at off[b] + the counts of buckets 0 .. q-1
+    auto bucket_start = [&](uint32_t b, uint32_t q) {
+        uint32_t st = off[b];
+        for (uint32_t k = 0; k < q; ++k) st += cntq[(kBuckets - 1ull) * b + k];
+        return st;
+    };
+    if (use_lds) {
+        for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0ull;
+        __syncthreads();
+        for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
+            const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
+            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+            if (!cls) return;
+            const uint32_t q = entry_bucket(cls, cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th));
+            atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1ull << (kBucketBits * q));
+        });
+        __syncthreads();
+        for (uint32_t k = tid; k < rarea; k += kThreads) {
+            const unsigned long long c = s_cnt[k];
+            if (c) {
+                const uint32_t b = (ry0 + k / rw) * bins_x + rx0 + k % rw;
+                uint32_t st = off[b];
+                for (uint32_t q = 0; q < kBuckets; ++q) {
+                    const uint32_t cq = (uint32_t)((c >> (kBucketBits * q)) & kBucketMask);
+                    s_base[q][k] = cq ? st + atomicAdd(cur + (unsigned long long)kBuckets * b + q, cq) : 0u;
+                    if (q < kBuckets - 1u) st += cntq[(kBuckets - 1ull) * b + q];
+                }
+            }
+            s_cnt[k] = 0ull;
+        }
+        __syncthreads();
+    }
+    for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
         if (!cls) return;
-        const uint32_t b = by * bins_x + bx;
-        // fill: front cursors (zeroed); fill2: the counts k_bin_count left,
-        // counted down (off[b] + count - 1 = off[b + 1] - 1 first)
-        const uint32_t pos = cls == 2 ? off[b] + atomicAdd(fill + b, 1u)
-                                      : off[b] + atomicSub(fill2 + b, 1u) - 1u;
         // the entry's word 11: plan meta (bits 0-13) | pixel mask << 16
         const uint32_t pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
+        const uint32_t q = entry_bucket(cls, pm);
+        uint32_t pos;
+        if (use_lds) {
+            const uint32_t k = (by - ry0) * rw + (bx - rx0);
+            const unsigned long long r = atomicAdd(&s_cnt[k], 1ull << (kBucketBits * q));
+            pos = s_base[q][k] + (uint32_t)((r >> (kBucketBits * q)) & kBucketMask);
+        } else {
+            const uint32_t b = by * bins_x + bx;
+            pos = bucket_start(b, q) + atomicAdd(cur + (unsigned long long)kBuckets * b + q, 1u);
+        }
         float4 *o = list + 4ull * pos;
         o[0] = r0;
         o[1] = r1;
@@ -909,36 +1084,35 @@ bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h
     return true;
 }
 
-int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const int32_t *first_idx,
-                          const uint32_t *dup_cnt,
-                          const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
-                          uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream) {
+int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
+                          float *prim, const TreeHeader *hdr, const uint32_t *tri_leaf,
+                          const int32_t *leaf_parent, const int32_t *parent, const BinCamera &c,
+                          const BinBuffers &b, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
-    // gcount[0] = global list length, gcount[3] = alive triangles (k_bin_compact),
-    // gcount[4..5] = the list total as a 64-bit sum (k_bin_count)
-    hipError_t e = hipMemsetAsync(b.gcount, 0, 6 * sizeof(uint32_t), st);
-    if (e == hipSuccess) e = hipMemsetAsync(b.cnt, 0, (size_t)nb * sizeof(uint32_t), st);
-    if (e != hipSuccess) return (int)e;
-    if (U > 0) {
-        const dim3 g((U + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_bin_leaf, g, dim3(kThreads), 0, st, first_idx, dup_cnt, U, prim);
-
-    }
+    const uint4 *node_prim = reinterpret_cast<const uint4 *>(prim + 16ull * n);
     if (n > 0) {
+        // gcount[0] = global list length, gcount[3] = alive triangles,
+        // gcount[4..5] = the list total as a 64-bit sum (k_bin_count); cnt,
+        // cntq and cur (adjacent) zeroed
         const dim3 g((n + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_bin_alive_count, g, dim3(kThreads), 0, st, prim, n, b.brect, b.bcnt);
-        e = (hipError_t)scan_exclusive(b.bcnt, b.boff, g.x, b.bpart, b.gcount + 3, stream);
+        const uint32_t zero_words = (uint32_t)((reinterpret_cast<const char *>(b.cur + (size_t)kBuckets * nb) -
+                                                reinterpret_cast<const char *>(b.cnt)) / 4);
+        hipLaunchKernelGGL(k_cam_tris, g, dim3(kThreads), 0, st, tris, n, origin[0], origin[1], origin[2], prim,
+                           nodes, m, reinterpret_cast<uint4 *>(prim + 16ull * n),
+                           reinterpret_cast<unsigned long long *>(b.bmask), b.bcnt, b.cnt, zero_words, b.gcount);
+        hipError_t e = (hipError_t)scan_exclusive(b.bcnt, b.boff, g.x, b.bpart, b.gcount + 3, stream);
         if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(k_bin_compact, g, dim3(kThreads), 0, st, prim, n, b.boff, b.live);
-        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, leaf_parent,
+        hipLaunchKernelGGL(k_live_compact, g, dim3(kThreads), 0, st,
+                           reinterpret_cast<const unsigned long long *>(b.bmask), b.boff, b.live);
+        hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, tri_leaf, leaf_parent,
                            parent, b.path, b.brect, b.binrec, b.gcount,
                            b.glist, b.live, b.gcount + 3);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
-                           reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt,
+                           reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt, b.cntq,
                            reinterpret_cast<unsigned long long *>(b.gcount + 4));
     }
-    e = hipGetLastError();
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     // off[nb] = the total (list length)
     return scan_exclusive(b.cnt, b.off, nb, b.partials, b.off + nb, stream);
@@ -957,11 +1131,10 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t nb = b.bins_x * b.bins_y;
     const uint32_t *gstat = b.gcount + 1;
-    hipError_t e = hipMemsetAsync(b.cnt2, 0, (size_t)nb * sizeof(uint32_t), st);
-    if (e != hipSuccess) return (int)e;
+    (void)nb;   // the cursors were zeroed by k_cam_tris
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cnt2, b.cnt,
+                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cntq, b.cur,
                            reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
     if (n > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,

@@ -20,6 +20,7 @@
 #include <float.h>
 
 #include "bih_internal.h"
+#include "bih_device.h"
 
 namespace bih {
 namespace {
@@ -284,11 +285,6 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *l
 // every tile a block waits for is resident or done.  The flag and the value
 // share one 64-bit word, so relaxed device-scope atomics suffice (no L2
 // writeback/invalidate fences: each block's output is its own).
-constexpr uint32_t kScanAgg = 1u, kScanPre = 2u;
-__device__ __forceinline__ unsigned long long scan_word(uint32_t tag, uint32_t flag, uint32_t v) {
-    return ((unsigned long long)((tag << 2) | flag) << 32) | v;
-}
-
 __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, uint32_t *out, uint32_t n,
                                                            unsigned long long *status, uint32_t tag,
                                                            uint32_t *total_out) {
@@ -307,27 +303,7 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
     if (threadIdx.x == 0) {
-        uint32_t prefix = 0;
-        if (tile == 0) {
-            __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t j = tile - 1;;) {
-                const unsigned long long w =
-                    __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t hi = (uint32_t)(w >> 32);
-                if ((hi >> 2) != tag || (hi & 3u) == 0u) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                prefix += (uint32_t)w;
-                if ((hi & 3u) == kScanPre) break;
-                --j;
-            }
-            __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const uint32_t prefix = dev::lookback_prefix(status, tile, tag, tot);
         s_prefix = prefix;
         if (tile == gridDim.x - 1 && total_out) *total_out = prefix + tot;
     }
@@ -341,14 +317,13 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     }
 }
 
-std::atomic<uint32_t> g_scan_tag{0};
 
 // `partials`: scan_partials_words(n) u32 words, 8-byte aligned (status words)
 hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                           uint32_t *total_dev, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const uint32_t nb = (n + kScanTile - 1) / kScanTile;
-    const uint32_t tag = ((g_scan_tag.fetch_add(1) % 0x3FFFFFFFu) + 1u);   // 1 .. 2^30-1
+    const uint32_t tag = next_scan_tag();
     hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kThreads), 0, st, in, out, n,
                        reinterpret_cast<unsigned long long *>(partials), tag, total_dev);
     return hipGetLastError();
@@ -428,14 +403,19 @@ __global__ void k_run_flags(const uint32_t *__restrict__ keys, uint32_t n, uint3
     if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
 }
 
+// pos = the exclusive scan of the flags; rewritten in place to the leaf of
+// each sorted triangle (pos + flag - 1: DeviceTree::tri_leaf)
 __global__ void k_run_compact(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ flags,
-                              const uint32_t *__restrict__ pos, uint32_t n,
+                              uint32_t *pos, uint32_t n,
                               uint32_t *__restrict__ umc, int32_t *__restrict__ first) {
     uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i < n && flags[i]) {
-        umc[pos[i]] = keys[i];
-        first[pos[i]] = (int32_t)i;
+    if (i >= n) return;
+    const uint32_t f = flags[i], p = pos[i];
+    if (f) {
+        umc[p] = keys[i];
+        first[p] = (int32_t)i;
     }
+    pos[i] = p + f - 1u;
 }
 
 __global__ void k_run_counts(const int32_t *__restrict__ first, const TreeHeader *__restrict__ hdr,
@@ -745,6 +725,13 @@ int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *part
                    uint32_t *total_dev, void *stream) {
     return (int)exclusive_scan(in, out, n, partials, total_dev, (hipStream_t)stream);
 }
+// tags of the look-back status words (dev::lookback_prefix): 1 .. 2^30-1,
+// unique per call
+uint32_t next_scan_tag() {
+    static std::atomic<uint32_t> tag{0};
+    return (tag.fetch_add(1) % 0x3FFFFFFFu) + 1u;
+}
+
 size_t scan_partials_words(uint32_t n) { return 2 * (size_t)((n + kScanTile - 1) / kScanTile) + 2; }
 
 void free_tree_device(DeviceTree &t) {

@@ -583,8 +583,22 @@ static void tile_shape(uint32_t spp, uint32_t *tw, uint32_t *th) {
 // (Re)builds the frustum bins for `cam` and a w x h image on `st`, after the
 // primary-ray records; every render that read the old ones has finished
 // (the caller waited for them).  Synchronises `st` once to size the lists.
+// Runs the camera's primary-ray records (launch_prim) when `need_prim` and
+// the bins take no part.
+static int prim_only(bih_tree *tr, const bih_camera *cam, const float dmax[3], bool need_prim, hipStream_t st) {
+    if (!need_prim) return BIH_OK;
+    const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
+    return map_hip(bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx, tr->t.dup_cnt,
+                                    tr->t.leaf_parent, tr->t.parent, n_int, cam->origin, dmax, tr->prim, st));
+}
+
+// (Re)builds the frustum bins for `cam` and a w x h image on `st`; with
+// `need_prim` also the camera's primary-ray records (k_cam_tris, or
+// launch_prim when no bins are built).  Every render that read the old ones
+// has finished (the caller waited for them).  Synchronises `st` once to size
+// the lists the first time.
 static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], uint32_t w,
-                      uint32_t h, uint32_t spp, hipStream_t st) {
+                      uint32_t h, uint32_t spp, bool need_prim, hipStream_t st) {
     tr->bins_valid = true;
     tr->bins_usable = false;
     ++tr->bins_gen;
@@ -595,24 +609,27 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     bih::BinCamera bc;
-    if (w > 0xffffu || h > 0xffffu || !bih::bin_camera(reinterpret_cast<const float *>(cam), dmax, w, h,
-                                                        tw, th, &bc))
-        return BIH_OK;   // no bins: the kernel runs the shortcut passes instead
+    if (n == 0 || U < 2 || w > 0xffffu || h > 0xffffu ||
+        !bih::bin_camera(reinterpret_cast<const float *>(cam), dmax, w, h, tw, th, &bc))
+        return prim_only(tr, cam, dmax, need_prim, st);   // no bins: the kernel runs the shortcut passes instead
     bih::BinBuffers b;
     b.bins_x = (w + tw - 1) / tw;
     b.bins_y = (h + th - 1) / th;
     const size_t nb = (size_t)b.bins_x * b.bins_y;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t s_brect = al((size_t)n * 8), s_cnt = al(nb * 4), s_cnt2 = al(nb * 4), s_off = al((nb + 1) * 4),
-                 s_g = al(4), s_glist = al((size_t)n * 4 + 4),
+    const uint32_t nblk = (n + 255) / 256;   // k_cam_tris blocks (bih::kThreads)
+    // cnt, cntq and cur follow each other with no gap (k_cam_tris zeroes them as one range)
+    const size_t s_brect = al((size_t)n * 8), s_cnt = nb * 4, s_cntq = nb * 4 * (bih::kBinBuckets - 1),
+                 s_cur = al(nb * 4 * bih::kBinBuckets),
+                 s_off = al((nb + 1) * 4),
+                 s_g = al(6 * 4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
-                 s_gent = al((size_t)4097 * 64), s_live = al((size_t)n * 4 + 4);
-    const uint32_t nblk = (n + 255) / 256;   // k_bin_compact blocks (bih::kThreads)
-    const size_t s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
+                 s_gent = al((size_t)4097 * 64), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
+                 s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
                  s_bpart = al(bih::scan_partials_words(nblk) * 4);
-    const size_t need = s_brect + s_cnt + s_cnt2 + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
-                        s_live + s_bcnt + s_boff + s_bpart;
+    const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
+                        s_live + s_bmask + s_bcnt + s_boff + s_bpart;
     if (tr->bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -626,7 +643,8 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     char *p = tr->bins_mem;
     b.brect = reinterpret_cast<uint2 *>(p); p += s_brect;
     b.cnt = reinterpret_cast<uint32_t *>(p); p += s_cnt;
-    b.cnt2 = reinterpret_cast<uint32_t *>(p); p += s_cnt2;
+    b.cntq = reinterpret_cast<uint32_t *>(p); p += s_cntq;
+    b.cur = reinterpret_cast<uint32_t *>(p); p += s_cur;
     b.off = reinterpret_cast<uint32_t *>(p); p += s_off;
     b.gcount = reinterpret_cast<uint32_t *>(p); p += s_g;
     b.glist = reinterpret_cast<uint32_t *>(p); p += s_glist;
@@ -635,12 +653,14 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.path = reinterpret_cast<uint2 *>(p); p += s_path;
     float *gent = reinterpret_cast<float *>(p); p += s_gent;
     b.live = reinterpret_cast<uint32_t *>(p); p += s_live;
+    b.bmask = reinterpret_cast<uint32_t *>(p); p += s_bmask;
     b.bcnt = reinterpret_cast<uint32_t *>(p); p += s_bcnt;
     b.boff = reinterpret_cast<uint32_t *>(p); p += s_boff;
     b.bpart = reinterpret_cast<uint32_t *>(p);
-    const uint4 *node_prim = reinterpret_cast<const uint4 *>(tr->prim + 16ull * n);
-    int le = bih::launch_bin_footprints(tr->prim, n, tr->t.hdr, tr->t.first_idx, tr->t.dup_cnt, tr->t.leaf_parent,
-                                        tr->t.parent, node_prim, U, bc, b, st);
+    // the triangle records are rewritten in any case (k_cam_tris computes the
+    // alive list from them); the node records too
+    int le = bih::launch_bin_footprints(tr->t.tris_s, n, tr->t.nodes, U - 1, cam->origin, tr->prim, tr->t.hdr,
+                                        tr->t.scan_tmp, tr->t.leaf_parent, tr->t.parent, bc, b, st);
     if (le) return map_hip(le);
     hipError_t e = hipSuccess;
     // A list buffer from an earlier camera: build into it without a host
@@ -870,6 +890,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             tr->prim_cap = need;
             tr->prim_valid = false;
         }
+        // the frustum bins' build computes the records itself (k_cam_tris)
+        const bool want_bins = bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0;
+        bool need_prim = false;
         if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
             // |D| per component over the primary rays: D = (llc + u h + v vert) - O
             // (Camera.cu:18-20) is affine in (u, v) in [0, 1]^2, so its largest
@@ -880,10 +903,14 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             // checks it against the kernel's evaluation with offset origins)
             float dmax[3];
             (void)bih_camera_ray_bound(cam, dmax);
-            int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
-                                      tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
-                                      cam->origin, dmax, tr->prim, st);
-            if (le) return map_hip(le);
+            if (want_bins) {
+                need_prim = true;
+            } else {
+                int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
+                                          tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
+                                          cam->origin, dmax, tr->prim, st);
+                if (le) return map_hip(le);
+            }
             memcpy(tr->prim_origin, ob, sizeof ob);
             tr->prim_valid = true;
             tr->bins_valid = false;
@@ -891,17 +918,19 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             tr->cull_valid = false;
         }
         const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
-        if (bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0 &&
-            (!tr->bins_valid || !bins_key_ok)) {
-            if (tr->bins_valid || tr->bins_redo) {
-                // rewritten in place (the records' words 13-15 too)
-                rc = wait_renders(tr, st);
-                if (rc) return rc;
-            }
+        if (want_bins && (!tr->bins_valid || !bins_key_ok)) {
+            // rewritten in place (the triangle and node records too): after
+            // every render still reading them (a no-op wait when need_prim
+            // already waited above)
+            rc = wait_renders(tr, st);
+            if (rc) return rc;
             float dmax[3];
             (void)bih_camera_ray_bound(cam, dmax);
-            rc = build_bins(tr, cam, dmax, w, h, spp, st);
-            if (rc) return rc;
+            rc = build_bins(tr, cam, dmax, w, h, spp, need_prim, st);
+            if (rc) {
+                if (need_prim) tr->prim_valid = false;
+                return rc;
+            }
             tr->bins_redo = false;
         }
     }

@@ -42,5 +42,73 @@ __device__ __forceinline__ void camera_dir(const RenderArgs &a, float u, float v
     dz = ((a.cam[5] + u * a.cam[8]) + v * a.cam[11]) - a.cam[2];
 }
 
+// Primary-ray triangle record of one Morton-ordered triangle t = {v0, e1, e2}
+// for camera origin O: {e1, e2, s = O - v0, q = cross(s, e1), tnum =
+// dot(e2, q), 0, 0, 0} -- the ray-independent half of
+// RayTriangleIntersection (CUDAKernels.cu:18-19, :33, :40, :47), computed
+// once per origin instead of once per ray.  Returns tnum.
+__device__ __forceinline__ float tri_prim_record(const float *__restrict__ t, float ox, float oy, float oz,
+                                                 float *__restrict__ prim) {
+    const float v0x = t[0], v0y = t[1], v0z = t[2];
+    const float e1x = t[3], e1y = t[4], e1z = t[5];
+    const float e2x = t[6], e2y = t[7], e2z = t[8];
+    const float sx = ox - v0x, sy = oy - v0y, sz = oz - v0z;    // tvec
+    const float qx = sy * e1z - e1y * sz;                       // qvec = cross(tvec, e1)
+    const float qy = sz * e1x - e1z * sx;
+    const float qz = sx * e1y - e1x * sy;
+    const float tn = (e2x * qx + e2y * qy) + e2z * qz;          // dot(e2, qvec)
+    float4 *o = reinterpret_cast<float4 *>(prim);
+    o[0] = make_float4(e1x, e1y, e1z, e2x);
+    o[1] = make_float4(e2y, e2z, sx, sy);
+    o[2] = make_float4(sz, qx, qy, qz);
+    o[3] = make_float4(tn, 0.f, 0.f, 0.f);
+    return tn;
+}
+
+// A primary ray from O can hit a triangle only if its tnum is a positive
+// finite f32: t = tnum * (1/det) with 1/det > 0 finite for every lane that
+// passes the det test (CUDAKernels.cu:33-47), so tnum <= 0, +inf or NaN gives
+// t <= 0, inf or NaN, and the t > 0 && t < FLT_MAX test fails for every ray.
+__device__ __forceinline__ bool tnum_alive(float tn) {
+    return __float_as_uint(tn) - 1u < 0x7f7fffffu;   // 0 < bits < 0x7f800000
+}
+
+// Decoupled look-back (single-pass scan): tile `tile` of a grid publishes its
+// aggregate `tot`, adds its predecessors' published values walking back
+// until one carries an inclusive prefix, publishes its own inclusive prefix
+// and returns its exclusive prefix.  A status word is {tag:30 | flag:2 |
+// value:32} (flag 1 = aggregate, 2 = inclusive prefix); the tag is unique
+// per call (next_scan_tag), so the words need no memset between calls.
+// Tiles are blockIdx.x: workgroups dispatch in id order, so every tile a
+// block waits for is resident or done.  Flag and value share one 64-bit word:
+// relaxed device-scope atomics suffice.  One thread of the block calls it.
+constexpr uint32_t kScanAgg = 1u, kScanPre = 2u;
+__device__ __forceinline__ unsigned long long scan_word(uint32_t tag, uint32_t flag, uint32_t v) {
+    return ((unsigned long long)((tag << 2) | flag) << 32) | v;
+}
+__device__ __forceinline__ uint32_t lookback_prefix(unsigned long long *status, uint32_t tile, uint32_t tag,
+                                                    uint32_t tot) {
+    if (tile == 0) {
+        __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0u;
+    }
+    __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t prefix = 0;
+    for (uint32_t j = tile - 1;;) {
+        const unsigned long long w = __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = (uint32_t)(w >> 32);
+        if ((hi >> 2) != tag || (hi & 3u) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        prefix += (uint32_t)w;
+        if ((hi & 3u) == kScanPre) break;
+        --j;
+    }
+    __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    return prefix;
+}
+
 }  // namespace dev
 }  // namespace bih

@@ -44,6 +44,10 @@ constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
 constexpr uint32_t kBinGlobalMax = 4096;          // longer global lists: no bins (the shortcut walk)
 constexpr uint32_t kBinsUnusable = 0xFFFFFFFFu;   // bins status: lists not built (k_bin_status)
 constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue state per set
+#ifndef BIH_BUCKETS
+#define BIH_BUCKETS 6
+#endif
+constexpr uint32_t kBinBuckets = BIH_BUCKETS;     // list-order buckets per tile (bih_bins.hip)
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif
@@ -128,13 +132,15 @@ struct BinCamera {
 struct BinBuffers {
     uint32_t bins_x = 0, bins_y = 0;
     uint2 *brect = nullptr;       // [n] bin rectangle per triangle
-    uint32_t *cnt = nullptr;      // [nb] counts / fill cursors (front)
-    uint32_t *cnt2 = nullptr;     // [nb] fill cursors (back)
+    uint32_t *cnt = nullptr;      // [nb] entries per tile (k_bin_count); cntq and cur follow (zeroed together)
+    uint32_t *cntq = nullptr;     // [nb][kBinBuckets - 1] entries per tile in the buckets but the last
+    uint32_t *cur = nullptr;      // [nb][kBinBuckets] the fill's cursors per tile and bucket
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
     uint32_t *gcount = nullptr;   // [4] global list length, status (k_bin_status), list total, alive count
-    uint32_t *live = nullptr;     // [n] alive triangles (k_bin_compact)
-    uint32_t *bcnt = nullptr;     // [blocks] alive triangles per k_bin_compact block
-    uint32_t *boff = nullptr;     // [blocks + 1] their exclusive scan
+    uint32_t *live = nullptr;     // [n] alive triangles (k_live_compact)
+    uint32_t *bmask = nullptr;    // [blocks][4] u64 alive masks of k_cam_tris' blocks
+    uint32_t *bcnt = nullptr;     // [blocks] their counts
+    uint32_t *boff = nullptr;     // [blocks + 1] the counts' exclusive scan
     uint32_t *bpart = nullptr;    // its scan scratch
     uint32_t *glist = nullptr;    // [n] global list (triangles)
     uint32_t *partials = nullptr; // scan scratch
@@ -154,7 +160,8 @@ struct DeviceTree {
     float *tri_lo = nullptr, *tri_hi = nullptr;     // f32[3N]
     uint32_t *keys = nullptr, *vals = nullptr;      // sorted morton / tri idx
     uint32_t *keys2 = nullptr, *vals2 = nullptr;    // sort ping-pong
-    uint32_t *scan_tmp = nullptr;                   // scan scratch
+    uint32_t *scan_tmp = nullptr;                   // scan scratch; after the build the leaf of
+                                                    // each sorted triangle (k_run_compact)
     uint32_t *flags = nullptr;                      // u32[N+1]
     uint32_t *unique_mc = nullptr, *dup_cnt = nullptr;
     int32_t *first_idx = nullptr, *leaf_parent = nullptr;
@@ -222,14 +229,14 @@ int launch_fast_boxes(const float *tris, uint32_t n, const uint4 *nodes, const i
 bool render_uses_prim(uint32_t spp);
 
 // frustum bins (bih_bins.hip): camera setup (false: degenerate camera, no
-// bins), footprints + per-tile counts + offsets (needs the primary-ray
-// records; writes their words 13-15), then the lists
+// bins); then the camera's primary-ray records (launch_prim's triangle and
+// node records), the alive list, footprints, per-tile counts and offsets
 bool bin_camera(const float cam[12], const float dmax[3], uint32_t w, uint32_t h, uint32_t tw,
                 uint32_t th, BinCamera *out);
-int launch_bin_footprints(float *prim, uint32_t n, const TreeHeader *hdr, const int32_t *first_idx,
-                          const uint32_t *dup_cnt,
-                          const int32_t *leaf_parent, const int32_t *parent, const uint4 *node_prim,
-                          uint32_t U, const BinCamera &c, const BinBuffers &b, void *stream);
+int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uint32_t m, const float origin[3],
+                          float *prim, const TreeHeader *hdr, const uint32_t *tri_leaf,
+                          const int32_t *leaf_parent, const int32_t *parent, const BinCamera &c,
+                          const BinBuffers &b, void *stream);
 // lists of 64-byte entries (list: per-tile, gent: the global list's)
 // the status word gcount[1] (k_bin_status: the global list length, or
 // kBinsUnusable when the lists exceed `cap` entries or the global list
@@ -249,6 +256,7 @@ int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x
 int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                    uint32_t *total_dev, void *stream);
 size_t scan_partials_words(uint32_t n);
+uint32_t next_scan_tag();   // tag of a dev::lookback_prefix call (bih_device.h)
 
 // host XORWOW helpers (xorwow_host.cpp)
 void xorwow_seed(uint64_t seed, uint32_t v[5], uint32_t *d);

@@ -2452,8 +2452,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_order(const uint32_t *__rest
 // det test (CUDAKernels.cu:33-47), so tnum <= 0, +inf or NaN gives t <= 0,
 // inf or NaN, and the t > 0 && t < FLT_MAX test fails for every ray.
 __device__ __forceinline__ bool tri_alive(const float *prim, uint32_t k) {
-    const uint32_t b = __float_as_uint(prim[16ull * k + 12]);
-    return b - 1u < 0x7f7fffffu;                 // 0 < b < 0x7f800000
+    return dev::tnum_alive(prim[16ull * k + 12]);
 }
 
 // Leaf k can produce a hit only if one of its triangles [first[k],
@@ -2525,29 +2524,15 @@ __global__ void __launch_bounds__(kThreads) k_node_prim(const uint4 *__restrict_
 }
 
 // Primary-ray triangle records for the camera origin O (every primary ray of
-// a frame starts at O, Camera.cu:18-20): per Morton-ordered triangle
-// {e1, e2, s = O - v0, q = cross(s, e1), tnum = dot(e2, q), 0, 0, 0}, the
-// ray-independent half of RayTriangleIntersection (:18-19, :33, :40, :47),
-// computed once per origin instead of once per ray.
+// a frame starts at O, Camera.cu:18-20): dev::tri_prim_record per
+// Morton-ordered triangle.  (Renders through the frustum bins get the same
+// records from k_cam_tris, bih_bins.hip.)
 __global__ void __launch_bounds__(kThreads) k_tri_prim(const float *__restrict__ tris, uint32_t n,
                                                        float ox, float oy, float oz,
                                                        float *__restrict__ prim) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
-    const float *t = tris + 9ull * i;
-    const float v0x = t[0], v0y = t[1], v0z = t[2];
-    const float e1x = t[3], e1y = t[4], e1z = t[5];
-    const float e2x = t[6], e2y = t[7], e2z = t[8];
-    const float sx = ox - v0x, sy = oy - v0y, sz = oz - v0z;    // tvec
-    const float qx = sy * e1z - e1y * sz;                       // qvec = cross(tvec, e1)
-    const float qy = sz * e1x - e1z * sx;
-    const float qz = sx * e1y - e1x * sy;
-    const float tn = (e2x * qx + e2y * qy) + e2z * qz;          // dot(e2, qvec)
-    float4 *o = reinterpret_cast<float4 *>(prim + 16ull * i);
-    o[0] = make_float4(e1x, e1y, e1z, e2x);
-    o[1] = make_float4(e2y, e2z, sx, sy);
-    o[2] = make_float4(sz, qx, qy, qz);
-    o[3] = make_float4(tn, 0.f, 0.f, 0.f);
+    (void)dev::tri_prim_record(tris + 9ull * i, ox, oy, oz, prim + 16ull * i);
 }
 
 // ---------------------------------------------------------------------------

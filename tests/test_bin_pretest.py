@@ -270,22 +270,55 @@ def test_refined_bound_soup_reference_camera(bihrt_mod):
     assert h > 50_000 and r > 0.95 * h, (h, r)
 
 
+def _edge_margin(K0, Ku, Kv):
+    """edge_margin (bih_bins.hip): 2^-21 fl(|K0| + |Ku| + |Kv|) + 2^-125, f32."""
+    S = (np.abs(K0) + np.abs(Ku)).astype(F) + np.abs(Kv)
+    return (F(2.0 ** -21) * S.astype(F)).astype(F) + F(2.0 ** -125)
+
+
 def _tile_class(K, bx, by, w, h, tw, th):
-    """tile_class (bih_bins.hip) on f32 coefficient triples K = [(K0, Ku, Kv)] x 3."""
-    pad = 2.0 ** -20
+    """tile_class (bih_bins.hip), op for op in f32, on coefficient triples
+    K = [(K0, Ku, Kv)] x 3."""
+    pad = F(2.0 ** -20)
+    iw, ih = F(1.0) / F(w), F(1.0) / F(h)
     xe = np.minimum((bx + 1) * tw, w)
     ye = np.minimum((by + 1) * th, h)
-    u0, u1 = bx * tw / w - pad, xe / w + pad
-    v0, v1 = by * th / h - pad, ye / h + pad
+    u0 = (bx * tw).astype(F) * iw - pad
+    u1 = xe.astype(F) * iw + pad
+    v0 = (by * th).astype(F) * ih - pad
+    v1 = ye.astype(F) * ih + pad
     out = np.full(len(bx), 2)
-    for K0, Ku, Kv in K:
-        K0, Ku, Kv = (x.astype(np.float64) for x in (K0, Ku, Kv))
-        sl = 2.0 ** -22 * (np.abs(K0) + np.abs(Ku) + np.abs(Kv))
-        hi = K0 + np.maximum(Ku * u0, Ku * u1) + np.maximum(Kv * v0, Kv * v1)
-        lo = K0 + np.minimum(Ku * u0, Ku * u1) + np.minimum(Kv * v0, Kv * v1)
-        with np.errstate(invalid="ignore"):
-            out = np.where(hi < -sl, 0, np.where(~(lo > sl), np.minimum(out, 1), out))
+    with np.errstate(all="ignore"):
+        for K0, Ku, Kv in K:
+            K0, Ku, Kv = (np.asarray(x, F) for x in (K0, Ku, Kv))
+            T = _edge_margin(K0, Ku, Kv)
+            au0, au1, bv0, bv1 = Ku * u0, Ku * u1, Kv * v0, Kv * v1
+            hi = (K0 + np.fmax(au0, au1)) + np.fmax(bv0, bv1)
+            lo = (K0 + np.fmin(au0, au1)) + np.fmin(bv0, bv1)
+            out = np.where(hi < -T, 0, np.where(~(lo > T), np.minimum(out, 1), out))
     return out
+
+
+def _pixel_mask(K, bx, by, w, h):
+    """pixel_mask (bih_bins.hip) of 4 x 4 tiles, op for op in f32."""
+    pad = F(2.0 ** -20)
+    iw, ih = F(1.0) / F(w), F(1.0) / F(h)
+    x = bx[:, None] * 4 + np.arange(4)[None, :]
+    y = by[:, None] * 4 + np.arange(4)[None, :]
+    ua, ub = x.astype(F) * iw - pad, (x + 1).astype(F) * iw + pad
+    va, vb = y.astype(F) * ih - pad, (y + 1).astype(F) * ih + pad
+    m = np.full(len(bx), 0xFFFF, np.int64)
+    with np.errstate(all="ignore"):
+        for K0, Ku, Kv in K:
+            K0, Ku, Kv = (np.asarray(z, F)[:, None] for z in (K0, Ku, Kv))
+            T = _edge_margin(K0, Ku, Kv)
+            cu = K0 + np.fmax(Ku * ua, Ku * ub)
+            cv = np.fmax(Kv * va, Kv * vb)
+            for py in range(4):
+                for px in range(4):
+                    out = (cu[:, px] + cv[:, py]) < -T[:, 0]
+                    m = np.where(out, m & ~(1 << (4 * py + px)), m)
+    return m
 
 
 @pytest.mark.parametrize("size", [0.02, 0.3])
@@ -328,6 +361,11 @@ def test_tile_class_keeps_passing_samples(bihrt_mod, size):
     cls = _tile_class(K, px // tw, py // th, W, H, tw, th)
     assert not np.any(passed & (cls == 0)), int((passed & (cls == 0)).sum())
     assert np.all(passed[cls == 2])
+    # the pixel mask of the sample's tile keeps the sample's pixel
+    m = _pixel_mask(K, px // tw, py // th, W, H)
+    bit = (m >> (4 * (py % th) + (px % tw))) & 1
+    assert not np.any(passed & (bit == 0)), int((passed & (bit == 0)).sum())
+    assert (bit[cls == 1] == 0).sum() > 0.05 * (cls == 1).sum(), np.bincount(bit[cls == 1])
     # the test has teeth: many tiles are dropped (and, for the large
     # triangles, many are fully covered)
     assert (cls == 0).sum() > 0.1 * n, np.bincount(cls)
