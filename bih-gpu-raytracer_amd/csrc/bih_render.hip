@@ -1799,7 +1799,7 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 // one per item: a single head word saturates near 90 dequeues per us.
 // ---------------------------------------------------------------------------
 #ifndef BIH_BINS_WAVES_PER_EU
-#define BIH_BINS_WAVES_PER_EU 0   // 0: the compiler's choice
+#define BIH_BINS_WAVES_PER_EU 5   // 0: the compiler's choice (97 VGPRs, 4 waves); 5 fits 91 without spills
 #endif
 #if BIH_BINS_WAVES_PER_EU
 #define BIH_BINS_OCC __attribute__((amdgpu_waves_per_eu(BIH_BINS_WAVES_PER_EU, BIH_BINS_WAVES_PER_EU)))
@@ -1890,6 +1890,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    __shared__ uint32_t s_rs[5][kThreads];   // each lane's XORWOW state between the frames of an item
     // the slot's next launch starts from a zeroed set: every one of the 1024
     // per-CU slot lines (cu_key() spans 0..1023 sparsely, whatever the grid)
     if (tid == 0)
@@ -1910,7 +1911,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.band = xcc_id();
     q.left = 8;
     q.has_pending = false;
-    q.nf = a.nframes;
+    q.nf = 1u;   // an item covers every frame of the launch
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
     // timing experiment: items dealt round-robin over the waves (no atomics)
@@ -1945,11 +1946,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
 #endif
         BIH_PH(0);
         const uint4 hb = q.hb;
-        // multi-frame launch: a band's items repeat per frame
-        const uint32_t fj = a.nframes > 1 ? it / hb.w : 0u;
-        it -= fj * hb.w;
-        uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
-        if (BIH_QUEUE_AHEAD && it < hb.y) q.claim(lane);   // a live tile: claim the next item now
+        const uint32_t nf = a.nframes;   // multi-frame launch: an item covers its tile in every frame
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
             const uint32_t k = (it - hb.y) * 64u + lane;
@@ -1957,14 +1954,17 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 const uint32_t t = a.bin_queue[hb.x + hb.y + k];
                 const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
                 const uint32_t x0 = tx * TW;
-                for (uint32_t r = 0; r < TH; ++r) {
-                    const uint32_t lr = ty * TH + r;
-                    if (lr >= a.nrows) break;
-                    uint32_t *o = fout + (uint64_t)lr * a.w + x0;
-                    if (TW == 4 && x0 + 4 <= a.w && ((uintptr_t)o & 15u) == 0) {
-                        *reinterpret_cast<uint4 *>(o) = make_uint4(bgpix, bgpix, bgpix, bgpix);
-                    } else {
-                        for (uint32_t c = 0; c < TW && x0 + c < a.w; ++c) o[c] = bgpix;
+                for (uint32_t fj = 0; fj < nf; ++fj) {
+                    uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
+                    for (uint32_t r = 0; r < TH; ++r) {
+                        const uint32_t lr = ty * TH + r;
+                        if (lr >= a.nrows) break;
+                        uint32_t *o = fout + (uint64_t)lr * a.w + x0;
+                        if (TW == 4 && x0 + 4 <= a.w && ((uintptr_t)o & 15u) == 0) {
+                            *reinterpret_cast<uint4 *>(o) = make_uint4(bgpix, bgpix, bgpix, bgpix);
+                        } else {
+                            for (uint32_t c = 0; c < TW && x0 + c < a.w; ++c) o[c] = bgpix;
+                        }
                     }
                 }
             }
@@ -1979,90 +1979,117 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         const uint64_t lp = (uint64_t)lr * a.w + x;
         const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
         const uint32_t bin = (global_row(ty * TH, a.row0, a.band_h, a.band_step) / TH) * a.bins_x + tx;
-        float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
+        const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
+        // the pixel's XORWOW state at the start of the launch's first frame;
+        // each frame takes 2*SPP draws (cudaRender), sample s the draws
+        // 2s+1 and 2s+2 of its frame
+        // (kept in LDS between frames: registers stay those of the list walk)
         if (valid) {
-            float ru = 0.f, rv = 0.f;
-            ray_jitter<SPP>(a, lp, s, ru, rv, fj);
-            const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
-            uf = ((float)x + ru) / fw;       // CUDAKernels.cu:414-415
-            vf = ((float)y + rv) / fh;
-            camera_dir(a, uf, vf, dx, dy, dz);
+            const uint64_t P = (uint64_t)a.nrows * a.w;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) s_rs[i][tid] = a.rng_in[(uint64_t)i * P + lp];
         }
-        // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
-        const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-        const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
-        float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
-        float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
-        const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
-        const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
-        bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
-        if (tymin > tMin) tMin = tymin;
-        if (tymax < tMax) tMax = tymax;
-        const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
-        const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
-        in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
-        if (tzmin > tMin) tMin = tzmin;
-        if (tzmax < tMax) tMax = tzmax;
-        const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
-        unsigned long long hits = 0ull, undecided = 0ull;
-        BIH_PH(2);
-        // bins_ok: the lists were built (k_bin_status); else the exact walk decides
-        const bool bins_ok = *a.bin_gstat != kBinsUnusable;
-        if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
-            uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
-            const unsigned long long found = bin_walk<LOG2SPP == 2>(a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand,
-                                                      cmeta, cent, fc_ent, fc_mt, pf);
-            if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
-            BIH_PH(3);
-            const bool ok = ((found >> lane) & 1ull) &&
-                            ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
-            hits = __ballot(ok);
-            undecided = live & found & ~hits;
-            BIH_PH(4);
-#if BIH_FAST_COUNTERS
-            {   // bin counters (bih_sync prints them): candidates decided by a
-                // plan, and plans that disagree with the root-path check (0)
-                const bool fnd = ((found >> lane) & 1ull) != 0ull;
-                const bool planned = fnd && ((cand >> 31) || (cmeta & 3u) != 3u);
-                const bool pv = fnd && path_verify(a.bin_path, cand & 0x7fffffffu, ix, iy, iz, tMin, tMax);
-                const unsigned long long rb = __ballot(planned), bad = __ballot(planned && (pv != ok));
-                if (lane == 0) {
-                    atomicAdd(a.work + 38, (uint32_t)__popcll(bad));
-                    atomicAdd(a.work + 39, (uint32_t)__popcll(rb));
-                    atomicAdd(a.work + 40, 1u);
-                    atomicAdd(a.work + 41, (uint32_t)__popcll(live));
-                    atomicAdd(a.work + 42, fc_ent);
-                    atomicAdd(a.work + 43, fc_mt);
-                    atomicAdd(a.work + 44, (uint32_t)__popcll(found));
-                    atomicAdd(a.work + 45, (uint32_t)__popcll(hits));
-                    atomicAdd(a.work + 46, (uint32_t)__popcll(undecided));
-                    atomicAdd(a.work + 47, found != live ? 1u : 0u);
+        uint32_t dfr = a.d_base;   // Weyl counter at the start of frame fj
+        for (uint32_t fj = 0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
+            uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
+            float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
+            if (valid) {
+                // the frame's 2*SPP draws on every lane (uniform control
+                // flow); rs ends at the next frame's state
+                float ru = 0.f, rv = 0.f;
+                uint32_t d = dfr, rs[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) rs[i] = s_rs[i][tid];
+#pragma unroll 8
+                for (uint32_t k = 0; k < 2u * SPP; ++k) {
+                    const float f = xorwow_uniform(rs, d);
+                    if (k == 2u * s) ru = f;
+                    if (k == 2u * s + 1u) rv = f;
                 }
+                if (fj + 1u < nf) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
+                }
+                uf = ((float)x + ru) / fw;       // CUDAKernels.cu:414-415
+                vf = ((float)y + rv) / fh;
+                camera_dir(a, uf, vf, dx, dy, dz);
             }
+            // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
+            const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+            const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+            float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+            float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+            const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+            const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+            bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
+            if (tymin > tMin) tMin = tymin;
+            if (tymax < tMax) tMax = tymax;
+            const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+            const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+            in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+            if (tzmin > tMin) tMin = tzmin;
+            if (tzmax < tMax) tMax = tzmax;
+            const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
+            unsigned long long hits = 0ull, undecided = 0ull;
+            BIH_PH(2);
+            // bins_ok: the lists were built (k_bin_status); else the exact walk decides
+            const bool bins_ok = *a.bin_gstat != kBinsUnusable;
+            if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
+                uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
+                const unsigned long long found = bin_walk<LOG2SPP == 2>(a, prims, bin, uf, vf, dx, dy, dz, live, lane,
+                                                                        cand, cmeta, cent, fc_ent, fc_mt, pf);
+                if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
+                BIH_PH(3);
+                const bool ok = ((found >> lane) & 1ull) &&
+                                ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
+                hits = __ballot(ok);
+                undecided = live & found & ~hits;
+                BIH_PH(4);
+#if BIH_FAST_COUNTERS
+                {   // bin counters (bih_sync prints them): candidates decided by a
+                    // plan, and plans that disagree with the root-path check (0)
+                    const bool fnd = ((found >> lane) & 1ull) != 0ull;
+                    const bool planned = fnd && ((cand >> 31) || (cmeta & 3u) != 3u);
+                    const bool pv = fnd && path_verify(a.bin_path, cand & 0x7fffffffu, ix, iy, iz, tMin, tMax);
+                    const unsigned long long rb = __ballot(planned), bad = __ballot(planned && (pv != ok));
+                    if (lane == 0) {
+                        atomicAdd(a.work + 38, (uint32_t)__popcll(bad));
+                        atomicAdd(a.work + 39, (uint32_t)__popcll(rb));
+                        atomicAdd(a.work + 40, 1u);
+                        atomicAdd(a.work + 41, (uint32_t)__popcll(live));
+                        atomicAdd(a.work + 42, fc_ent);
+                        atomicAdd(a.work + 43, fc_mt);
+                        atomicAdd(a.work + 44, (uint32_t)__popcll(found));
+                        atomicAdd(a.work + 45, (uint32_t)__popcll(hits));
+                        atomicAdd(a.work + 46, (uint32_t)__popcll(undecided));
+                        atomicAdd(a.work + 47, found != live ? 1u : 0u);
+                    }
+                }
 #endif
-            if (a.dbg & 4u) {              // tests: every live lane to the fallback
-                hits = 0ull;
-                undecided = live;
+                if (a.dbg & 4u) {              // tests: every live lane to the fallback
+                    hits = 0ull;
+                    undecided = live;
+                }
+            } else if (live) {
+                undecided = live;              // one leaf (U == 1) or no lists: the exact walk decides
             }
-        } else if (live) {
-            undecided = live;              // one leaf (U == 1) or no lists: the exact walk decides
-        }
-        if (undecided) {
-            uint32_t r = 0;
-            if (lane == 0) r = atomicAdd(a.bin_heads + 8 * 32, 1u);
-            r = __builtin_amdgcn_readfirstlane(r);
-            if (lane < 6) {
-                const uint32_t v[6] = {tile, (uint32_t)undecided, (uint32_t)(undecided >> 32), (uint32_t)hits,
-                                       (uint32_t)(hits >> 32), fj};
-                a.bin_fb[(uint64_t)r * kFbWords + lane] = v[lane];
+            if (undecided) {
+                uint32_t r = 0;
+                if (lane == 0) r = atomicAdd(a.bin_heads + 8 * 32, 1u);
+                r = __builtin_amdgcn_readfirstlane(r);
+                if (lane < 6) {
+                    const uint32_t v[6] = {tile, (uint32_t)undecided, (uint32_t)(undecided >> 32), (uint32_t)hits,
+                                           (uint32_t)(hits >> 32), fj};
+                    a.bin_fb[(uint64_t)r * kFbWords + lane] = v[lane];
+                }
+                continue;
             }
-            continue;
+            if (valid && s == SPP - 1) {
+                const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
+                fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
+            }
+            BIH_PH(5);
         }
-        if (valid && s == SPP - 1) {
-            const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
-            fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
-        }
-        BIH_PH(5);
     }
 #if BIH_PHASES
     if (lane == 0)
