@@ -710,16 +710,19 @@ __device__ __forceinline__ uint32_t entry_bucket(int cls, uint32_t pm) {
 // triangles are Morton neighbours, so their footprints share tiles: the block
 // counts in LDS over the bounding rectangle of its footprints and adds each
 // non-zero count to the global counters once.  Blocks whose rectangle exceeds
-// kCountLds tiles count with global atomics directly.
-constexpr uint32_t kCountLds = 2048;
+// kBlockTiles tiles count with global atomics directly.  The block's LDS
+// counts also go to blkcnt[block][..] for k_bin_fill, which takes the same
+// blocks and rectangles (a pass of its own would recount them).
+constexpr uint32_t kBlockTiles = kBinBlockTiles;
 __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict__ brect,
                                                         const uint32_t *__restrict__ live,
                                                         const uint32_t *__restrict__ live_count,
                                                         uint32_t bins_x, const float4 *__restrict__ binrec,
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
                                                         uint32_t *__restrict__ cnt, uint32_t *__restrict__ cntq,
+                                                        unsigned long long *__restrict__ blkcnt,
                                                         unsigned long long *__restrict__ total64) {
-    __shared__ unsigned long long s_cnt[kCountLds];
+    __shared__ unsigned long long s_cnt[kBlockTiles];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
     __shared__ unsigned long long s_tot;   // the block's entries (64-bit: the list total may pass 2^32)
     __shared__ PairLds L;
@@ -743,7 +746,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     __syncthreads();
     const uint32_t rx0 = s_rect[0], rx1 = s_rect[1], ry0 = s_rect[2], ry1 = s_rect[3];
     const uint32_t rw = rx1 - rx0 + 1;
-    const bool use_lds = rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kCountLds;   // block-uniform
+    const bool use_lds = rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kBlockTiles;   // block-uniform
     const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
     for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0ull;
     __syncthreads();
@@ -766,6 +769,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     __syncthreads();
     for (uint32_t k = tid; k < rarea; k += kThreads) {
         const unsigned long long c = s_cnt[k];
+        blkcnt[(uint64_t)blockIdx.x * kBlockTiles + k] = c;
         if (!c) continue;
         const uint32_t b = (ry0 + k / rw) * bins_x + rx0 + k % rw;
         uint32_t all = 0;
@@ -783,18 +787,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
 // The lists: each (triangle, tile) pair k_bin_count counted copies the
 // triangle's 64-byte entry into the tile's list, in its bucket's range
 // (off[b] + the counts of the buckets before it) at a position from the
-// bucket's cursor cur[kBuckets * b + q] (zeroed).  When the block's tile rectangle
-// fits kFillLds tiles, a first pass counts the block's entries per (tile,
-// bucket) in LDS, one global atomic per (tile, bucket) reserves their range,
-// and a second pass ranks them through LDS atomics; larger rectangles take one
-// global atomic per entry.  (Per-entry global atomics throughout cost 0.10 of
-// this kernel's 0.15 ms.)  Within a bucket the order is the blocks' (Morton
-// order, roughly) -- it can change which candidate a lane verifies, never a
-// pixel.
-#ifndef BIH_FILL_LDS
-#define BIH_FILL_LDS 512
-#endif
-constexpr uint32_t kFillLds = BIH_FILL_LDS;
+// bucket's cursor cur[kBuckets * b + q] (zeroed).  When the block's tile
+// rectangle fits kBlockTiles tiles, k_bin_count's per-(tile, bucket) counts
+// of the same block (blkcnt) are reserved with one global atomic per (tile,
+// bucket), and the pass over the pairs ranks them through LDS atomics;
+// larger rectangles take one global atomic per entry.  (Per-entry global
+// atomics throughout cost 0.10 of this kernel's 0.15 ms.)  Within a bucket
+// the order is the blocks' (Morton order, roughly) -- it can change which
+// candidate a lane verifies, never a pixel.
 __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__ brect,
                                                        const uint32_t *__restrict__ live,
                                                        const uint32_t *__restrict__ live_count,
@@ -802,12 +802,13 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        uint32_t tw, uint32_t th,
                                                        const uint32_t *__restrict__ off,
                                                        const uint32_t *__restrict__ cntq,
+                                                       const unsigned long long *__restrict__ blkcnt,
                                                        uint32_t *__restrict__ cur,
                                                        const float4 *__restrict__ binrec,
                                                        const uint32_t *__restrict__ gstat,
                                                        float4 *__restrict__ list) {
     if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
-    constexpr uint32_t kS = kFillLds > 0 ? kFillLds : 1u;
+    constexpr uint32_t kS = kBlockTiles;
     __shared__ unsigned long long s_cnt[kS];
     __shared__ uint32_t s_base[kBuckets][kS];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
@@ -831,7 +832,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
     __syncthreads();
     const uint32_t rx0 = s_rect[0], rx1 = s_rect[1], ry0 = s_rect[2], ry1 = s_rect[3];
     const uint32_t rw = rx1 - rx0 + 1;
-    const bool use_lds = kFillLds > 0 && rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kFillLds;   // block-uniform
+    const bool use_lds = rx0 <= rx1 && (uint64_t)rw * (ry1 - ry0 + 1) <= kBlockTiles;   // block-uniform
     const uint32_t rarea = use_lds ? rw * (ry1 - ry0 + 1) : 0u;
     // bucket q of tile b starts at off[b] + the counts of buckets 0 .. q-1
     auto bucket_start = [&](uint32_t b, uint32_t q) {
@@ -840,18 +841,8 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
         return st;
     };
     if (use_lds) {
-        for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0ull;
-        __syncthreads();
-        for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
-            const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
-            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
-            if (!cls) return;
-            const uint32_t q = entry_bucket(cls, cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th));
-            atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1ull << (kBucketBits * q));
-        });
-        __syncthreads();
         for (uint32_t k = tid; k < rarea; k += kThreads) {
-            const unsigned long long c = s_cnt[k];
+            const unsigned long long c = blkcnt[(uint64_t)blockIdx.x * kBlockTiles + k];   // k_bin_count's
             if (c) {
                 const uint32_t b = (ry0 + k / rw) * bins_x + rx0 + k % rw;
                 uint32_t st = off[b];
@@ -1110,6 +1101,7 @@ int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uin
                            b.glist, b.live, b.gcount + 3);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt, b.cntq,
+                           reinterpret_cast<unsigned long long *>(b.blkcnt),
                            reinterpret_cast<unsigned long long *>(b.gcount + 4));
     }
     const hipError_t e = hipGetLastError();
@@ -1134,7 +1126,8 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
     (void)nb;   // the cursors were zeroed by k_cam_tris
     if (n > 0)
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cntq, b.cur,
+                           b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cntq,
+                           reinterpret_cast<const unsigned long long *>(b.blkcnt), b.cur,
                            reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
     if (n > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,

@@ -627,9 +627,10 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
                  s_gent = al((size_t)4097 * 64), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
                  s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
-                 s_bpart = al(bih::scan_partials_words(nblk) * 4);
+                 s_bpart = al(bih::scan_partials_words(nblk) * 4),
+                 s_blkcnt = al((size_t)nblk * bih::kBinBlockTiles * 8);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
-                        s_live + s_bmask + s_bcnt + s_boff + s_bpart;
+                        s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt;
     if (tr->bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -656,7 +657,8 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.bmask = reinterpret_cast<uint32_t *>(p); p += s_bmask;
     b.bcnt = reinterpret_cast<uint32_t *>(p); p += s_bcnt;
     b.boff = reinterpret_cast<uint32_t *>(p); p += s_boff;
-    b.bpart = reinterpret_cast<uint32_t *>(p);
+    b.bpart = reinterpret_cast<uint32_t *>(p); p += s_bpart;
+    b.blkcnt = reinterpret_cast<uint32_t *>(p);
     // the triangle records are rewritten in any case (k_cam_tris computes the
     // alive list from them); the node records too
     int le = bih::launch_bin_footprints(tr->t.tris_s, n, tr->t.nodes, U - 1, cam->origin, tr->prim, tr->t.hdr,

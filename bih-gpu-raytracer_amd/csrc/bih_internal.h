@@ -48,6 +48,10 @@ constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue sta
 #define BIH_BUCKETS 6
 #endif
 constexpr uint32_t kBinBuckets = BIH_BUCKETS;     // list-order buckets per tile (bih_bins.hip)
+#ifndef BIH_BLOCK_TILES
+#define BIH_BLOCK_TILES 512
+#endif
+constexpr uint32_t kBinBlockTiles = BIH_BLOCK_TILES;   // tile rectangle of a bins block counted in LDS
 #ifndef BIH_PACKET_COUNTERS
 #define BIH_PACKET_COUNTERS 0
 #endif
@@ -135,6 +139,7 @@ struct BinBuffers {
     uint32_t *cnt = nullptr;      // [nb] entries per tile (k_bin_count); cntq and cur follow (zeroed together)
     uint32_t *cntq = nullptr;     // [nb][kBinBuckets - 1] entries per tile in the buckets but the last
     uint32_t *cur = nullptr;      // [nb][kBinBuckets] the fill's cursors per tile and bucket
+    uint32_t *blkcnt = nullptr;   // [blocks][kBinBlockTiles] u64: k_bin_count's per-block (tile, bucket) counts
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
     uint32_t *gcount = nullptr;   // [4] global list length, status (k_bin_status), list total, alive count
     uint32_t *live = nullptr;     // [n] alive triangles (k_live_compact)

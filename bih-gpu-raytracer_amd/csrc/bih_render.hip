@@ -1799,7 +1799,7 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 // one per item: a single head word saturates near 90 dequeues per us.
 // ---------------------------------------------------------------------------
 #ifndef BIH_BINS_WAVES_PER_EU
-#define BIH_BINS_WAVES_PER_EU 5   // 0: the compiler's choice (97 VGPRs, 4 waves); 5 fits 91 without spills
+#define BIH_BINS_WAVES_PER_EU 0   // 0: the compiler's choice (97 VGPRs, 4 waves: 0.048 vs 0.050 ms/frame forced to 5)
 #endif
 #if BIH_BINS_WAVES_PER_EU
 #define BIH_BINS_OCC __attribute__((amdgpu_waves_per_eu(BIH_BINS_WAVES_PER_EU, BIH_BINS_WAVES_PER_EU)))
