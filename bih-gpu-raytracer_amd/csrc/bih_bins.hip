@@ -31,7 +31,8 @@
 // one keeps it as a candidate; it stands only after fast_verify replays the
 // reference's BIH decisions along the leaf's root path (bih_render.hip).
 //
-// List entries are 64-byte records {edge pre-test (9 f32), triangle, leaf}:
+// List entries are 48-byte records {edge pre-test (9 f32), triangle, leaf, plan meta |
+// pixel mask}; the plan values stay in the triangle's 64-byte record (binrec):
 //   edge pre-test: MT accepting direction D implies (miss_bary) the exact
 //     line's barycentrics u* >= -a, v* >= -b, u* + v* <= 1 + c, i.e. with
 //     det* > 0: D.Gu >= 0, D.Gv >= 0, D.Gw >= 0 for Gu = Nu + a Nd,
@@ -785,7 +786,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
 }
 
 // The lists: each (triangle, tile) pair k_bin_count counted copies the
-// triangle's 64-byte entry into the tile's list, in its bucket's range
+// first 48 bytes of the triangle's record into the tile's list, in its bucket's range
 // (off[b] + the counts of the buckets before it) at a position from the
 // bucket's cursor cur[kBuckets * b + q] (zeroed).  When the block's tile
 // rectangle fits kBlockTiles tiles, k_bin_count's per-(tile, bucket) counts
@@ -872,15 +873,14 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
             const uint32_t b = by * bins_x + bx;
             pos = bucket_start(b, q) + atomicAdd(cur + (unsigned long long)kBuckets * b + q, 1u);
         }
-        float4 *o = list + 4ull * pos;
+        float4 *o = list + (uint64_t)kBinEntryF4 * pos;
         o[0] = r0;
         o[1] = r1;
         o[2] = make_float4(r2.x, r2.y, r2.z, __uint_as_float((__float_as_uint(r2.w) & 0xFFFFu) | (pm << 16)));
-        o[3] = binrec[4ull * i + 3];
     });
 }
 
-// The global list's entries (the same 64-byte records); gstat as k_bin_status
+// The global list's entries (the same 48-byte entries); gstat as k_bin_status
 // left it (a grid over kBinGlobalMax entries: no host copy of the count).
 __global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restrict__ gstat,
                                                         const uint32_t *__restrict__ glist,
@@ -890,9 +890,10 @@ __global__ void __launch_bounds__(kThreads) k_bin_gfill(const uint32_t *__restri
     const uint32_t gn = *gstat;
     if (gn == kBinsUnusable || j >= gn) return;
     const uint32_t i = glist[j];
-    for (int k = 0; k < 4; ++k) gent[4ull * j + k] = binrec[4ull * i + k];
+    for (uint32_t k = 0; k < 2; ++k) gent[(uint64_t)kBinEntryF4 * j + k] = binrec[4ull * i + k];
     const float4 r2 = binrec[4ull * i + 2];   // every pixel of every tile
-    gent[4ull * j + 2] = make_float4(r2.x, r2.y, r2.z, __uint_as_float(__float_as_uint(r2.w) | 0xFFFF0000u));
+    gent[(uint64_t)kBinEntryF4 * j + 2] =
+        make_float4(r2.x, r2.y, r2.z, __uint_as_float(__float_as_uint(r2.w) | 0xFFFF0000u));
 }
 
 // The bins' device status word (gstat = gcount + 1, RenderArgs::bin_gstat):

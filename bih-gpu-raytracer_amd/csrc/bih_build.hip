@@ -51,6 +51,31 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 }
 
 // ---------------------------------------------------------------------------
+// Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
+// (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
+// by k_prep_final.  The build is a deterministic function of the soup, so an
+// unchanged hash after a rebuild means an unchanged tree, and the per-camera
+// structures derived from it (bih_capi.cpp finish_build) stay valid.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ void content_word(uint32_t w, uint32_t i, uint32_t &x, uint32_t &y) {
+    x ^= fmix32(w ^ (i * 0x9E3779B1u));
+    y ^= fmix32((w + 0x165667B1u) ^ fmix32(i + 0x27D4EB2Fu));
+}
+
+// Triangle AABB on one axis with std::minmax's rules (App.cpp:103-142):
+// leftmost min, rightmost max (k_prep; k_seg_leaf recomputes it bit-equal).
+__device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float &m, float &M) {
+    m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
+    M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
+}
+
 // k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
 // the scene AABB.  The reference folds triangles sequentially with
 // std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
@@ -64,17 +89,20 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
                                                    unsigned long long *__restrict__ part) {
     unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
     uint32_t bad = 0;
+    uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
         const float *p = v + 9ull * i;
         float q[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) q[k] = p[k];
 #pragma unroll
+        for (int k = 0; k < 9; ++k) content_word(__float_as_uint(q[k]), 9u * i + (uint32_t)k, hx, hy);
+#pragma unroll
         for (int a = 0; a < 3; ++a) {
             float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
             bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
-            float m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
-            float M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
+            float m, M;
+            axis_minmax(x0, x1, x2, m, M);
             lo[3ull * i + a] = m;
             hi[3ull * i + a] = M;
             unsigned long long tie = 0xFFFFFFFFull - i;
@@ -86,7 +114,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
     }
     // wave reduce, block reduce through LDS, one partial per block (the
     // single-block k_prep_final folds them: no contended atomics)
-    __shared__ unsigned long long s_key[6][kThreads / 64];
+    __shared__ unsigned long long s_key[7][kThreads / 64];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -96,6 +124,10 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             kmax[a] = oM > kmax[a] ? oM : kmax[a];
         }
     }
+    for (int off = 32; off > 0; off >>= 1) {
+        hx ^= __shfl_xor(hx, off);
+        hy ^= __shfl_xor(hy, off);
+    }
     const unsigned long long anybad = __ballot(bad);
     const uint32_t wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -104,15 +136,16 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             s_key[a][wv] = kmin[a];
             s_key[3 + a][wv] = kmax[a];
         }
+        s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
         if (anybad) atomicOr(&hdr->nonfinite, 1u);
     }
     __syncthreads();
-    if (threadIdx.x < 6) {
+    if (threadIdx.x < 7) {
         const int a = threadIdx.x;
         unsigned long long r = s_key[a][0];
         for (uint32_t w = 1; w < kThreads / 64; ++w) {
             const unsigned long long o = s_key[a][w];
-            r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+            r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
         part[(size_t)a * gridDim.x + blockIdx.x] = r;
     }
@@ -135,45 +168,6 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
     }
 }
 
-// Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
-// (32-bit arithmetic: HBM-bound).  The build is a deterministic function of
-// the soup, so an unchanged hash after a rebuild means an unchanged tree, and
-// the per-camera structures derived from it (bih_capi.cpp finish_build) stay
-// valid.
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x85ebca6bu;
-    h ^= h >> 13;
-    h *= 0xc2b2ae35u;
-    h ^= h >> 16;
-    return h;
-}
-__global__ void __launch_bounds__(kThreads) k_content_hash(const uint32_t *__restrict__ v, uint32_t words,
-                                                           TreeHeader *hdr) {
-    __shared__ uint32_t s_x[kThreads / 64], s_y[kThreads / 64];
-    uint32_t x = 0u, y = 0u;
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < words; i += gridDim.x * kThreads) {
-        const uint32_t w = v[i];
-        x ^= fmix32(w ^ (i * 0x9E3779B1u));
-        y ^= fmix32((w + 0x165667B1u) ^ fmix32(i + 0x27D4EB2Fu));
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        x ^= __shfl_xor(x, o);
-        y ^= __shfl_xor(y, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_x[threadIdx.x >> 6] = x;
-        s_y[threadIdx.x >> 6] = y;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {   // one atomic per block (a single address: few blocks)
-        for (int k = 1; k < kThreads / 64; ++k) {
-            x ^= s_x[k];
-            y ^= s_y[k];
-        }
-        if (x | y) atomicXor(&hdr->content, ((unsigned long long)y << 32) | x);
-    }
-}
 
 __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
                                                          const float *__restrict__ lo,
@@ -182,7 +176,7 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
                                                          const unsigned long long *__restrict__ part,
                                                          uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
-    __shared__ unsigned long long s_red[6][kThreads / 64];
+    __shared__ unsigned long long s_red[7][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -197,7 +191,18 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
         }
         if (lane == 0) s_red[a][wv] = r;
     }
+    {   // the content hash: XOR of the blocks' partials
+        unsigned long long hxy = 0ull;
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= part[(size_t)6 * nparts + i];
+        for (int off = 32; off > 0; off >>= 1) hxy ^= __shfl_xor(hxy, off);
+        if (lane == 0) s_red[6][wv] = hxy;
+    }
     __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long hxy = 0ull;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) hxy ^= s_red[6][w];
+        hdr->content = hxy;
+    }
     const int a = threadIdx.x;
     if (a >= 3) return;
     if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
@@ -527,10 +532,28 @@ __device__ __forceinline__ uint64_t seg_level_off(uint64_t nn, int L) {
     return off;
 }
 
+// Sorted triangle i as the render reads it: {v0, e1 = v1 - v0, e2 = v2 - v0}
+// (CUDAKernels.cu:18-19), from the input triangle p; returns its AABB (the
+// values k_prep wrote, axis_minmax).
+__device__ __forceinline__ void pack_tri(const float *__restrict__ p, float *__restrict__ o, float lo[3],
+                                         float hi[3]) {
+    float q[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) q[k] = p[k];
+    o[0] = q[0]; o[1] = q[1]; o[2] = q[2];
+    o[3] = q[3] - q[0]; o[4] = q[4] - q[1]; o[5] = q[5] - q[2];   // v0v1, CUDAKernels.cu:18
+    o[6] = q[6] - q[0]; o[7] = q[7] - q[1]; o[8] = q[8] - q[2];   // v0v2, :19
+#pragma unroll
+    for (int a = 0; a < 3; ++a) axis_minmax(q[a], q[3 + a], q[6 + a], lo[a], hi[a]);
+}
+
+// Leaf boxes, and the sorted triangle records of each leaf's run (the runs
+// partition the sorted triangles: k_pack_tris' work, read once with the
+// vertices the boxes come from).
 __global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restrict__ hdr,
                                                        const uint32_t *__restrict__ tri_idx,
-                                                       const float *__restrict__ lo,
-                                                       const float *__restrict__ hi,
+                                                       const float *__restrict__ v,
+                                                       float *__restrict__ tris_s,
                                                        const int32_t *__restrict__ first,
                                                        const uint32_t *__restrict__ cnt,
                                                        float *__restrict__ seg, uint64_t cap) {
@@ -541,15 +564,14 @@ __global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restr
     const int32_t f = first[k];
     const uint32_t c = cnt[k];
     float blo[3], bhi[3];
-    const uint32_t t0 = tri_idx[f];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { blo[a] = lo[3ull * t0 + a]; bhi[a] = hi[3ull * t0 + a]; }
+    pack_tri(v + 9ull * tri_idx[f], tris_s + 9ull * f, blo, bhi);
     for (uint32_t i = 1; i < c; ++i) {
-        const uint32_t t = tri_idx[f + i];
+        float tlo[3], thi[3];
+        pack_tri(v + 9ull * tri_idx[f + i], tris_s + 9ull * (f + i), tlo, thi);
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            blo[a] = tmin(blo[a], lo[3ull * t + a]);
-            bhi[a] = tmax(bhi[a], hi[3ull * t + a]);
+            blo[a] = tmin(blo[a], tlo[a]);
+            bhi[a] = tmax(bhi[a], thi[a]);
         }
     }
 #pragma unroll
@@ -689,17 +711,15 @@ __global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__res
     nodes[p] = nd;
 }
 
-__global__ void __launch_bounds__(kThreads) k_pack_tris(const float *__restrict__ v,
+__global__ void __launch_bounds__(kThreads) k_pack_tris(const TreeHeader *__restrict__ hdr,
+                                                        const float *__restrict__ v,
                                                         const uint32_t *__restrict__ tri_idx, uint32_t n,
                                                         float *__restrict__ out) {
-    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const float *p = v + 9ull * tri_idx[i];
-    float *o = out + 9ull * i;
-    float v0x = p[0], v0y = p[1], v0z = p[2];
-    o[0] = v0x; o[1] = v0y; o[2] = v0z;
-    o[3] = p[3] - v0x; o[4] = p[4] - v0y; o[5] = p[5] - v0z;   // v0v1, CUDAKernels.cu:18
-    o[6] = p[6] - v0x; o[7] = p[7] - v0y; o[8] = p[8] - v0z;   // v0v2, :19
+    if (hdr->n_unique >= 2) return;   // k_seg_leaf packed every leaf run
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        float lo[3], hi[3];
+        pack_tri(v + 9ull * tri_idx[i], out + 9ull * i, lo, hi);
+    }
 }
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kThreads - 1) / kThreads); }
@@ -784,7 +804,12 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
         BIH_TRY(dalloc(&t.hist, hist_n, b));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, b));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 6ull * kPrepBlocks, b));
+        BIH_TRY(dalloc(&t.prep_part, 7ull * kPrepBlocks, b));
+        // look-back words (k_scan_onepass) start at tag 0 (never a call's
+        // tag): stale data in fresh memory must not pass for a predecessor's
+        // published prefix; afterwards every word carries an older call's
+        // (unique) tag
+        BIH_TRY(hipMemsetAsync(t.partials, 0, (2 * (uint64_t)max_parts + 2) * sizeof(uint32_t), st));
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     BIH_TRY(hipEventCreate(&e0));
@@ -824,8 +849,9 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr,
                            t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
         const uint64_t cap = seg_capacity(nn);
-        hipLaunchKernelGGL(k_seg_leaf, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.tri_lo,
-                           t.tri_hi, t.first_idx, t.dup_cnt, t.fit_seg, cap);
+        // (also the sorted triangle records when U >= 2: every leaf run)
+        hipLaunchKernelGGL(k_seg_leaf, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.v,
+                           t.tris_s, t.first_idx, t.dup_cnt, t.fit_seg, cap);
         uint64_t lsize = nn;   // capacity of level L0 (>= its valid entries)
         for (int L0 = 0; lsize > 1; L0 += kSegSteps) {
             hipLaunchKernelGGL(k_seg_up, dim3((uint32_t)((lsize + kSegBlock - 1) / kSegBlock)), dim3(kThreads), 0,
@@ -836,12 +862,10 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.axis, t.fit_seg, cap, nn, t.clip);
         hipLaunchKernelGGL(k_pack_nodes, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.clip,
                            t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
-        hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.v, t.vals, n,
-                           t.tris_s);
-        const uint32_t words = 9u * n;     // n <= BIH_MAX_TRIS = 2^27
-        const uint32_t hb = (words + kThreads - 1) / kThreads;
-        hipLaunchKernelGGL(k_content_hash, dim3(hb < 512u ? hb : 512u), dim3(kThreads), 0, st,
-                           reinterpret_cast<const uint32_t *>(t.v), words, t.hdr);
+        // one leaf (U < 2: k_seg_leaf did not run): the records here; a
+        // no-op otherwise (U is on the device only until the build ends)
+        hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n) < 1024u ? blocks_for(n) : 1024u), dim3(kThreads), 0, st,
+                           t.hdr, t.v, t.vals, n, t.tris_s);
         BIH_TRY(hipGetLastError());
     }
     BIH_TRY(hipEventRecord(e1, st));

@@ -32,6 +32,55 @@
 #endif
 constexpr int kSlots = BIH_RENDER_SLOTS;
 constexpr int kRngBufs = kSlots + 1;
+constexpr size_t kEntryBytes = 16 * bih::kBinEntryF4;   // frustum-bin list entry
+
+// Per-camera structures (bih_render.hip / bih_bins.hip): primary-ray records,
+// frustum bins and the tile queue of one camera.  A tree keeps kCamSets of
+// them: a camera change builds into a set the latest render does not read,
+// after only the renders that read that set -- so camera k+1's structures
+// build while frame k renders (a moving camera, bench `moving_camera`).
+#ifndef BIH_CAM_SETS
+#define BIH_CAM_SETS 2
+#endif
+constexpr int kCamSets = BIH_CAM_SETS;
+struct CamSet {
+    float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
+    size_t prim_cap = 0;             // bytes
+    bool prim_valid = false;
+    bool fast_valid = false;         // the BIH walk's shortcut boxes match the records
+    bool cull_valid = false;         // node_cull matches the records (launch_prim_cull)
+    uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
+    // frustum bins (bih_bins.hip) of the camera the records were built for,
+    // for one image size and tile shape (bins_key = {w, h, spp})
+    char *bins_mem = nullptr;        // brect, cnt, off, gcount, glist, partials, binrec, path, gent
+    size_t bins_mem_cap = 0;         // bytes
+    float *bin_list = nullptr;       // 48-byte entries (bih::kBinEntryF4 float4)
+    size_t bin_list_cap = 0;         // entries
+    bih::BinBuffers bins;
+    bool bins_valid = false;         // built for prim_origin and bins_key
+    bool bins_usable = false;        // built and within the limits (else the kernel skips them)
+    uint32_t bins_key[3] = {0, 0, 0};
+    float *bin_gent = nullptr;       // global list entries (in bins_mem)
+    uint32_t bin_gn = 0;             // global list length (host copy once resolved)
+    // bins built without a host round trip (build_bins): the device status
+    // word decides the render; the host learns the totals from bins_host once
+    // ev_bins has passed (resolve_bins) and regrows the list if it overflowed
+    bool bins_pending = false;
+    bool bins_regrow = false;        // the last lists overflowed: rebuild with a sized list
+    bool bins_redo = false;          // the current lists are unusable but still read by renders
+    uint32_t *bins_host = nullptr;   // pinned: {gcount, status, total}
+    uint64_t bin_entries = 0;        // list entries over all tiles
+    uint32_t gen = 0;                // bih_tree::bins_gen of this set's last bins build
+    size_t bins_layout = 0;          // tiles of the bins_mem layout whose scan words are zeroed
+    // the render kernel's tile queue over one launch's rows (launch_bin_queue),
+    // for q_key = {w, h, spp, row0, nrows, band_h, band_step, gen}
+    char *q_mem = nullptr;
+    size_t q_cap = 0;
+    bool q_valid = false;
+    uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t *q_list = nullptr, *q_hdr = nullptr;
+    hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
+};
 
 struct bih_tree {
     bih::DeviceTree t;
@@ -52,7 +101,6 @@ struct bih_tree {
     // waits on it, so a render on another stream never reads half-written
     // records.
     hipEvent_t ev_rng = nullptr;
-    hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
     bool rng_pending = false;
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
@@ -76,40 +124,12 @@ struct bih_tree {
     uint32_t *chunk_buf = nullptr;
     size_t chunk_cap = 0;
     uint32_t chunk_key[kSlots][6] = {};
-    float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
-    size_t prim_cap = 0;             // bytes
-    bool prim_valid = false;
-    bool fast_valid = false;         // the BIH walk's shortcut boxes match the records
-    bool cull_valid = false;         // node_cull matches the records (launch_prim_cull)
-    uint32_t prim_origin[12] = {0};        // bit patterns of the camera they were built for
-    // frustum bins (bih_bins.hip) of the camera the records were built for,
-    // for one image size and tile shape (bins_key = {w, h, spp})
-    char *bins_mem = nullptr;        // brect, cnt, off, gcount, glist, partials, binrec, path, gent
-    size_t bins_mem_cap = 0;         // bytes
-    float *bin_list = nullptr;       // 64-byte entries
-    size_t bin_list_cap = 0;         // entries
-    bih::BinBuffers bins;
-    bool bins_valid = false;         // built for prim_origin and bins_key
-    bool bins_usable = false;        // built and within the limits (else the kernel skips them)
-    uint32_t bins_key[3] = {0, 0, 0};
-    float *bin_gent = nullptr;       // global list entries (in bins_mem)
-    uint32_t bin_gn = 0;             // global list length (host copy once resolved)
-    // bins built without a host round trip (build_bins): the device status
-    // word decides the render; the host learns the totals from bins_host once
-    // ev_bins has passed (resolve_bins) and regrows the list if it overflowed
-    bool bins_pending = false;
-    bool bins_regrow = false;        // the last lists overflowed: rebuild with a sized list
-    bool bins_redo = false;          // the current lists are unusable but still read by renders
-    uint32_t *bins_host = nullptr;   // pinned: {gcount, status, total}
-    uint32_t bins_gen = 0;           // incremented by every bins build
-    uint64_t bin_entries = 0;        // list entries over all tiles
-    // the render kernel's tile queue over one launch's rows (launch_bin_queue),
-    // for q_key = {w, h, spp, row0, nrows, band_h, band_step, bins_gen}
-    char *q_mem = nullptr;
-    size_t q_cap = 0;
-    bool q_valid = false;
-    uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t *q_list = nullptr, *q_hdr = nullptr;
+    // per-camera structures: kCamSets sets, so that the structures of a new
+    // camera are built while renders of the previous one still read theirs
+    CamSet cs[kCamSets];
+    int cs_cur = 0;                  // set of the latest render's camera
+    int slot_cs[kSlots] = {};        // set the slot's last render read
+    uint32_t bins_gen = 0;           // incremented by every bins build (any set)
     // per render slot two sets of 8 band heads (32 words apart): a launch
     // draws from set q_par[slot] and zeroes the other for the slot's next launch
     uint32_t *q_count = nullptr;
@@ -153,6 +173,16 @@ int check_device(int device) {
 int wait_renders(bih_tree *tr, hipStream_t st) {
     for (int k = 0; k < kSlots; ++k)
         if (tr->used[k]) {
+            hipError_t e = hipStreamWaitEvent(st, tr->evd[k], 0);
+            if (e != hipSuccess) return map_hip((int)e);
+        }
+    return BIH_OK;
+}
+
+// Orders `st` after every render in flight that read camera set `c`.
+int wait_set_readers(bih_tree *tr, int c, hipStream_t st) {
+    for (int k = 0; k < kSlots; ++k)
+        if (tr->used[k] && tr->slot_cs[k] == c) {
             hipError_t e = hipStreamWaitEvent(st, tr->evd[k], 0);
             if (e != hipSuccess) return map_hip((int)e);
         }
@@ -240,10 +270,11 @@ int finish_build(bih_tree *tr) {
     // the soup: a rebuild of an unchanged soup (same content hash, N and U;
     // the tree is bit-identical) keeps them
     const bool same = had && e == 0 && tr->t.content == old_content && tr->t.n == old_n && tr->t.u == old_u;
-    if (!same) {
-        tr->prim_valid = false;  // triangle records follow the (re)sorted triangles
-        tr->bins_valid = false;
-    }
+    if (!same)
+        for (CamSet &c : tr->cs) {
+            c.prim_valid = false;  // triangle records follow the (re)sorted triangles
+            c.bins_valid = false;
+        }
     if (e) return map_hip(e);
     // renders issued on other streams order after the (re)build; tr->stream
     // waited for every render above, so this also follows the last advance
@@ -271,8 +302,10 @@ int create_tree(int device, void *stream, bih_tree **out) {
         if (e == hipSuccess) e = hipEventCreate(&tr->ev2[k]);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_bins, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&tr->bins_host, 4 * sizeof(uint32_t), hipHostMallocDefault);
+    for (CamSet &c : tr->cs) {
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c.ev_bins, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&c.bins_host, 4 * sizeof(uint32_t), hipHostMallocDefault);
+    }
     if (e == hipSuccess && bih::upload_rng_tables(device) != 0) e = hipErrorUnknown;
     if (e != hipSuccess) {
         delete tr;
@@ -412,17 +445,22 @@ void bih_free(bih_tree *tr) {
     for (int k = 0; k < kSlots; ++k)
         if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
     // a bins readback into bins_host may still be in flight (a failed render)
-    if (tr->bins_pending) (void)hipEventSynchronize(tr->ev_bins);
+    for (CamSet &c : tr->cs)
+        if (c.bins_pending) (void)hipEventSynchronize(c.ev_bins);
     bih::free_tree_device(tr->t);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
     if (tr->spill) (void)hipFree(tr->spill);
     if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
-    if (tr->prim) (void)hipFree(tr->prim);
-    if (tr->bins_mem) (void)hipFree(tr->bins_mem);
-    if (tr->bin_list) (void)hipFree(tr->bin_list);
-    if (tr->q_mem) (void)hipFree(tr->q_mem);
+    for (CamSet &c : tr->cs) {
+        if (c.prim) (void)hipFree(c.prim);
+        if (c.bins_mem) (void)hipFree(c.bins_mem);
+        if (c.bin_list) (void)hipFree(c.bin_list);
+        if (c.q_mem) (void)hipFree(c.q_mem);
+        if (c.ev_bins) (void)hipEventDestroy(c.ev_bins);
+        if (c.bins_host) (void)hipHostFree(c.bins_host);
+    }
     if (tr->q_count) (void)hipFree(tr->q_count);
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
     if (tr->wh_mem) (void)hipFree(tr->wh_mem);
@@ -433,8 +471,6 @@ void bih_free(bih_tree *tr) {
         if (tr->ev2[k]) (void)hipEventDestroy(tr->ev2[k]);
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
-    if (tr->ev_bins) (void)hipEventDestroy(tr->ev_bins);
-    if (tr->bins_host) (void)hipHostFree(tr->bins_host);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
     delete tr;
 }
@@ -459,8 +495,9 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // tree + canonical arrays, the XORWOW ring (kRngBufs x 5 planes) and the
     // per-slot accumulators, the host-path framebuffer, the per-camera
     // records, and the per-slot tile queues, spill areas and chunk orders
-    info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 +
-                         tr->prim_cap + tr->bins_mem_cap + tr->bin_list_cap * 64 + tr->q_cap +
+    size_t cam = 0;
+    for (const CamSet &c : tr->cs) cam += c.prim_cap + c.bins_mem_cap + c.bin_list_cap * kEntryBytes + c.q_cap;
+    info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
@@ -585,11 +622,11 @@ static void tile_shape(uint32_t spp, uint32_t *tw, uint32_t *th) {
 // (the caller waited for them).  Synchronises `st` once to size the lists.
 // Runs the camera's primary-ray records (launch_prim) when `need_prim` and
 // the bins take no part.
-static int prim_only(bih_tree *tr, const bih_camera *cam, const float dmax[3], bool need_prim, hipStream_t st) {
+static int prim_only(bih_tree *tr, CamSet &c, const bih_camera *cam, const float dmax[3], bool need_prim, hipStream_t st) {
     if (!need_prim) return BIH_OK;
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
     return map_hip(bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx, tr->t.dup_cnt,
-                                    tr->t.leaf_parent, tr->t.parent, n_int, cam->origin, dmax, tr->prim, st));
+                                    tr->t.leaf_parent, tr->t.parent, n_int, cam->origin, dmax, c.prim, st));
 }
 
 // (Re)builds the frustum bins for `cam` and a w x h image on `st`; with
@@ -597,21 +634,21 @@ static int prim_only(bih_tree *tr, const bih_camera *cam, const float dmax[3], b
 // launch_prim when no bins are built).  Every render that read the old ones
 // has finished (the caller waited for them).  Synchronises `st` once to size
 // the lists the first time.
-static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], uint32_t w,
+static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const float dmax[3], uint32_t w,
                       uint32_t h, uint32_t spp, bool need_prim, hipStream_t st) {
-    tr->bins_valid = true;
-    tr->bins_usable = false;
-    ++tr->bins_gen;
-    tr->bins_key[0] = w;
-    tr->bins_key[1] = h;
-    tr->bins_key[2] = spp;
+    c.bins_valid = true;
+    c.bins_usable = false;
+    c.gen = ++tr->bins_gen;
+    c.bins_key[0] = w;
+    c.bins_key[1] = h;
+    c.bins_key[2] = spp;
     const uint32_t n = tr->t.n, U = tr->t.u;
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     bih::BinCamera bc;
     if (n == 0 || U < 2 || w > 0xffffu || h > 0xffffu ||
         !bih::bin_camera(reinterpret_cast<const float *>(cam), dmax, w, h, tw, th, &bc))
-        return prim_only(tr, cam, dmax, need_prim, st);   // no bins: the kernel runs the shortcut passes instead
+        return prim_only(tr, c, cam, dmax, need_prim, st);   // no bins: the kernel runs the shortcut passes instead
     bih::BinBuffers b;
     b.bins_x = (w + tw - 1) / tw;
     b.bins_y = (h + th - 1) / th;
@@ -625,23 +662,24 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
                  s_g = al(6 * 4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
-                 s_gent = al((size_t)4097 * 64), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
+                 s_gent = al((size_t)4097 * kEntryBytes), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
                  s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
                  s_bpart = al(bih::scan_partials_words(nblk) * 4),
                  s_blkcnt = al((size_t)nblk * bih::kBinBlockTiles * 8);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
                         s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt;
-    if (tr->bins_mem_cap < need) {
+    if (c.bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
-        if (tr->bins_mem) (void)hipFree(tr->bins_mem);
-        tr->bins_mem = nullptr;
-        tr->bins_mem_cap = 0;
-        e = hipMalloc((void **)&tr->bins_mem, need);
+        if (c.bins_mem) (void)hipFree(c.bins_mem);
+        c.bins_mem = nullptr;
+        c.bins_mem_cap = 0;
+        e = hipMalloc((void **)&c.bins_mem, need);
         if (e != hipSuccess) return map_hip((int)e);
-        tr->bins_mem_cap = need;
+        c.bins_mem_cap = need;
+        c.bins_layout = 0;
     }
-    char *p = tr->bins_mem;
+    char *p = c.bins_mem;
     b.brect = reinterpret_cast<uint2 *>(p); p += s_brect;
     b.cnt = reinterpret_cast<uint32_t *>(p); p += s_cnt;
     b.cntq = reinterpret_cast<uint32_t *>(p); p += s_cntq;
@@ -659,9 +697,18 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     b.boff = reinterpret_cast<uint32_t *>(p); p += s_boff;
     b.bpart = reinterpret_cast<uint32_t *>(p); p += s_bpart;
     b.blkcnt = reinterpret_cast<uint32_t *>(p);
+    // the scans' look-back words (partials, bpart) must start at tag 0 (never
+    // a call's tag) wherever this layout puts them: stale data there must not
+    // pass for a published prefix.  Later calls leave older, unique tags.
+    if (c.bins_layout != nb) {
+        hipError_t e = hipMemsetAsync(b.partials, 0, s_part, st);
+        if (e == hipSuccess) e = hipMemsetAsync(b.bpart, 0, s_bpart, st);
+        if (e != hipSuccess) return map_hip((int)e);
+        c.bins_layout = nb;
+    }
     // the triangle records are rewritten in any case (k_cam_tris computes the
     // alive list from them); the node records too
-    int le = bih::launch_bin_footprints(tr->t.tris_s, n, tr->t.nodes, U - 1, cam->origin, tr->prim, tr->t.hdr,
+    int le = bih::launch_bin_footprints(tr->t.tris_s, n, tr->t.nodes, U - 1, cam->origin, c.prim, tr->t.hdr,
                                         tr->t.scan_tmp, tr->t.leaf_parent, tr->t.parent, bc, b, st);
     if (le) return map_hip(le);
     hipError_t e = hipSuccess;
@@ -676,22 +723,22 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
     }();
     size_t cap_test = 0;
     if (const char *v = getenv("BIH_BINS_CAP")) cap_test = (size_t)strtoull(v, nullptr, 10);
-    const bool speculative = tr->bin_list_cap > 0 && !always_sync && !tr->bins_regrow;
+    const bool speculative = c.bin_list_cap > 0 && !always_sync && !c.bins_regrow;
     if (speculative) {
-        const size_t cap = cap_test ? std::min(cap_test, tr->bin_list_cap) : tr->bin_list_cap;
+        const size_t cap = cap_test ? std::min(cap_test, c.bin_list_cap) : c.bin_list_cap;
         le = bih::launch_bin_status(b, cap, st);
         if (le) return map_hip(le);
-        e = hipMemcpyAsync(tr->bins_host, b.gcount, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipEventRecord(tr->ev_bins, st);
+        e = hipMemcpyAsync(c.bins_host, b.gcount, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(c.ev_bins, st);
         if (e != hipSuccess) return map_hip((int)e);
-        tr->bins_pending = true;
+        c.bins_pending = true;
     } else {
-        tr->bins_pending = false;
+        c.bins_pending = false;
         uint32_t g[6] = {0, 0, 0, 0, 0, 0};   // gcount words; [4..5] = 64-bit list total
         e = hipMemcpyAsync(g, b.gcount, sizeof g, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return map_hip((int)e);
-        tr->bins_regrow = false;
+        c.bins_regrow = false;
         const uint64_t total = (uint64_t)g[4] | ((uint64_t)g[5] << 32);
         // every packet tests the whole global list: beyond a few thousand
         // triangles the shortcut passes are the better proof
@@ -701,30 +748,30 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
         size_t mem_free = 0, mem_total = 0;
         if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 0;
         const uint64_t cap = total + total / 8 + 1024;
-        if (cap > 0xFFFFFFFFull || cap * 64 > (uint64_t)mem_free / 2 + (uint64_t)tr->bin_list_cap * 64)
+        if (cap > 0xFFFFFFFFull || cap * kEntryBytes > (uint64_t)mem_free / 2 + (uint64_t)c.bin_list_cap * kEntryBytes)
             return BIH_OK;
-        if (tr->bin_list_cap < total + 1) {
-            if (tr->bin_list) (void)hipFree(tr->bin_list);   // st waited for every render
-            tr->bin_list = nullptr;
-            tr->bin_list_cap = 0;
-            e = hipMalloc((void **)&tr->bin_list, cap * 64);
+        if (c.bin_list_cap < total + 1) {
+            if (c.bin_list) (void)hipFree(c.bin_list);   // st waited for every render
+            c.bin_list = nullptr;
+            c.bin_list_cap = 0;
+            e = hipMalloc((void **)&c.bin_list, cap * kEntryBytes);
             if (e != hipSuccess) {
                 (void)hipGetLastError();   // not sticky: this camera renders without bins
-                tr->bin_list = nullptr;
+                c.bin_list = nullptr;
                 return BIH_OK;
             }
-            tr->bin_list_cap = cap;
+            c.bin_list_cap = cap;
         }
-        le = bih::launch_bin_status(b, tr->bin_list_cap, st);
+        le = bih::launch_bin_status(b, c.bin_list_cap, st);
         if (le) return map_hip(le);
-        tr->bin_gn = g[0];
-        tr->bin_entries = total;
+        c.bin_gn = g[0];
+        c.bin_entries = total;
     }
-    le = bih::launch_bin_fill(n, bc, b, tr->bin_list, gent, st);
+    le = bih::launch_bin_fill(n, bc, b, c.bin_list, gent, st);
     if (le) return map_hip(le);
-    tr->bins = b;
-    tr->bin_gent = gent;
-    tr->bins_usable = true;
+    c.bins = b;
+    c.bin_gent = gent;
+    c.bins_usable = true;
     return BIH_OK;
 }
 
@@ -734,62 +781,62 @@ static int build_bins(bih_tree *tr, const bih_camera *cam, const float dmax[3], 
 // past the buffer make the next render rebuild them with a sized buffer.
 // Until then the device status word already kept every render exact (the
 // lists were not written; every live packet took the exact walk).
-static void resolve_bins(bih_tree *tr, bool block) {
-    if (!tr->bins_pending) return;
-    const hipError_t e = block ? hipEventSynchronize(tr->ev_bins) : hipEventQuery(tr->ev_bins);
+static void resolve_bins(CamSet &c, bool block) {
+    if (!c.bins_pending) return;
+    const hipError_t e = block ? hipEventSynchronize(c.ev_bins) : hipEventQuery(c.ev_bins);
     if (e != hipSuccess) return;   // hipErrorNotReady: later
-    tr->bins_pending = false;
-    const uint32_t gc = tr->bins_host[0], st = tr->bins_host[1], tot = tr->bins_host[2];
-    tr->bin_gn = gc;
-    tr->bin_entries = tot;
+    c.bins_pending = false;
+    const uint32_t gc = c.bins_host[0], st = c.bins_host[1], tot = c.bins_host[2];
+    c.bin_gn = gc;
+    c.bin_entries = tot;
     if (st != bih::kBinsUnusable) return;
     if (gc > bih::kBinGlobalMax) {
-        tr->bins_usable = false;
+        c.bins_usable = false;
     } else {
-        tr->bins_regrow = true;
-        tr->bins_valid = false;   // rebuilt by the next render (after its readers)
-        tr->bins_redo = true;
+        c.bins_regrow = true;
+        c.bins_valid = false;   // rebuilt by the next render (after its readers)
+        c.bins_redo = true;
     }
 }
 
 // The render kernel's tile queue for this launch's rows (launch_bin_queue):
 // rebuilt when the bins or the rows change, after every render that may
 // still read the old one.
-static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_rows &rows,
+static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32_t h, uint32_t spp, const bih_rows &rows,
                              int slot, hipStream_t st, bih::RenderArgs &a, uint32_t nframes) {
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     const uint32_t tiles_x = (w + tw - 1) / tw;
     const uint32_t ntiles = tiles_x * ((rows.nrows + th - 1) / th);
     const size_t nrec = (size_t)ntiles * nframes;   // fallback records: one per packet at most
-    const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, tr->bins_gen};
+    const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, c.gen};
     if (!tr->q_count) {
         hipError_t e = hipMalloc((void **)&tr->q_count, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
         if (e == hipSuccess)
             e = hipMemset(tr->q_count, 0, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip((int)e);
     }
-    if (!tr->q_valid || memcmp(key, tr->q_key, sizeof key) != 0) {
-        int rc = wait_renders(tr, st);
+    if (!c.q_valid || memcmp(key, c.q_key, sizeof key) != 0) {
+        int rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
         const size_t need = bih::bin_queue_bytes(ntiles);
-        if (tr->q_cap < need) {
+        if (c.q_cap < need) {
             for (int k = 0; k < kSlots; ++k)
                 if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
-            if (tr->q_mem) (void)hipFree(tr->q_mem);
-            tr->q_mem = nullptr;
-            tr->q_cap = 0;
-            tr->q_valid = false;
-            hipError_t e = hipMalloc((void **)&tr->q_mem, need);
+            if (c.q_mem) (void)hipFree(c.q_mem);
+            c.q_mem = nullptr;
+            c.q_cap = 0;
+            c.q_valid = false;
+            hipError_t e = hipMalloc((void **)&c.q_mem, need);
             if (e != hipSuccess) return map_hip((int)e);
-            tr->q_cap = need;
+            c.q_cap = need;
         }
-        int le = bih::launch_bin_queue(tr->bins.off, tr->bins.gcount + 1, tr->bins.bins_x, tiles_x, ntiles, rows.row0,
-                                       rows.band_h, rows.band_step, th, tr->q_mem, &tr->q_list, &tr->q_hdr,
+        int le = bih::launch_bin_queue(c.bins.off, c.bins.gcount + 1, c.bins.bins_x, tiles_x, ntiles, rows.row0,
+                                       rows.band_h, rows.band_step, th, c.q_mem, &c.q_list, &c.q_hdr,
                                        st);
         if (le) return map_hip(le);
-        memcpy(tr->q_key, key, sizeof key);
-        tr->q_valid = true;
+        memcpy(c.q_key, key, sizeof key);
+        c.q_valid = true;
     }
     if (tr->fbq_cap < nrec) {
         for (int k = 0; k < kSlots; ++k)
@@ -802,8 +849,8 @@ static int prepare_bin_queue(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp,
         tr->fbq_cap = nrec;
     }
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
-    a.bin_queue = tr->q_list;
-    a.bin_qhdr = tr->q_hdr;
+    a.bin_queue = c.q_list;
+    a.bin_qhdr = c.q_hdr;
     // timing experiments (BIH_DBG bits: skip phases or checks; they change
     // pixels, so only a BIH_DEBUG_KNOBS=1 build reads them) and the fallback
     // test mode (routes packets to the exact walk: same pixels)
@@ -841,7 +888,22 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
-    resolve_bins(tr, false);
+    // the camera's set of per-camera structures: the one built for this
+    // camera, else the next one after the latest render's (with two sets:
+    // not the one the renders in flight read)
+    uint32_t ob[12];
+    static_assert(sizeof(bih_camera) == sizeof ob, "bih_camera is 12 f32");
+    memcpy(ob, cam, sizeof ob);
+    int ci = (tr->cs_cur + 1) % kCamSets;
+    for (int k = 0; k < kCamSets; ++k) {
+        const int j = (tr->cs_cur + k) % kCamSets;
+        if (tr->cs[j].prim_valid && memcmp(ob, tr->cs[j].prim_origin, sizeof ob) == 0) {
+            ci = j;
+            break;
+        }
+    }
+    CamSet &c = tr->cs[ci];
+    resolve_bins(c, false);
     if (!tr->work) {
         tr->spill_per_slot = bih::spill_words(bih::wave_grid_blocks(tr->t.device));
         hipError_t e = hipMalloc((void **)&tr->work, kSlots * bih::kWorkWords * sizeof(uint32_t));
@@ -871,31 +933,28 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // also the direction bounds)
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
     if (bih::render_uses_prim(spp) && tr->t.n > 0) {
-        uint32_t ob[12];
-        static_assert(sizeof(bih_camera) == sizeof ob, "bih_camera is 12 f32");
-        memcpy(ob, cam, sizeof ob);
         const size_t need = bih::prim_bytes(tr->t.n, n_int);
-        const bool grow = tr->prim_cap < need;
-        if (grow || !tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
+        const bool grow = c.prim_cap < need;
+        if (grow || !c.prim_valid || memcmp(ob, c.prim_origin, sizeof ob) != 0) {
             // rewritten in place: after every render still reading the records
-            rc = wait_renders(tr, st);
+            rc = wait_set_readers(tr, ci, st);
             if (rc) return rc;
         }
         if (grow) {
             for (int k = 0; k < kSlots; ++k)
                 if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
-            if (tr->prim) (void)hipFree(tr->prim);
-            tr->prim = nullptr;
-            tr->prim_cap = 0;
-            e = hipMalloc((void **)&tr->prim, need);
+            if (c.prim) (void)hipFree(c.prim);
+            c.prim = nullptr;
+            c.prim_cap = 0;
+            e = hipMalloc((void **)&c.prim, need);
             if (e != hipSuccess) return map_hip((int)e);
-            tr->prim_cap = need;
-            tr->prim_valid = false;
+            c.prim_cap = need;
+            c.prim_valid = false;
         }
         // the frustum bins' build computes the records itself (k_cam_tris)
         const bool want_bins = bins_enabled() && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && n_int > 0;
         bool need_prim = false;
-        if (!tr->prim_valid || memcmp(ob, tr->prim_origin, sizeof ob) != 0) {
+        if (!c.prim_valid || memcmp(ob, c.prim_origin, sizeof ob) != 0) {
             // |D| per component over the primary rays: D = (llc + u h + v vert) - O
             // (Camera.cu:18-20) is affine in (u, v) in [0, 1]^2, so its largest
             // magnitude is at a corner.  The kernel evaluates it in f32: four
@@ -910,36 +969,36 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             } else {
                 int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
                                           tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
-                                          cam->origin, dmax, tr->prim, st);
+                                          cam->origin, dmax, c.prim, st);
                 if (le) return map_hip(le);
             }
-            memcpy(tr->prim_origin, ob, sizeof ob);
-            tr->prim_valid = true;
-            tr->bins_valid = false;
-            tr->fast_valid = false;
-            tr->cull_valid = false;
+            memcpy(c.prim_origin, ob, sizeof ob);
+            c.prim_valid = true;
+            c.bins_valid = false;
+            c.fast_valid = false;
+            c.cull_valid = false;
         }
-        const bool bins_key_ok = tr->bins_key[0] == w && tr->bins_key[1] == h && tr->bins_key[2] == spp;
-        if (want_bins && (!tr->bins_valid || !bins_key_ok)) {
+        const bool bins_key_ok = c.bins_key[0] == w && c.bins_key[1] == h && c.bins_key[2] == spp;
+        if (want_bins && (!c.bins_valid || !bins_key_ok)) {
             // rewritten in place (the triangle and node records too): after
             // every render still reading them (a no-op wait when need_prim
             // already waited above)
-            rc = wait_renders(tr, st);
+            rc = wait_set_readers(tr, ci, st);
             if (rc) return rc;
             float dmax[3];
             (void)bih_camera_ray_bound(cam, dmax);
-            rc = build_bins(tr, cam, dmax, w, h, spp, need_prim, st);
+            rc = build_bins(tr, c, cam, dmax, w, h, spp, need_prim, st);
             if (rc) {
-                if (need_prim) tr->prim_valid = false;
+                if (need_prim) c.prim_valid = false;
                 return rc;
             }
-            tr->bins_redo = false;
+            c.bins_redo = false;
         }
     }
     bih::RenderArgs a;
     bool use_bins = false;
-    if (tr->bins_usable && tr->bins_valid && tr->bins_key[0] == w && tr->bins_key[1] == h &&
-        tr->bins_key[2] == spp && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && tr->prim) {
+    if (c.bins_usable && c.bins_valid && c.bins_key[0] == w && c.bins_key[1] == h &&
+        c.bins_key[2] == spp && traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats && c.prim) {
         uint32_t tw = 0, th = 0;
         tile_shape(spp, &tw, &th);
         // a packet's rows are one bin row when tiles and bands align
@@ -958,14 +1017,35 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     tr->next_frame = frame + nframes;
     a.nframes = nframes;
     a.out_stride = out_stride;
+    if (use_bins && nframes > 1) {
+        // frames per k_render_bins item: every frame of the launch when the
+        // launch has many tiles (the list is walked nframes times while it is
+        // cached), fewer when it has few (a rank's bands of the frame), so the
+        // items keep outnumbering the resident waves (BIH_ITEM_TILES: the tile
+        // count below which an item's frames are split; A/B and tests: it
+        // changes the order of the work, never a pixel)
+        uint32_t item_tiles = 65536u;
+        if (const char *v = getenv("BIH_ITEM_TILES")) item_tiles = (uint32_t)strtoul(v, nullptr, 10);
+        uint32_t tw = 0, th = 0;
+        tile_shape(spp, &tw, &th);
+        const uint64_t ntiles = (uint64_t)((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
+        uint64_t ns = ntiles ? (item_tiles + ntiles / 2) / ntiles : nframes;
+        ns = std::max<uint64_t>(1, std::min<uint64_t>(ns, nframes));
+        a.fpi = (uint32_t)((nframes + ns - 1) / ns);
+        a.nsplit = (nframes + a.fpi - 1) / a.fpi;
+    } else {
+        a.fpi = nframes;
+        a.nsplit = 1;
+    }
     if (use_bins) {
-        a.bin_off = tr->bins.off;
-        a.bin_list = tr->bin_list;
-        a.bin_glist = tr->bin_gent;
-        a.bin_path = tr->bins.path;
-        a.bins_x = tr->bins.bins_x;
-        a.bin_gstat = tr->bins.gcount + 1;
-        rc = prepare_bin_queue(tr, w, h, spp, rows, slot, st, a, nframes);
+        a.bin_off = c.bins.off;
+        a.bin_list = c.bin_list;
+        a.bin_glist = c.bin_gent;
+        a.bin_rec = c.bins.binrec;
+        a.bin_path = c.bins.path;
+        a.bins_x = c.bins.bins_x;
+        a.bin_gstat = c.bins.gcount + 1;
+        rc = prepare_bin_queue(tr, c, ci, w, h, spp, rows, slot, st, a, nframes);
         if (rc) return rc;
     } else {
         // the cost order pays off for the long BIH walks; with the bins the
@@ -975,28 +1055,28 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     }
     // the BIH walk kernels read the culled node records: built on first use
     // for this camera (renders through the bins never need them)
-    if (!use_bins && bih::render_uses_prim(spp) && tr->prim && n_int > 0 && !tr->cull_valid) {
-        rc = wait_renders(tr, st);
+    if (!use_bins && bih::render_uses_prim(spp) && c.prim && n_int > 0 && !c.cull_valid) {
+        rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
         const int le = bih::launch_prim_cull(tr->t.n, tr->t.nodes, tr->t.first_idx, tr->t.dup_cnt, n_int,
-                                             cam->origin, tr->prim, st);
+                                             cam->origin, c.prim, st);
         if (le) return map_hip(le);
-        tr->cull_valid = true;
+        c.cull_valid = true;
     }
     // the BIH walk's shortcut boxes (any-hit without bins), built on first
     // use for this camera
-    const bool use_fast = tr->prim && n_int > 0 && fast_enabled() > 0 && !use_bins &&
+    const bool use_fast = c.prim && n_int > 0 && fast_enabled() > 0 && !use_bins &&
                           traverse == BIH_TRAVERSE_ANYHIT && !d_ray_stats;
-    if (use_fast && !tr->fast_valid) {
-        rc = wait_renders(tr, st);
+    if (use_fast && !c.fast_valid) {
+        rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
         float dmax[3];
         (void)bih_camera_ray_bound(cam, dmax);
         const int le = bih::launch_fast_boxes(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
                                               tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
-                                              cam->origin, dmax, tr->prim, st);
+                                              cam->origin, dmax, c.prim, st);
         if (le) return map_hip(le);
-        tr->fast_valid = true;
+        c.fast_valid = true;
     }
     // the next render (on any stream) orders after the advance above, the
     // per-camera records, the shortcut boxes and the tile queue, which it
@@ -1020,12 +1100,12 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     a.n_nodes = n_int;
     a.nodes = tr->t.nodes;
     a.tris = tr->t.tris_s;
-    a.tri_prim = tr->prim;
-    a.node_prim = tr->prim ? reinterpret_cast<const uint4 *>(tr->prim + 16ull * tr->t.n) : nullptr;
+    a.tri_prim = c.prim;
+    a.node_prim = c.prim ? reinterpret_cast<const uint4 *>(c.prim + 16ull * tr->t.n) : nullptr;
     a.node_cull = a.node_prim ? a.node_prim + (n_int + 1) : nullptr;
     a.dup_cnt = tr->t.dup_cnt;
     if (use_fast) {
-        a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(tr->prim) +
+        a.fast = reinterpret_cast<const float *>(reinterpret_cast<const char *>(c.prim) +
                                                  bih::fast_offset(tr->t.n, n_int));
         if (fast_enabled() > 1) a.fast2 = a.fast + 16ull * (n_int + 1);
     }
@@ -1047,6 +1127,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
+    tr->slot_cs[slot] = ci;
+    tr->cs_cur = ci;
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;                 // frame+1's state
@@ -1099,7 +1181,6 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
-    resolve_bins(tr, false);
     // the queues are shared by every Whitted render of this tree: order after
     // every render in flight (and after the last writer of the RNG ring)
     int rc = wait_renders(tr, st);
@@ -1160,6 +1241,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
+    tr->slot_cs[slot] = -1;            // reads no camera set
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;
@@ -1367,13 +1449,14 @@ int bih_bins_get_stats(const bih_tree *ctr, bih_bins_stats *out) {
     bih_tree *tr = const_cast<bih_tree *>(ctr);
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
-    resolve_bins(tr, true);
+    CamSet &c = tr->cs[tr->cs_cur];   // the latest render's camera
+    resolve_bins(c, true);
     memset(out, 0, sizeof *out);
-    out->usable = tr->bins_usable && tr->bins_valid ? 1u : 0u;
-    out->tiles_x = tr->bins.bins_x;
-    out->tiles_y = tr->bins.bins_y;
-    out->list_entries = tr->bin_entries;
-    out->global_entries = tr->bin_gn;
+    out->usable = c.bins_usable && c.bins_valid ? 1u : 0u;
+    out->tiles_x = c.bins.bins_x;
+    out->tiles_y = c.bins.bins_y;
+    out->list_entries = c.bin_entries;
+    out->global_entries = c.bin_gn;
     return BIH_OK;
 }
 

@@ -41,7 +41,8 @@ constexpr int kLdsStack = BIH_LDS_STACK;
 constexpr uint32_t kSlotStrideWords = 32;
 constexpr uint32_t kWorkWords = 64 + kSlotStrideWords * 1024 + 64;   // + histograms (counter builds)
 constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
-constexpr uint32_t kBinGlobalMax = 4096;          // longer global lists: no bins (the shortcut walk)
+constexpr uint32_t kBinGlobalMax = 4096;
+constexpr uint32_t kBinEntryF4 = 3;               // list entry: 3 x float4 = 48 bytes (bih_bins.hip)          // longer global lists: no bins (the shortcut walk)
 constexpr uint32_t kBinsUnusable = 0xFFFFFFFFu;   // bins status: lists not built (k_bin_status)
 constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue state per set
 #ifndef BIH_BUCKETS
@@ -66,7 +67,7 @@ struct TreeHeader {
     uint32_t pad0;
     unsigned long long lo_key[3];   // argmin keys (App.cpp:133-137 tie rules)
     unsigned long long hi_key[3];   // argmax keys
-    unsigned long long content;     // hash of the input soup (k_content_hash): the tree is a function of it
+    unsigned long long content;     // hash of the input soup (k_prep / k_prep_final): the tree is a function of it
 };
 
 // Render parameters, passed by value.
@@ -99,8 +100,9 @@ struct RenderArgs {
     // (bin_list[bin_off[b] .. bin_off[b+1])), and the global list
     // (bin_glist[0 .. *bin_gstat)); null: no bins (rows not tile-aligned)
     const uint32_t *bin_off = nullptr;
-    const float *bin_list = nullptr;        // 64-byte entries (bih_bins.hip)
+    const float *bin_list = nullptr;        // 48-byte entries (bih_bins.hip)
     const float *bin_glist = nullptr;       // global list entries
+    const float *bin_rec = nullptr;         // per triangle the 64-byte record (k_bin_fp): plan values at 12..15
     const uint2 *bin_path = nullptr;        // [U][32] root path steps per leaf
     uint32_t bins_x = 0;
     const uint32_t *bin_gstat = nullptr;    // bins status: global list length or kBinsUnusable
@@ -118,6 +120,12 @@ struct RenderArgs {
     // out + j * out_stride, its XORWOW draws 2*spp*j past rng_in's
     uint32_t nframes = 1;
     uint64_t out_stride = 0;
+    // k_render_bins: frames per queue item (an item covers its tile in
+    // frames [s*fpi, min((s+1)*fpi, nframes)) of the launch, s = 0 ..
+    // nsplit-1); few tiles per launch (a rank's bands) take fewer frames per
+    // item so that the items still outnumber the waves
+    uint32_t fpi = 1;
+    uint32_t nsplit = 1;
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
@@ -242,7 +250,7 @@ int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uin
                           float *prim, const TreeHeader *hdr, const uint32_t *tri_leaf,
                           const int32_t *leaf_parent, const int32_t *parent, const BinCamera &c,
                           const BinBuffers &b, void *stream);
-// lists of 64-byte entries (list: per-tile, gent: the global list's)
+// lists of 48-byte entries (list: per-tile, gent: the global list's)
 // the status word gcount[1] (k_bin_status: the global list length, or
 // kBinsUnusable when the lists exceed `cap` entries or the global list
 // kBinGlobalMax) and gcount[2] = the list total; the fill and the render read it

@@ -1503,7 +1503,7 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 
 // Frustum-bin walk (bih_bins.hip): the packet tests the triangles of its
 // tile's list and then of the global list with the exact intersector until
-// every lane of `live` has a hit.  Each 64-byte entry starts with the
+// every lane of `live` has a hit.  Each 48-byte entry starts with the
 // triangle's edge pre-test (three affine functions of the lane's f32 (u, v),
 // each >= 0 whenever MT can accept): a lane failing one skips the triangle,
 // and a triangle no remaining lane passes costs no MT.  A lane with a hit
@@ -1514,7 +1514,7 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #define BIH_BINS 1
 #endif
 // The list is streamed in chunks of 64 entries: lane j loads entry e + j
-// (its first 48 bytes, coalesced vector loads), the next chunk is requested
+// (48 bytes, coalesced vector loads), the next chunk is requested
 // before the current one is consumed, and each entry reaches the scalar unit
 // by v_readlane -- one memory round trip per 64 entries instead of one per
 // entry.
@@ -1540,7 +1540,7 @@ __device__ __forceinline__ void bin_chunk_load(const float4 *ents, uint32_t e, u
                                                uint32_t lane, float4 &c0, float4 &c1, float4 &c2) {
     const uint32_t k = e + lane;
     if (k < end) {
-        const float4 *p = ents + 4ull * k;
+        const float4 *p = ents + (uint64_t)kBinEntryF4 * k;
         c0 = p[0];
         c1 = p[1];
         c2 = p[2];
@@ -1616,7 +1616,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 if (h & me) {
                     cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
                     cmeta = __builtin_amdgcn_readlane(__float_as_uint(d2.w), j);
-                    cent = ((uint32_t)part << 31) | (e + j);
+                    cent = ti;
                 }
                 rem &= ~h;
                 if (PMASK && h) rpix = pixels_of(rem);
@@ -1761,8 +1761,8 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
     meta &= 0xFFFFu;                   // (bits 16-31: the entry's pixel mask)
     const uint32_t n = meta & 3u;
     if (n == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
-    const float4 *base = reinterpret_cast<const float4 *>((cent >> 31) ? a.bin_glist : a.bin_list);
-    const float4 v = base[4ull * (cent & 0x7fffffffu) + 3];
+    // the triangle's plan values (its k_bin_fp record; the same in every list)
+    const float4 v = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * cent + 3];
     bool ok = true;
 #pragma unroll
     for (uint32_t c = 0; c < 2; ++c) {
@@ -1911,7 +1911,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.band = xcc_id();
     q.left = 8;
     q.has_pending = false;
-    q.nf = 1u;   // an item covers every frame of the launch
+    q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
     // timing experiment: items dealt round-robin over the waves (no atomics)
@@ -1946,7 +1946,11 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
 #endif
         BIH_PH(0);
         const uint4 hb = q.hb;
-        const uint32_t nf = a.nframes;   // multi-frame launch: an item covers its tile in every frame
+        // multi-frame launch: an item covers its tile in frames [f0, nf)
+        const uint32_t fs = a.nsplit > 1 ? it / hb.w : 0u;
+        it -= fs * hb.w;
+        const uint32_t f0 = fs * a.fpi;
+        const uint32_t nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
             const uint32_t k = (it - hb.y) * 64u + lane;
@@ -1954,7 +1958,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 const uint32_t t = a.bin_queue[hb.x + hb.y + k];
                 const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
                 const uint32_t x0 = tx * TW;
-                for (uint32_t fj = 0; fj < nf; ++fj) {
+                for (uint32_t fj = f0; fj < nf; ++fj) {
                     uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
                     for (uint32_t r = 0; r < TH; ++r) {
                         const uint32_t lr = ty * TH + r;
@@ -1984,13 +1988,19 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         // each frame takes 2*SPP draws (cudaRender), sample s the draws
         // 2s+1 and 2s+2 of its frame
         // (kept in LDS between frames: registers stay those of the list walk)
+        uint32_t dfr = a.d_base + f0 * (2u * SPP * kWeyl);   // Weyl counter at the start of frame fj
         if (valid) {
             const uint64_t P = (uint64_t)a.nrows * a.w;
+            uint32_t rs[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) s_rs[i][tid] = a.rng_in[(uint64_t)i * P + lp];
+            for (int i = 0; i < 5; ++i) rs[i] = a.rng_in[(uint64_t)i * P + lp];
+            // frame f0's state: f0 frames of 2*SPP draws past the launch's first
+            uint32_t d = a.d_base;
+            for (uint32_t k = 0; k < f0 * 2u * SPP; ++k) (void)xorwow_uniform(rs, d);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
         }
-        uint32_t dfr = a.d_base;   // Weyl counter at the start of frame fj
-        for (uint32_t fj = 0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
+        for (uint32_t fj = f0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
             uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
             float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
             if (valid) {

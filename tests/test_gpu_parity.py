@@ -469,19 +469,28 @@ def _moved_camera(bihrt, w, h, dx, dy, dz):
     return bihrt.Camera.from_list(c)
 
 
-@pytest.mark.parametrize("nstreams", [3])
-def test_camera_change_mid_sequence_on_streams(nstreams, gpu, bihrt_mod):
+@pytest.mark.parametrize("nstreams,order", [(3, "cycle3"), (3, "alternate2"), (2, "every_frame")])
+def test_camera_change_mid_sequence_on_streams(nstreams, order, gpu, bihrt_mod):
     """Frames in flight on several streams while the camera changes (and the
     tree is rebuilt) mid-sequence on a 1M-triangle soup, where rebuilding the
     per-camera records takes long enough to race a render issued on another
-    stream: every frame equals the same frame rendered alone on one stream."""
+    stream: every frame equals the same frame rendered alone on one stream.
+    The library keeps two sets of per-camera structures (bih_capi.cpp
+    CamSet): a new camera builds into the set the latest render does not
+    read; "alternate2" returns to a camera whose set is still valid, and
+    "every_frame" moves the camera on every frame."""
     import torch
     tris = bihrt_mod.scenes.soup(1_000_000, seed=1)
     w, h = 320, 180
     cams = [bihrt_mod.camera_reference(w, h), _moved_camera(bihrt_mod, w, h, 0.05, -0.03, 0.2),
             _moved_camera(bihrt_mod, w, h, -0.3, 0.1, -0.1)]
-    seq = [(0, 0), (1, 0), (2, 1), (3, 1), (4, 2), (5, 0), (6, 2), (7, 2), (8, 1), (9, 1),
-           (10, 0), (11, 0)]
+    if order == "cycle3":
+        seq = [(0, 0), (1, 0), (2, 1), (3, 1), (4, 2), (5, 0), (6, 2), (7, 2), (8, 1), (9, 1),
+               (10, 0), (11, 0)]
+    elif order == "alternate2":
+        seq = [(f, f % 2) for f in range(12)]
+    else:
+        seq = [(f, (f * 2) % 3) for f in range(12)]
     rebuild_at = 7
 
     def run(multi):
@@ -525,9 +534,12 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
     r = bihrt_mod.Renderer(g, w, h)
     cams = [bihrt_mod.camera_reference(w, h), _moved_camera(bihrt_mod, w, h, 0.05, -0.03, 0.2),
             _moved_camera(bihrt_mod, w, h, -0.3, 0.1, -0.1)]
-    # (frame, camera, forced list capacity or None, bins usable after the frame)
-    plan = [(0, 0, None, True), (1, 1, "1000", False), (2, 1, None, True), (3, 2, None, True),
-            (4, 0, "1000", False), (5, 0, None, True), (6, 1, None, True)]
+    # (frame, camera, forced list capacity or None, bins usable after the frame);
+    # the library keeps two sets of per-camera structures (CamSet), and a
+    # set's first build sizes its list with a round trip: the forced capacity
+    # acts from each set's second camera on
+    plan = [(0, 0, None, True), (1, 1, None, True), (2, 2, "1000", False), (3, 2, None, True),
+            (4, 0, "1000", False), (5, 0, None, True), (6, 1, None, True), (7, 0, None, True)]
     out = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     for f, c, cap, usable in plan:
         if cap is None:
@@ -551,7 +563,8 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
     g.close()
 
 
-@pytest.mark.parametrize("case", ["bins", "bands", "force_fallback", "spp3_per_frame"])
+@pytest.mark.parametrize("case", ["bins", "bins_items_all_frames", "bins_items_3_frames", "bands",
+                                  "bands_items_all_frames", "force_fallback", "spp3_per_frame"])
 def test_render_device_frames_equals_single_frames(case, gpu, bihrt_mod, oracle_mod, monkeypatch):
     """bih_render_device_frames: nframes consecutive frames in one call
     (one launch of each kernel through the frustum bins; frame j's jitter
@@ -566,10 +579,17 @@ def test_render_device_frames_equals_single_frames(case, gpu, bihrt_mod, oracle_
     g = bihrt_mod.GPUArrayManager(tris)
     w, h = 480, 270
     spp = 3 if case == "spp3_per_frame" else 4
-    rows = band_rows(h, 8, 1, 3) if case == "bands" else None
+    rows = band_rows(h, 8, 1, 3) if case.startswith("bands") else None
     nrows = rows.nrows if rows is not None else h
     if case == "force_fallback":
         monkeypatch.setenv("BIH_BINS_FORCE_FALLBACK", "1")
+    # frames per k_render_bins item (BIH_ITEM_TILES, bih_capi.cpp): the
+    # default splits this small image's 5 frames into 5 items per tile; 1
+    # puts all 5 in one item, 16320 (about 2x the tiles) 3 + 2
+    if case.endswith("items_all_frames"):
+        monkeypatch.setenv("BIH_ITEM_TILES", "1")
+    elif case.endswith("items_3_frames"):
+        monkeypatch.setenv("BIH_ITEM_TILES", "16320")
     r = bihrt_mod.Renderer(g, w, h, spp=spp)
     ref = []
     for f in range(7):
