@@ -40,9 +40,18 @@ constexpr size_t kEntryBytes = 16 * bih::kBinEntryF4;   // frustum-bin list entr
 // after only the renders that read that set -- so camera k+1's structures
 // build while frame k renders (a moving camera, bench `moving_camera`).
 #ifndef BIH_CAM_SETS
-#define BIH_CAM_SETS 2
+#define BIH_CAM_SETS 3
 #endif
 constexpr int kCamSets = BIH_CAM_SETS;
+// sets in use (BIH_CAM_SETS=1..kCamSets in the environment: A/B)
+static int cam_sets() {
+    static const int n = [] {
+        const char *e = getenv("BIH_CAM_SETS");
+        const int v = e ? atoi(e) : kCamSets;
+        return v < 1 ? 1 : (v > kCamSets ? kCamSets : v);
+    }();
+    return n;
+}
 struct CamSet {
     float *prim = nullptr;           // primary-ray triangle + node records (bih::prim_bytes)
     size_t prim_cap = 0;             // bytes
@@ -102,6 +111,10 @@ struct bih_tree {
     // records.
     hipEvent_t ev_rng = nullptr;
     bool rng_pending = false;
+    // after the last (re)build of the tree: the per-camera builds order after
+    // it (and after the renders that read their set), not after each other
+    hipEvent_t ev_tree = nullptr;
+    bool tree_pending = false;
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
     // render state cache (Renderer::d_rand_state / CreateCUDABuffers)
@@ -279,8 +292,10 @@ int finish_build(bih_tree *tr) {
     // renders issued on other streams order after the (re)build; tr->stream
     // waited for every render above, so this also follows the last advance
     hipError_t he = hipEventRecord(tr->ev_rng, tr->stream);
+    if (he == hipSuccess) he = hipEventRecord(tr->ev_tree, tr->stream);
     if (he != hipSuccess) return map_hip((int)he);
     tr->rng_pending = true;
+    tr->tree_pending = true;
     return BIH_OK;
 }
 
@@ -302,6 +317,7 @@ int create_tree(int device, void *stream, bih_tree **out) {
         if (e == hipSuccess) e = hipEventCreate(&tr->ev2[k]);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_tree, hipEventDisableTiming);
     for (CamSet &c : tr->cs) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c.ev_bins, hipEventDisableTiming);
         if (e == hipSuccess) e = hipHostMalloc((void **)&c.bins_host, 4 * sizeof(uint32_t), hipHostMallocDefault);
@@ -471,6 +487,7 @@ void bih_free(bih_tree *tr) {
         if (tr->ev2[k]) (void)hipEventDestroy(tr->ev2[k]);
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
+    if (tr->ev_tree) (void)hipEventDestroy(tr->ev_tree);
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
     delete tr;
 }
@@ -894,9 +911,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     uint32_t ob[12];
     static_assert(sizeof(bih_camera) == sizeof ob, "bih_camera is 12 f32");
     memcpy(ob, cam, sizeof ob);
-    int ci = (tr->cs_cur + 1) % kCamSets;
-    for (int k = 0; k < kCamSets; ++k) {
-        const int j = (tr->cs_cur + k) % kCamSets;
+    const int nsets = cam_sets();
+    int ci = (tr->cs_cur + 1) % nsets;
+    for (int k = 0; k < nsets; ++k) {
+        const int j = (tr->cs_cur + k) % nsets;
         if (tr->cs[j].prim_valid && memcmp(ob, tr->cs[j].prim_origin, sizeof ob) == 0) {
             ci = j;
             break;
@@ -918,17 +936,17 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     //    ran after render f-1-S, the last reader of buffer cur before).
     // Renders f-S+1 .. f-1 are not waited for: consecutive frames on
     // separate streams overlap, each filling the one before's tail.
+    // The camera's structures come first: a new camera's build waits only
+    // for the tree and for the renders that read its set (not for the
+    // renders or camera builds in flight on other streams), then the slot and
+    // the RNG ring as below.
     const int slot = tr->slot;
-    if (tr->used[slot]) {
-        hipError_t e = hipStreamWaitEvent(st, tr->evd[slot], 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
-    if (tr->rng_pending) {
-        hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
     int rc = BIH_OK;
     hipError_t e = hipSuccess;
+    if (tr->tree_pending) {
+        e = hipStreamWaitEvent(st, tr->ev_tree, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     // primary-ray records follow the camera (the origin; the miss-proof boxes
     // also the direction bounds)
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
@@ -994,6 +1012,16 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             }
             c.bins_redo = false;
         }
+    }
+    if (tr->used[slot]) {
+        e = hipStreamWaitEvent(st, tr->evd[slot], 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
+    if (tr->rng_pending) {
+        // (also after the structures of a camera an earlier render on
+        // another stream built, when this render reuses them)
+        e = hipStreamWaitEvent(st, tr->ev_rng, 0);
+        if (e != hipSuccess) return map_hip((int)e);
     }
     bih::RenderArgs a;
     bool use_bins = false;

@@ -533,13 +533,13 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
     g = bihrt_mod.GPUArrayManager(tris)
     r = bihrt_mod.Renderer(g, w, h)
     cams = [bihrt_mod.camera_reference(w, h), _moved_camera(bihrt_mod, w, h, 0.05, -0.03, 0.2),
-            _moved_camera(bihrt_mod, w, h, -0.3, 0.1, -0.1)]
+            _moved_camera(bihrt_mod, w, h, -0.3, 0.1, -0.1), _moved_camera(bihrt_mod, w, h, 0.1, 0.05, 0.1)]
     # (frame, camera, forced list capacity or None, bins usable after the frame);
-    # the library keeps two sets of per-camera structures (CamSet), and a
-    # set's first build sizes its list with a round trip: the forced capacity
-    # acts from each set's second camera on
-    plan = [(0, 0, None, True), (1, 1, None, True), (2, 2, "1000", False), (3, 2, None, True),
-            (4, 0, "1000", False), (5, 0, None, True), (6, 1, None, True), (7, 0, None, True)]
+    # the library keeps up to three sets of per-camera structures (CamSet),
+    # and a set's first build sizes its list with a round trip: three
+    # cameras warm every set first, then the forced capacity acts
+    plan = [(0, 0, None, True), (1, 1, None, True), (2, 2, None, True), (3, 3, "1000", False),
+            (4, 3, None, True), (5, 0, "1000", False), (6, 0, None, True), (7, 1, None, True)]
     out = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     for f, c, cap, usable in plan:
         if cap is None:
