@@ -147,6 +147,8 @@ struct bih_tree {
     // draws from set q_par[slot] and zeroes the other for the slot's next launch
     uint32_t *q_count = nullptr;
     uint32_t q_par[kSlots] = {};
+    uint32_t *rsplit = nullptr;      // per slot: XORWOW start states of a launch's later item splits
+    size_t rsplit_cap = 0;           // words per slot
     uint32_t *fb_mem = nullptr;      // per slot: fallback records of k_render_bins (8 words per tile)
     size_t fbq_cap = 0;              // tiles per slot
     // config C4 (bih_whitted.hip): two ray queues, counters and per-sample hits
@@ -479,6 +481,7 @@ void bih_free(bih_tree *tr) {
     }
     if (tr->q_count) (void)hipFree(tr->q_count);
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
+    if (tr->rsplit) (void)hipFree(tr->rsplit);
     if (tr->wh_mem) (void)hipFree(tr->wh_mem);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
@@ -518,7 +521,7 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
-                          (size_t)kSlots * tr->fbq_cap * 8) * 4;
+                          (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
     info->build_ms = tr->build_ms;
     return BIH_OK;
 }
@@ -1040,9 +1043,6 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     if (rc) return rc;
     const size_t P = (size_t)rows.nrows * w;
     const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
-    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st));
-    if (rc) return rc;
-    tr->next_frame = frame + nframes;
     a.nframes = nframes;
     a.out_stride = out_stride;
     if (use_bins && nframes > 1) {
@@ -1054,6 +1054,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         // changes the order of the work, never a pixel)
         uint32_t item_tiles = 65536u;
         if (const char *v = getenv("BIH_ITEM_TILES")) item_tiles = (uint32_t)strtoul(v, nullptr, 10);
+        // (A/B, 1M soup at 1080p, 16 frames per call: one item of 16 frames
+        // per tile 0.047 ms per frame, two of 8 0.051; a rank's eighth of the
+        // bands, 8 frames per call: items of 8 frames 0.0107 ms per frame, of
+        // 2 0.0078; 16 per call, items of 4: 0.0069)
         uint32_t tw = 0, th = 0;
         tile_shape(spp, &tw, &th);
         const uint64_t ntiles = (uint64_t)((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
@@ -1065,6 +1069,29 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         a.fpi = nframes;
         a.nsplit = 1;
     }
+    // the launch's XORWOW state after its frames (the next launch's input),
+    // and the start states of the item splits after the first (rng_split,
+    // per slot: this render reads them, the slot's next one rewrites them)
+    uint32_t *split = nullptr;
+    if (a.nsplit > 1) {
+        const size_t words = (size_t)(a.nsplit - 1) * 5 * P;
+        if (tr->rsplit_cap < words) {
+            for (int k = 0; k < kSlots; ++k)
+                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
+            if (tr->rsplit) (void)hipFree(tr->rsplit);
+            tr->rsplit = nullptr;
+            tr->rsplit_cap = 0;
+            e = hipMalloc((void **)&tr->rsplit, (size_t)kSlots * words * sizeof(uint32_t));
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->rsplit_cap = words;
+        }
+        split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
+        a.rng_split = split;
+    }
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
+                                         2 * spp * a.fpi, a.nsplit));
+    if (rc) return rc;
+    tr->next_frame = frame + nframes;
     if (use_bins) {
         a.bin_off = c.bins.off;
         a.bin_list = c.bin_list;

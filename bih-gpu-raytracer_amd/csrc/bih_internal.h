@@ -126,6 +126,7 @@ struct RenderArgs {
     // item so that the items still outnumber the waves
     uint32_t fpi = 1;
     uint32_t nsplit = 1;
+    const uint32_t *rng_split = nullptr;    // split s >= 1's start states at (s-1) * 5 planes (k_rng_advance)
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
@@ -208,7 +209,7 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
 int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
-                       void *stream);
+                       void *stream, uint32_t *split = nullptr, uint32_t every = 0, uint32_t nsplit = 0);
 // ev_k0 / ev_k1 (hipEvent_t or null): recorded right before and after the
 // main render kernel (bih_last_render_ms)
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev_k0 = nullptr,

@@ -135,14 +135,23 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
 // may be src).  2*spp steps: the state the next frame starts from
 // (cudaRender's write-back, CUDAKernels.cu:419); more: a gap in the frame
 // sequence.  The Weyl counter d is derived from the frame index, not stored.
+// split (optional): the states after every `every` steps, s = 1 .. nsplit-1
+// at split + (s-1) * 5 * P (the starts of a multi-frame k_render_bins
+// launch's later frame splits, RenderArgs::rng_split)
 __global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst,
-                                                          uint64_t P, uint32_t steps) {
+                                                          uint64_t P, uint32_t steps, uint32_t *split,
+                                                          uint32_t every, uint32_t nsplit) {
     const uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (lp >= P) return;
     uint32_t v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
     for (uint32_t k = 0; k < steps; ++k) {
+        if (split && k && k % every == 0 && k / every < nsplit) {
+            uint32_t *o = split + (uint64_t)(k / every - 1) * 5 * P;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) o[(uint64_t)i * P + lp] = v[i];
+        }
         const uint32_t t = v[0] ^ (v[0] >> 2);
         v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
         v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
@@ -1990,15 +1999,12 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         // (kept in LDS between frames: registers stay those of the list walk)
         uint32_t dfr = a.d_base + f0 * (2u * SPP * kWeyl);   // Weyl counter at the start of frame fj
         if (valid) {
+            // frame f0's state: the launch's first frame's, or the split's
+            // start that k_rng_advance stored (f0 frames of 2*SPP draws on)
             const uint64_t P = (uint64_t)a.nrows * a.w;
-            uint32_t rs[5];
+            const uint32_t *src = fs ? a.rng_split + (uint64_t)(fs - 1) * 5 * P : a.rng_in;
 #pragma unroll
-            for (int i = 0; i < 5; ++i) rs[i] = a.rng_in[(uint64_t)i * P + lp];
-            // frame f0's state: f0 frames of 2*SPP draws past the launch's first
-            uint32_t d = a.d_base;
-            for (uint32_t k = 0; k < f0 * 2u * SPP; ++k) (void)xorwow_uniform(rs, d);
-#pragma unroll
-            for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
+            for (int i = 0; i < 5; ++i) s_rs[i][tid] = src[(uint64_t)i * P + lp];
         }
         for (uint32_t fj = f0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
             uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
@@ -2820,11 +2826,11 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
 }
 
 int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
-                       void *stream) {
+                       void *stream, uint32_t *split, uint32_t every, uint32_t nsplit) {
     if (pixels == 0 || (steps == 0 && src == dst)) return 0;
     const uint32_t blocks = (uint32_t)((pixels + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, src,
-                       dst, (uint64_t)pixels, steps);
+                       dst, (uint64_t)pixels, steps, split, every ? every : 1u, split ? nsplit : 0u);
     return (int)hipGetLastError();
 }
 
