@@ -428,7 +428,7 @@ def main():
                "gbs": alg_bytes / (launch_ms * 1e-3) / 1e9}
     bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
             "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
-            "entry_bytes": 64,
+            "entry_bytes": 48,
             "note": "frustum bins of the bench camera (bih_bins_get_stats): per 4x4-pixel tile the "
                     "triangles whose edge pre-test a sample of the tile can pass"}
 
