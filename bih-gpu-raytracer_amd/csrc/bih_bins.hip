@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(kThreads) k_cam_tris(const float *__restrict__
     if (i == 0) {
         gcount[0] = gcount[1] = gcount[2] = 0u;
         gcount[4] = gcount[5] = 0u;
+        gcount[6] = 0u;   // pair-result positions (k_bin_count)
     }
     const unsigned long long mk = __ballot(al);
     if (lane == 0) {
@@ -631,15 +632,20 @@ __device__ __forceinline__ uint32_t pixel_mask(const float4 r0, const float4 r1,
 // whose area range holds p, tile p - its start in row-major order), so a
 // large rectangle (a triangle close to the camera or seen edge-on) is spread
 // over the whole block and every lane runs the same `visit` code.
+// `reserve(tot)` (thread 0, after the scan) returns the block's base in the
+// pair-result buffer (k_bin_count reserves it, k_bin_fill reads it back; ~0:
+// none); `visit` gets (triangle, tile x, tile y, base, pair index).
 struct PairLds {
     uint32_t off[kThreads + 1];   // exclusive scan of the areas; off[kThreads] = the block's pairs
     uint32_t tri[kThreads];
     uint2 rect[kThreads];
     uint32_t wsum[kThreads / 64];
+    uint32_t base;
 };
-template <typename F>
+template <typename R, typename F>
 __device__ __forceinline__ void for_block_pairs(const uint2 *__restrict__ brect, const uint32_t *__restrict__ live,
-                                                const uint32_t *__restrict__ live_count, PairLds &L, F &&visit) {
+                                                const uint32_t *__restrict__ live_count, PairLds &L, R &&reserve,
+                                                F &&visit) {
     const uint32_t tid = threadIdx.x, j0 = blockIdx.x * kThreads + tid, lane = tid & 63u, w = tid >> 6;
     const uint32_t nl = *live_count;
     uint2 q = make_uint2(1u, 0u);
@@ -667,8 +673,12 @@ __device__ __forceinline__ void for_block_pairs(const uint2 *__restrict__ brect,
         tot += L.wsum[k];
     }
     L.off[tid] = base + x - area;
-    if (tid == 0) L.off[kThreads] = tot;
+    if (tid == 0) {
+        L.off[kThreads] = tot;
+        L.base = reserve(tot);
+    }
     __syncthreads();
+    const uint32_t pbase = L.base;
     for (uint32_t p = tid; p < tot; p += kThreads) {
         // the last triangle t with off[t] <= p (zero areas repeat an offset)
         uint32_t lo = 0, hi = kThreads;   // off[lo] <= p < off[hi]
@@ -680,7 +690,7 @@ __device__ __forceinline__ void for_block_pairs(const uint2 *__restrict__ brect,
         const uint2 r = L.rect[lo];
         const uint32_t k = p - L.off[lo], wx = r.y;
         const uint32_t ty = k / wx;
-        visit(L.tri[lo], (r.x & 0xffffu) + (k - ty * wx), (r.x >> 16) + ty);
+        visit(L.tri[lo], (r.x & 0xffffu) + (k - ty * wx), (r.x >> 16) + ty, pbase, p);
     }
 }
 
@@ -722,7 +732,10 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
                                                         uint32_t w, uint32_t h, uint32_t tw, uint32_t th,
                                                         uint32_t *__restrict__ cnt, uint32_t *__restrict__ cntq,
                                                         unsigned long long *__restrict__ blkcnt,
-                                                        unsigned long long *__restrict__ total64) {
+                                                        unsigned long long *__restrict__ total64,
+                                                        uint32_t *__restrict__ pres, uint32_t pres_cap,
+                                                        uint32_t *__restrict__ pcount,
+                                                        uint32_t *__restrict__ pbase_out) {
     __shared__ unsigned long long s_cnt[kBlockTiles];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
     __shared__ unsigned long long s_tot;   // the block's entries (64-bit: the list total may pass 2^32)
@@ -752,11 +765,24 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     for (uint32_t k = tid; k < rarea; k += kThreads) s_cnt[k] = 0ull;
     __syncthreads();
     unsigned long long mine = 0ull;
-    for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    auto reserve = [&](uint32_t tot) {
+        uint32_t b = ~0u;
+        if (pres && tot) {
+            b = atomicAdd(pcount, tot);
+            if (b > pres_cap || pres_cap - b < tot) b = ~0u;   // past the buffer: the fill recomputes
+        }
+        pbase_out[blockIdx.x] = b;
+        return b;
+    };
+    for_block_pairs(brect, live, live_count, L, reserve, [&](uint32_t i, uint32_t bx, uint32_t by, uint32_t pb,
+                                                             uint32_t p) {
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
         const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+        const uint32_t pm = cls == 2 ? 0xFFFFu : (cls ? pixel_mask(r0, r1, r2, bx, by, w, h, tw, th) : 0u);
+        const uint32_t q = entry_bucket(cls, pm);
+        // the pair's result for k_bin_fill: listed | pixel mask << 8 | bucket
+        if (pb != ~0u) pres[pb + p] = cls ? (0x80000000u | (pm << 8) | q) : 0u;
         if (!cls) return;
-        const uint32_t q = entry_bucket(cls, cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th));
         ++mine;
         if (use_lds) {
             atomicAdd(&s_cnt[(by - ry0) * rw + (bx - rx0)], 1ull << (kBucketBits * q));
@@ -807,7 +833,9 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
                                                        uint32_t *__restrict__ cur,
                                                        const float4 *__restrict__ binrec,
                                                        const uint32_t *__restrict__ gstat,
-                                                       float4 *__restrict__ list) {
+                                                       float4 *__restrict__ list,
+                                                       const uint32_t *__restrict__ pres,
+                                                       const uint32_t *__restrict__ pbase_in) {
     if (*gstat == kBinsUnusable) return;   // the lists would not fit: the render falls back
     constexpr uint32_t kS = kBlockTiles;
     __shared__ unsigned long long s_cnt[kS];
@@ -857,13 +885,26 @@ __global__ void __launch_bounds__(kThreads) k_bin_fill(const uint2 *__restrict__
         }
         __syncthreads();
     }
-    for_block_pairs(brect, live, live_count, L, [&](uint32_t i, uint32_t bx, uint32_t by) {
+    auto reserve = [&](uint32_t) { return pres ? pbase_in[blockIdx.x] : ~0u; };
+    for_block_pairs(brect, live, live_count, L, reserve, [&](uint32_t i, uint32_t bx, uint32_t by, uint32_t pb,
+                                                             uint32_t p) {
+        // the pair's class, pixel mask and bucket: k_bin_count's result when
+        // its block had room in the pair buffer, else computed again
+        uint32_t pm, q;
+        if (pb != ~0u) {
+            const uint32_t r = pres[pb + p];
+            if (!(r >> 31)) return;
+            pm = (r >> 8) & 0xFFFFu;
+            q = r & 0xFFu;
+        } else {
+            const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
+            const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
+            if (!cls) return;
+            pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
+            q = entry_bucket(cls, pm);
+        }
         const float4 r0 = binrec[4ull * i], r1 = binrec[4ull * i + 1], r2 = binrec[4ull * i + 2];
-        const int cls = tile_class(r0, r1, r2, bx, by, w, h, tw, th);
-        if (!cls) return;
         // the entry's word 11: plan meta (bits 0-13) | pixel mask << 16
-        const uint32_t pm = cls == 2 ? 0xFFFFu : pixel_mask(r0, r1, r2, bx, by, w, h, tw, th);
-        const uint32_t q = entry_bucket(cls, pm);
         uint32_t pos;
         if (use_lds) {
             const uint32_t k = (by - ry0) * rw + (bx - rx0);
@@ -1103,7 +1144,8 @@ int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uin
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt, b.cntq,
                            reinterpret_cast<unsigned long long *>(b.blkcnt),
-                           reinterpret_cast<unsigned long long *>(b.gcount + 4));
+                           reinterpret_cast<unsigned long long *>(b.gcount + 4), b.pres, b.pres_cap, b.gcount + 6,
+                           b.pbase);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
@@ -1129,7 +1171,8 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
         hipLaunchKernelGGL(k_bin_fill, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                            b.brect, b.live, b.gcount + 3, b.bins_x, c.w, c.h, c.tw, c.th, b.off, b.cntq,
                            reinterpret_cast<const unsigned long long *>(b.blkcnt), b.cur,
-                           reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list));
+                           reinterpret_cast<const float4 *>(b.binrec), gstat, reinterpret_cast<float4 *>(list),
+                           b.pres, b.pbase);
     if (n > 0)
         hipLaunchKernelGGL(k_bin_gfill, dim3((kBinGlobalMax + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                            gstat, b.glist, reinterpret_cast<const float4 *>(b.binrec),

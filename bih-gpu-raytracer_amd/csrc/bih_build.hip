@@ -115,6 +115,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
     // wave reduce, block reduce through LDS, one partial per block (the
     // single-block k_prep_final folds them: no contended atomics)
     __shared__ unsigned long long s_key[7][kThreads / 64];
+    __shared__ uint32_t s_bad[kThreads / 64];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -137,7 +138,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             s_key[3 + a][wv] = kmax[a];
         }
         s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
-        if (anybad) atomicOr(&hdr->nonfinite, 1u);
+        s_bad[wv] = anybad ? 1u : 0u;
     }
     __syncthreads();
     if (threadIdx.x < 7) {
@@ -148,6 +149,11 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
         part[(size_t)a * gridDim.x + blockIdx.x] = r;
+    }
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
+        uint32_t b = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
+        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
     }
 }
 
@@ -176,7 +182,7 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
                                                          const unsigned long long *__restrict__ part,
                                                          uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
-    __shared__ unsigned long long s_red[7][kThreads / 64];
+    __shared__ unsigned long long s_red[8][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -197,11 +203,24 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
         for (int off = 32; off > 0; off >>= 1) hxy ^= __shfl_xor(hxy, off);
         if (lane == 0) s_red[6][wv] = hxy;
     }
+    {   // non-finite flags of the blocks
+        unsigned long long b = 0ull;
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= part[(size_t)7 * nparts + i];
+        for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off);
+        if (lane == 0) s_red[7][wv] = b;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long hxy = 0ull;
-        for (uint32_t w = 0; w < kThreads / 64; ++w) hxy ^= s_red[6][w];
+        // the rest of the header (k_hdr_init's work when there are triangles)
+        unsigned long long hxy = 0ull, bad = 0ull;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            hxy ^= s_red[6][w];
+            bad |= s_red[7][w];
+        }
         hdr->content = hxy;
+        hdr->nonfinite = bad ? 1u : 0u;
+        hdr->n_unique = 0;
+        hdr->pad0 = 0;
     }
     const int a = threadIdx.x;
     if (a >= 3) return;
@@ -447,6 +466,7 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
     const int U = (int)hdr->n_unique;
     uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
     if (U < 2 || idx > (uint32_t)(U - 2)) return;
+    if (idx == 0) parent[0] = -1;   // the root; every other node is written as a child below
     uint32_t cur = umc[idx];
     uint32_t pre0 = 0xFFFFFFFFu, pre1 = 0xFFFFFFFFu;
     if (idx) pre0 = (uint32_t)clz32(cur ^ umc[idx - 1]);
@@ -548,7 +568,7 @@ __device__ __forceinline__ void pack_tri(const float *__restrict__ p, float *__r
 }
 
 // Leaf boxes, and the sorted triangle records of each leaf's run (the runs
-// partition the sorted triangles: k_pack_tris' work, read once with the
+// partition the sorted triangles: read once with the
 // vertices the boxes come from).
 __global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restrict__ hdr,
                                                        const uint32_t *__restrict__ tri_idx,
@@ -693,10 +713,22 @@ __global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__res
                                                          const uint8_t *__restrict__ is_leaf,
                                                          const int32_t *__restrict__ first,
                                                          const uint32_t *__restrict__ cnt,
-                                                         uint4 *__restrict__ nodes) {
+                                                         uint4 *__restrict__ nodes,
+                                                         const float *__restrict__ v,
+                                                         const uint32_t *__restrict__ tri_idx, uint32_t n,
+                                                         float *__restrict__ tris_s) {
     const uint32_t U = hdr->n_unique;
     uint32_t p = blockIdx.x * kThreads + threadIdx.x;
-    if (U < 2 || p >= U - 1) return;
+    if (U < 2) {
+        // one leaf: no node, and k_seg_leaf did not run -- the sorted
+        // triangle records here (k_seg_leaf packs every leaf run otherwise)
+        for (uint32_t i = p; i < n; i += gridDim.x * kThreads) {
+            float lo[3], hi[3];
+            pack_tri(v + 9ull * tri_idx[i], tris_s + 9ull * i, lo, hi);
+        }
+        return;
+    }
+    if (p >= U - 1) return;
     uint32_t split = (uint32_t)children[2 * p];
     uint32_t lL = is_leaf[2 * p], lR = is_leaf[2 * p + 1];
     uint32_t mid = (uint32_t)first[split + 1];
@@ -711,16 +743,6 @@ __global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__res
     nodes[p] = nd;
 }
 
-__global__ void __launch_bounds__(kThreads) k_pack_tris(const TreeHeader *__restrict__ hdr,
-                                                        const float *__restrict__ v,
-                                                        const uint32_t *__restrict__ tri_idx, uint32_t n,
-                                                        float *__restrict__ out) {
-    if (hdr->n_unique >= 2) return;   // k_seg_leaf packed every leaf run
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
-        float lo[3], hi[3];
-        pack_tri(v + 9ull * tri_idx[i], out + 9ull * i, lo, hi);
-    }
-}
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kThreads - 1) / kThreads); }
 
@@ -804,7 +826,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
         BIH_TRY(dalloc(&t.hist, hist_n, b));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, b));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 7ull * kPrepBlocks, b));
+        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, b));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
         // tag): stale data in fresh memory must not pass for a predecessor's
         // published prefix; afterwards every word carries an older call's
@@ -816,8 +838,8 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     BIH_TRY(hipEventCreate(&e1));
     BIH_TRY(hipEventRecord(e0, st));
 
-    // header reset: keys to their identities, counters to zero
-    hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
+    // header reset (no triangles; otherwise k_prep_final writes the header)
+    if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
@@ -845,7 +867,6 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.scan_tmp, n, t.unique_mc, t.first_idx);
         hipLaunchKernelGGL(k_run_counts, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.first_idx,
                            t.hdr, n, t.dup_cnt, t.leaf_parent);
-        BIH_TRY(hipMemsetAsync(t.parent, 0xFF, sizeof(int32_t) * nn, st));
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr,
                            t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
         const uint64_t cap = seg_capacity(nn);
@@ -861,11 +882,8 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
                            t.axis, t.fit_seg, cap, nn, t.clip);
         hipLaunchKernelGGL(k_pack_nodes, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.clip,
-                           t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes);
-        // one leaf (U < 2: k_seg_leaf did not run): the records here; a
-        // no-op otherwise (U is on the device only until the build ends)
-        hipLaunchKernelGGL(k_pack_tris, dim3(blocks_for(n) < 1024u ? blocks_for(n) : 1024u), dim3(kThreads), 0, st,
-                           t.hdr, t.v, t.vals, n, t.tris_s);
+                           t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes, t.v, t.vals, n,
+                           t.tris_s);
         BIH_TRY(hipGetLastError());
     }
     BIH_TRY(hipEventRecord(e1, st));

@@ -679,15 +679,20 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
     const size_t s_brect = al((size_t)n * 8), s_cnt = nb * 4, s_cntq = nb * 4 * (bih::kBinBuckets - 1),
                  s_cur = al(nb * 4 * bih::kBinBuckets),
                  s_off = al((nb + 1) * 4),
-                 s_g = al(6 * 4), s_glist = al((size_t)n * 4 + 4),
+                 s_g = al(8 * 4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
                  s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
                  s_gent = al((size_t)4097 * kEntryBytes), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
                  s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
                  s_bpart = al(bih::scan_partials_words(nblk) * 4),
-                 s_blkcnt = al((size_t)nblk * bih::kBinBlockTiles * 8);
+                 s_blkcnt = al((size_t)nblk * bih::kBinBlockTiles * 8),
+                 s_pbase = al((size_t)nblk * 4);
+    // pair results (k_bin_count -> k_bin_fill): 4 B per (triangle, tile)
+    // pair; blocks past the buffer recompute in the fill
+    const uint32_t pres_cap = (uint32_t)std::min<uint64_t>(4ull * n + (1u << 20), 0x3FFFFFFFull);
+    const size_t s_pres = al((size_t)pres_cap * 4);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
-                        s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt;
+                        s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt + s_pbase + s_pres;
     if (c.bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -716,7 +721,10 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
     b.bcnt = reinterpret_cast<uint32_t *>(p); p += s_bcnt;
     b.boff = reinterpret_cast<uint32_t *>(p); p += s_boff;
     b.bpart = reinterpret_cast<uint32_t *>(p); p += s_bpart;
-    b.blkcnt = reinterpret_cast<uint32_t *>(p);
+    b.blkcnt = reinterpret_cast<uint32_t *>(p); p += s_blkcnt;
+    b.pbase = reinterpret_cast<uint32_t *>(p); p += s_pbase;
+    b.pres = reinterpret_cast<uint32_t *>(p);
+    b.pres_cap = pres_cap;
     // the scans' look-back words (partials, bpart) must start at tag 0 (never
     // a call's tag) wherever this layout puts them: stale data there must not
     // pass for a published prefix.  Later calls leave older, unique tags.

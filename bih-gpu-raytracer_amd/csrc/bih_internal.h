@@ -150,7 +150,8 @@ struct BinBuffers {
     uint32_t *cur = nullptr;      // [nb][kBinBuckets] the fill's cursors per tile and bucket
     uint32_t *blkcnt = nullptr;   // [blocks][kBinBlockTiles] u64: k_bin_count's per-block (tile, bucket) counts
     uint32_t *off = nullptr;      // [nb + 1] list offsets, off[nb] = list length
-    uint32_t *gcount = nullptr;   // [4] global list length, status (k_bin_status), list total, alive count
+    uint32_t *gcount = nullptr;   // [8] global list length, status (k_bin_status), list total, alive count,
+                                  // 64-bit list total, pair-result cursor
     uint32_t *live = nullptr;     // [n] alive triangles (k_live_compact)
     uint32_t *bmask = nullptr;    // [blocks][4] u64 alive masks of k_cam_tris' blocks
     uint32_t *bcnt = nullptr;     // [blocks] their counts
@@ -160,6 +161,9 @@ struct BinBuffers {
     uint32_t *partials = nullptr; // scan scratch
     float *binrec = nullptr;      // [n][16] list entry of each triangle
     uint2 *path = nullptr;        // [U][32] root path steps per leaf
+    uint32_t *pres = nullptr;     // [pres_cap] per (triangle, tile) pair: k_bin_count's class / pixel mask / bucket
+    uint32_t pres_cap = 0;
+    uint32_t *pbase = nullptr;    // [blocks] each count block's base in pres (~0: none)
 };
 
 // Device buffers of one tree.
