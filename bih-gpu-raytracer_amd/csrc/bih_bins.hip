@@ -384,7 +384,15 @@ __device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint
 // bx1 << 16, by0 | by1 << 16; empty = bx0 > bx1) and its list entry
 // binrec[i]; the global list takes the rest.  leaf = the leaf of each sorted
 // triangle (DeviceTree::tri_leaf).
-__global__ void __launch_bounds__(kThreads) k_bin_fp(const float *__restrict__ prim, uint32_t n,
+#ifndef BIH_FP_WAVES_PER_EU
+#define BIH_FP_WAVES_PER_EU 0   // 0: the compiler's choice (128 VGPRs, 4 waves/SIMD)
+#endif
+#if BIH_FP_WAVES_PER_EU
+#define BIH_FP_OCC __attribute__((amdgpu_waves_per_eu(BIH_FP_WAVES_PER_EU, BIH_FP_WAVES_PER_EU)))
+#else
+#define BIH_FP_OCC
+#endif
+__global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__restrict__ prim, uint32_t n,
                                                      BinCamera c, const TreeHeader *__restrict__ hdr,
                                                      const uint4 *__restrict__ node_prim,
                                                      const uint32_t *__restrict__ tri_leaf,
