@@ -43,6 +43,8 @@ constexpr int kWLds = 8;                // stack slots per lane in LDS; deeper o
 constexpr uint32_t kWBlocksPerCU = 32;  // persistent grid of k_wh_trace
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
+constexpr uint32_t kWCounts = 32;       // counter words: [0..9] rays per queue, [16..25] rays taken (k_wh_trace_dyn)
+constexpr uint32_t kWFetch = 16;
 
 struct WScene {
     const uint4 *nodes;
@@ -239,7 +241,7 @@ __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, ui
     const uint64_t gid = (uint64_t)blockIdx.x * kWT + threadIdx.x;
     if (gid == 0) {
         counts[0] = (uint32_t)rays;
-        for (int k = 1; k < 16; ++k) counts[k] = 0u;
+        for (uint32_t k = 1; k < kWCounts; ++k) counts[k] = 0u;
     }
     if (gid >= rays) return;
     const uint64_t lp = gid / a.spp;
@@ -329,6 +331,199 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
     }
 }
 
+// k_wh_trace with per-lane ray fetching (U >= 2): a lane whose walk has
+// ended takes the next ray of the queue while the other lanes of its wave
+// keep walking, so a wave no longer waits for its slowest ray before taking
+// 64 new ones (secondary rays trapped in the soup walk very unequal visit
+// sets).  Each lane's walk is closest_walk's, step for step: one iteration of
+// its loop per wave iteration, the same decisions, intervals, stack and (t, i)
+// rule -- the same hit.  Idle lanes are refilled with one atomic per wave
+// when a quarter of the wave is idle (or all of it).
+struct WRay {
+    float o[3], d[3], ix, iy, iz, tMin, tMax, bt;
+    uint32_t sg, cur, sp, bi, sid;
+};
+__device__ __forceinline__ bool wray_start(const WScene &s, WRay &r) {
+    r.bt = FLT_MAX;
+    r.bi = kNoHit;
+    r.cur = 0;
+    r.sp = 0;
+    r.ix = 1.0f / r.d[0];
+    r.iy = 1.0f / r.d[1];
+    r.iz = 1.0f / r.d[2];
+    r.sg = (r.ix < 0.0f ? 1u : 0u) | (r.iy < 0.0f ? 2u : 0u) | (r.iz < 0.0f ? 4u : 0u);
+    // scene-AABB slab test, CUDAKernels.cu:237-262 (as closest_walk)
+    float tMin = (((r.sg & 1) ? s.shi[0] : s.slo[0]) - r.o[0]) * r.ix;
+    float tMax = (((r.sg & 1) ? s.slo[0] : s.shi[0]) - r.o[0]) * r.ix;
+    const float tymin = (((r.sg & 2) ? s.shi[1] : s.slo[1]) - r.o[1]) * r.iy;
+    const float tymax = (((r.sg & 2) ? s.slo[1] : s.shi[1]) - r.o[1]) * r.iy;
+    if ((tMin > tymax) || (tymin > tMax)) return false;
+    if (tymin > tMin) tMin = tymin;
+    if (tymax < tMax) tMax = tymax;
+    const float tzmin = (((r.sg & 4) ? s.shi[2] : s.slo[2]) - r.o[2]) * r.iz;
+    const float tzmax = (((r.sg & 4) ? s.slo[2] : s.shi[2]) - r.o[2]) * r.iz;
+    if ((tMin > tzmax) || (tzmin > tMax)) return false;
+    if (tzmin > tMin) tMin = tzmin;
+    if (tzmax < tMax) tMax = tzmax;
+    r.tMin = tMin;
+    r.tMax = tMax;
+    return true;
+}
+// one iteration of closest_walk's loop; true when the walk has ended
+__device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, const WStack &stk) {
+    auto leaf = [&](uint32_t b, uint32_t e) {
+        for (uint32_t i = b; i < e; ++i) {
+            float t;
+            if (mt_t(s.tris + 9ull * i, r.o[0], r.o[1], r.o[2], r.d[0], r.d[1], r.d[2], t_lo, t) &&
+                (t < r.bt || (t == r.bt && i < r.bi))) {
+                r.bt = t;
+                r.bi = i;
+            }
+        }
+    };
+    const float best = r.bi != kNoHit ? r.bt : __builtin_inff();
+    if (r.tMin > best) {                          // entered beyond the best hit: skip
+        if (r.sp == 0) return true;
+        --r.sp;
+        stk.pop(r.sp, r.cur, r.tMin, r.tMax);
+        return false;
+    }
+    if (best < r.tMax) r.tMax = best;
+    const uint4 nd = s.nodes[r.cur];
+    const uint32_t ax = (nd.z >> 27) & 3u;
+    const float org = pick3(ax, r.o[0], r.o[1], r.o[2]), inv = pick3(ax, r.ix, r.iy, r.iz);
+    const uint32_t nr = (r.sg >> ax) & 1u;
+    const float t0 = (__uint_as_float(nd.x) - org) * inv;
+    const float t1 = (__uint_as_float(nd.y) - org) * inv;
+    const float tn = nr ? t1 : t0, tf = nr ? t0 : t1;
+    const bool A = r.tMin < tn, B = r.tMax < tf;
+    const uint32_t split = nd.z & kIdxMask, mid = nd.w & kIdxMask;
+    const bool leafL = (nd.z >> 29) & 1u, leafR = (nd.z >> 30) & 1u;
+    const bool leafN = nr ? leafR : leafL, leafF = nr ? leafL : leafR;
+    uint32_t cL = (nd.w >> 27) & 3u, cR = (nd.w >> 29) & 3u;
+    if (leafL && cL == 0) cL = s.dup[split];
+    if (leafR && cR == 0) cR = s.dup[split + 1];
+    const uint32_t nb = nr ? mid : mid - cL, ne = nr ? mid + cR : mid;
+    const uint32_t fb = nr ? mid - cL : mid, fe = nr ? mid : mid + cR;
+    const uint32_t nearc = split + nr, farc = split + 1u - nr;
+    bool pop = false;
+    if (!A && B) {
+        pop = true;
+    } else if (A && B) {
+        if (leafN) { leaf(nb, ne); pop = true; }
+        else { r.cur = nearc; r.tMax = tn; }
+    } else if (!A && !B) {
+        if (leafF) { leaf(fb, fe); pop = true; }
+        else { r.cur = farc; r.tMin = tf; }
+    } else {
+        if (leafN && leafF) {
+            leaf(nb, ne);
+            leaf(fb, fe);
+            pop = true;
+        } else if (!leafN && leafF) {
+            leaf(fb, fe);
+            r.cur = nearc; r.tMax = tn;
+        } else if (leafN && !leafF) {
+            leaf(nb, ne);
+            r.cur = farc; r.tMin = tf;
+        } else {
+            stk.push(r.sp, farc, tf, r.tMax);
+            ++r.sp;
+            r.cur = nearc; r.tMax = tn;
+        }
+    }
+    if (pop) {
+        if (r.sp == 0) return true;
+        --r.sp;
+        stk.pop(r.sp, r.cur, r.tMin, r.tMax);
+    }
+    return false;
+}
+__global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
+                                                      uint32_t *counts, uint8_t *hits, uint32_t *spill) {
+    __shared__ uint32_t s_node[kWLds * kWT];
+    __shared__ float s_min[kWLds * kWT];
+    __shared__ float s_max[kWLds * kWT];
+    const uint32_t lane = threadIdx.x;
+    WStack stk;
+    stk.sn = s_node + lane;
+    stk.smin = s_min + lane;
+    stk.smax = s_max + lane;
+    stk.gthreads = (uint64_t)gridDim.x * kWT;
+    stk.spill = spill + (uint64_t)blockIdx.x * kWT + lane;
+    const WScene sc = load_wscene(a);
+    const uint32_t n = counts[depth];
+    uint32_t *fetch = counts + kWFetch + depth;   // rays of queue `depth` taken so far
+    const float t_lo = depth ? kBounceTLo : 0.0f;
+    const uint32_t *sid_in = reinterpret_cast<const uint32_t *>(qin.p) + 6 * qin.cap;
+    WRay r;
+    bool has = false;          // this lane walks a ray
+    bool more = true;          // (wave-uniform) the queue may still hold rays
+    for (;;) {
+        const unsigned long long idle = __ballot(!has);
+        if (more && (__popcll(idle) >= kWT / 4 || idle == ~0ull)) {
+            const uint32_t k = (uint32_t)__popcll(idle);
+            uint32_t first = 0;
+            if (lane == 0) first = atomicAdd(fetch, k);
+            first = __builtin_amdgcn_readfirstlane(first);
+            if (first + k >= n) more = false;
+            if (!has) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint64_t i = (uint64_t)first + rk;
+                if (i < n) {
+                    for (int c = 0; c < 3; ++c) {
+                        r.o[c] = qin.p[c * qin.cap + i];
+                        r.d[c] = qin.p[(3 + c) * qin.cap + i];
+                    }
+                    r.sid = sid_in[i];
+                    has = wray_start(sc, r);   // a ray that misses the scene box ends here: no hit
+                }
+            }
+        }
+        if (!__ballot(has)) {
+            if (!more) break;
+            continue;
+        }
+        bool fin = false;
+        if (has) fin = wray_step(sc, r, t_lo, stk);
+        const bool hit = fin && r.bi != kNoHit;
+        if (hit) hits[r.sid] = (uint8_t)(depth + 1);
+        // the mirror ray (oracle whitted_path), then compaction into qout
+        const bool next = hit && depth < 8u;
+        float po[3], rd[3];
+        if (next) {
+            const float *v = sc.tris + 9ull * r.bi;
+            const float e1x = v[3], e1y = v[4], e1z = v[5], e2x = v[6], e2y = v[7], e2z = v[8];
+            const float nx = e1y * e2z - e2y * e1z;        // n = cross(e1, e2), glm order
+            const float ny = e1z * e2x - e2z * e1x;
+            const float nz = e1x * e2y - e2x * e1y;
+            const float dn = (r.d[0] * nx + r.d[1] * ny) + r.d[2] * nz;
+            const float nn = (nx * nx + ny * ny) + nz * nz;
+            const float kk = (2.0f * dn) / nn;
+            const float nv[3] = {nx, ny, nz};
+            for (int k = 0; k < 3; ++k) {
+                const float td = r.bt * r.d[k];
+                po[k] = r.o[k] + td;
+                const float kn = kk * nv[k];
+                rd[k] = r.d[k] - kn;
+            }
+        }
+        const unsigned long long m = __ballot(next);
+        if (m) {
+            uint32_t first = 0;
+            if (lane == 0) first = atomicAdd(counts + depth + 1, (uint32_t)__popcll(m));
+            first = __builtin_amdgcn_readfirstlane(first);
+            if (next) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                qout.put((uint64_t)first + rk, po, rd, r.sid);
+            }
+        }
+        if (fin) has = false;
+    }
+}
+
 // shade of a sample with h hits (oracle whitted_shade), f32
 __device__ __forceinline__ void wh_shade(uint32_t h, float &r, float &g, float &b) {
     if (h > 8u) { r = 255.0f; g = 255.0f; b = 0.0f; h = 8u; }
@@ -369,7 +564,7 @@ static uint32_t whitted_grid(uint64_t rays) {
 // two queues of 7 planes, 16 counters, per-sample hits (u8), the stack spill
 size_t whitted_bytes(uint64_t rays) {
     const uint64_t q = 2 * 7 * rays * 4, hits = (rays + 255) & ~255ull;
-    return q + 64 + hits + (uint64_t)whitted_grid(rays) * kWT * (kWStack - kWLds) * 3 * 4;
+    return q + kWCounts * 4 + hits + (uint64_t)whitted_grid(rays) * kWT * (kWStack - kWLds) * 3 * 4;
 }
 
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
@@ -379,15 +574,27 @@ int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hi
     float *base = reinterpret_cast<float *>(mem);
     WQueue q0{base, rays}, q1{base + 7 * rays, rays};
     uint32_t *counts = reinterpret_cast<uint32_t *>(base + 14 * rays);
-    uint8_t *hits = reinterpret_cast<uint8_t *>(counts + 16);
+    uint8_t *hits = reinterpret_cast<uint8_t *>(counts + kWCounts);
     uint32_t *spill = reinterpret_cast<uint32_t *>(hits + ((rays + 255) & ~255ull));
     hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits);
     hipError_t e = ev_k0 ? hipEventRecord((hipEvent_t)ev_k0, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
     const uint32_t grid = whitted_grid(rays);
-    for (uint32_t d = 0; d <= 8; ++d)
-        hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0, (d & 1) ? q0 : q1,
-                           counts, hits, spill);
+    // per-lane ray fetching (k_wh_trace_dyn) needs internal nodes; a one-leaf
+    // tree (or BIH_WH_STATIC=1, A/B) takes the wave-per-64-rays kernel
+    static const bool dyn_on = [] {
+        const char *e = getenv("BIH_WH_STATIC");
+        return !(e && e[0] == '1');
+    }();
+    const bool dyn = dyn_on && a.n_nodes > 0;
+    for (uint32_t d = 0; d <= 8; ++d) {
+        if (dyn)
+            hipLaunchKernelGGL(k_wh_trace_dyn, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0,
+                               (d & 1) ? q0 : q1, counts, hits, spill);
+        else
+            hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0,
+                               (d & 1) ? q0 : q1, counts, hits, spill);
+    }
     e = ev_k1 ? hipEventRecord((hipEvent_t)ev_k1, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
     const uint64_t P = (uint64_t)a.nrows * a.w;
