@@ -339,6 +339,12 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
 // its loop per wave iteration, the same decisions, intervals, stack and (t, i)
 // rule -- the same hit.  Idle lanes are refilled with one atomic per wave
 // when a quarter of the wave is idle (or all of it).
+#ifndef BIH_WH_REFILL
+#define BIH_WH_REFILL 16   // idle lanes of a wave that trigger a refill
+#endif
+#ifndef BIH_WH_STEPS
+#define BIH_WH_STEPS 4     // walk steps per lane between refill checks (A/B: 1 1.792 s, 2 1.777, 4 1.755 per 4K frame)
+#endif
 struct WRay {
     float o[3], d[3], ix, iy, iz, tMin, tMax, bt;
     uint32_t sg, cur, sp, bi, sid;
@@ -461,7 +467,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
     bool more = true;          // (wave-uniform) the queue may still hold rays
     for (;;) {
         const unsigned long long idle = __ballot(!has);
-        if (more && (__popcll(idle) >= kWT / 4 || idle == ~0ull)) {
+        if (more && (__popcll(idle) >= BIH_WH_REFILL || idle == ~0ull)) {
             const uint32_t k = (uint32_t)__popcll(idle);
             uint32_t first = 0;
             if (lane == 0) first = atomicAdd(fetch, k);
@@ -486,7 +492,8 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
             continue;
         }
         bool fin = false;
-        if (has) fin = wray_step(sc, r, t_lo, stk);
+        if (has)
+            for (int k = 0; k < BIH_WH_STEPS && !fin; ++k) fin = wray_step(sc, r, t_lo, stk);
         const bool hit = fin && r.bi != kNoHit;
         if (hit) hits[r.sid] = (uint8_t)(depth + 1);
         // the mirror ray (oracle whitted_path), then compaction into qout
