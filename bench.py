@@ -286,6 +286,39 @@ def main():
                              f"({Q} x slowest share ms); excludes the gather to rank 0 "
                              f"({H * W * 4 * (Q - 1) // Q / 1e6:.1f} MB over xGMI per frame)"}
 
+    # config C2 (BASELINE.json configs[1]): a ~70k-triangle mesh at 1920x1080.
+    # The Stanford bunny is not available offline; the stand-in is the
+    # closed 69,432-triangle torus (bihrt.scenes.torus), same camera, same
+    # frame sequence and calls as the headline
+    c2_leg = None
+    if world == 1 and not args.headline_only:
+        tt = bihrt.scenes.torus()
+        d_tt = torch.from_numpy(tt).to(f"cuda:{local}")
+        a2 = bihrt.GPUArrayManager.from_device(d_tt.data_ptr(), tt.shape[0], device=local, stream=sptr)
+        r2 = bihrt.Renderer(a2, W, H, spp=SPP, seed=1984, camera=cam)
+        rows2 = band_rows(H, args.band, 0, 1)
+
+        def c2_call(k, f0, m):
+            s2 = streams[k % F]
+            r2.render_device_frames(outs[k % F].data_ptr(), f0, m, H * W, rows=rows2, stream=s2.cuda_stream)
+
+        for k in range(0, args.warmup, G):
+            c2_call(k // G, k, min(G, args.warmup - k))
+        sync_all()
+        k0 = ((args.warmup + G - 1) // G) * G
+        t0 = time.perf_counter()
+        for k in range(0, args.steps, G):
+            c2_call((k0 + k) // G, k0 + k, min(G, args.steps - k))
+        sync_all()
+        el2 = time.perf_counter() - t0
+        c2_leg = {"config": "C2 stand-in: 69,432-triangle closed torus (bunny unavailable offline), 1920x1080, "
+                            "4 spp, any-hit, frames per call as the headline",
+                  "tris": int(tt.shape[0]), "value": rays_per_frame * args.steps / el2, "unit": "rays/s",
+                  "ms_per_step": 1e3 * el2 / args.steps,
+                  "note": "parity: tests/test_gpu_parity.py::test_c2_torus_1080p (oracle rows, exact walk)"}
+        a2.close()
+        del d_tt
+
     # config C4 (BASELINE.json configs[3]): 8-bounce Whitted mirror rays at
     # 3840x2160 on the same soup and tree (bih_render_whitted_device)
     whitted_leg = None
@@ -522,6 +555,7 @@ def main():
             "other_decomposition": side_leg,
             "band_share": share_leg,
             "whitted_c4": whitted_leg,
+            "c2_torus": c2_leg,
         }
         if parity_rows is not None:
             res["parity_sample_rows_equal"] = parity_rows

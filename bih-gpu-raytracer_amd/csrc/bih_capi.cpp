@@ -689,7 +689,9 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
                  s_pbase = al((size_t)nblk * 4);
     // pair results (k_bin_count -> k_bin_fill): 4 B per (triangle, tile)
     // pair; blocks past the buffer recompute in the fill
-    const uint32_t pres_cap = (uint32_t)std::min<uint64_t>(4ull * n + (1u << 20), 0x3FFFFFFFull);
+    uint32_t pres_cap = (uint32_t)std::min<uint64_t>(4ull * n + (1u << 20), 0x3FFFFFFFull);
+    if (const char *v = getenv("BIH_PAIR_CAP"))   // tests: blocks past a small buffer recompute
+        pres_cap = std::min<uint32_t>(pres_cap, (uint32_t)strtoul(v, nullptr, 10));
     const size_t s_pres = al((size_t)pres_cap * 4);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
                         s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt + s_pbase + s_pres;

@@ -441,6 +441,43 @@ def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
         assert np.array_equal(a, ref[f]), (scene, "in flight", f, int((a != ref[f]).sum()))
 
 
+@pytest.mark.parametrize("cap", ["0", "5000"])
+def test_pair_results_past_buffer_recompute(cap, gpu, bihrt_mod, monkeypatch):
+    """k_bin_fill takes each (triangle, tile) pair's class, pixel mask and
+    bucket from k_bin_count's pair buffer; count blocks past the buffer
+    (BIH_PAIR_CAP caps it: 0 = every block, 5000 = most) leave them to be
+    computed again by the fill.  Every frame equals the reference walk's."""
+    tris = bihrt_mod.scenes.soup(200_000, seed=11)
+    monkeypatch.setenv("BIH_PAIR_CAP", cap)
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 480, 270
+    for f in (0, 2):
+        a = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_ANYHIT)
+        b = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_REFERENCE)
+        assert np.array_equal(a, b), (cap, f, int((a != b).sum()))
+    assert g.bins_stats().usable
+
+
+def test_c2_torus_1080p(gpu, bihrt_mod, oracle_mod):
+    """Config C2's size with its stand-in mesh (the 69,432-triangle torus;
+    the Stanford bunny is not available offline): 1920x1080 x 4 spp, the
+    any-hit render (frustum bins) equals the reference walk on two frames and
+    the oracle on every 16th row of frame 0."""
+    tris = bihrt_mod.scenes.torus()
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 1920, 1080
+    imgs = []
+    for f in (0, 1):
+        a = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_ANYHIT)
+        b = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_REFERENCE)
+        assert np.array_equal(a, b), (f, int((a != b).sum()))
+        imgs.append(a)
+    assert g.bins_stats().usable
+    ref, _ = oracle_mod.OracleTree(tris).render(w, h, rows=(0, (h + 15) // 16, 16))
+    assert np.array_equal(imgs[0][::16], ref)
+    assert (imgs[0] != imgs[0][0, 0]).any()   # the torus is in view
+
+
 def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod, oracle_mod):
     """Config C5's scene and size on one GPU (10M-triangle soup, 3840x2160,
     4 spp): the any-hit shortcut and the exact walk agree on every pixel of
