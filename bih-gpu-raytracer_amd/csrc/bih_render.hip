@@ -1817,7 +1817,7 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 #endif
 constexpr uint32_t kFbWords = 8;   // fallback record: tile, undecided lo/hi, hits lo/hi, pad
 #ifndef BIH_BIN_BATCH
-#define BIH_BIN_BATCH 16
+#define BIH_BIN_BATCH 8   // A/B (16 frames per call): 8 0.0464 ms per frame, 16 0.0471, 32 0.0482
 #endif
 #ifndef BIH_PHASES
 #define BIH_PHASES BIH_FAST_COUNTERS   // per-phase wave cycles (bih_sync prints them)

@@ -478,6 +478,33 @@ def test_c2_torus_1080p(gpu, bihrt_mod, oracle_mod):
     assert (imgs[0] != imgs[0][0, 0]).any()   # the torus is in view
 
 
+def test_bins_list_total_past_u32_renders_without_bins(gpu, bihrt_mod):
+    """33,500 front-facing triangles that each cover the whole 1080p image:
+    the frustum-bin lists would hold 33,500 x 129,600 > 2^32 entries.  The
+    64-bit list total (k_bin_count) makes the camera render without bins (the
+    BIH walk with its proven shortcuts) instead of wrapping the u32 offsets;
+    rows rendered that way equal the reference walk's."""
+    from bihrt.tiling import band_rows
+    w, h = 1920, 1080
+    cam = np.array(bihrt_mod.camera_reference(w, h).as_list(), np.float32)
+    O, llc, hh, vv = cam[0:3], cam[3:6], cam[6:9], cam[9:12]
+    n = 33_500
+    d = (1.2 + 1e-5 * np.arange(n, dtype=np.float64))[:, None]
+
+    def P(u, v):
+        return O[None, :] + d * ((llc + u * hh + v * vv) - O)[None, :]
+
+    tris = np.concatenate([P(-20, -20), P(-20, 40), P(40, -20)], 1).astype(np.float32)   # front-facing
+    g = bihrt_mod.GPUArrayManager(tris)
+    rows = band_rows(h, 4, 67, 270)          # rows 268..271
+    a = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_ANYHIT, rows=rows)
+    st = g.bins_stats()
+    assert not st.usable, (st.usable, st.list_entries)
+    b = _device_render(bihrt_mod, g, w, h, 4, 0, bihrt_mod.TRAVERSE_REFERENCE, rows=rows)
+    assert np.array_equal(a, b)
+    assert (a == 0x00FFFF).all()             # every sample hits
+
+
 def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod, oracle_mod):
     """Config C5's scene and size on one GPU (10M-triangle soup, 3840x2160,
     4 spp): the any-hit shortcut and the exact walk agree on every pixel of
