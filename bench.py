@@ -16,8 +16,12 @@ region (its device time is reported as build_ms; the reference rebuilds it
 every frame, Renderer.cpp:415-503 -- the "with_rebuild" leg times that).
 
 Single process:   python bench.py
-Multi-GPU:        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
-Rank 0 prints one JSON line.
+Multi-GPU:        python bench.py --gpus N        (starts the N ranks itself), or
+                  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Rank 0 prints one JSON line.  Every per-call device buffer is sized before the
+timed region (bih_reserve) and the warm-up issues every call size the timed
+loop issues; the line reports the allocations the headline made
+(device_allocs_in_headline, expected 0).
 """
 from __future__ import annotations
 
@@ -39,7 +43,11 @@ FB_B, RNG_B = 4, 48
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one rank each).  Without a launcher (no WORLD_SIZE in the "
+                         "environment) N > 1 starts the N ranks itself (torch.distributed.run, before this "
+                         "process touches the GPU) and relays rank 0's line; under a launcher it must equal "
+                         "WORLD_SIZE.  Default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--tris", type=int, default=1_000_000)
@@ -74,6 +82,8 @@ def parse():
                     help="rows timed single-threaded with the reference's host debug rules "
                          "(CPUTraverseTree visits ~40k nodes per ray at 1M triangles: one row)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--parity-row-step", type=int, default=16,
+                    help="rows of frames 7 and 15 of the timed call shape checked against the oracle")
     ap.add_argument("--traffic", type=int, default=1,
                     help="N=1: measure HBM traffic per launch with rocprofv3 PMC passes "
                          "(child processes, before this process touches the GPU)")
@@ -83,20 +93,208 @@ def parse():
                     help="record torch events around every timed render (kernel_ms per leg)")
     ap.add_argument("--whitted-frames", type=int, default=3,
                     help="N=1: frames of config C4 (8-bounce Whitted, 3840x2160, same soup) to time; 0 = skip")
+    ap.add_argument("--c5", type=int, default=1,
+                    help="config C5 leg: 10M-triangle soup at 3840x2160 with the headline's call shape "
+                         "and decomposition (row bands + gather at N > 1); 0 = skip")
+    ap.add_argument("--c5-tris", type=int, default=10_000_000)
     ap.add_argument("--no-reference-leg", action="store_true")
     ap.add_argument("--no-rebuild-leg", action="store_true",
                     help="skip the leg that rebuilds the BIH every frame (as the reference does)")
     ap.add_argument("--headline-only", action="store_true",
                     help="time the headline leg only (no side legs), e.g. under rocprofv3 so that "
                          "its kernel average is the headline's launches")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher test: ranks join a gloo group, check the world size and rank 0 prints "
+                         "a JSON line; no GPU work")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start the N ranks as child
+    processes (torch.distributed.run on 127.0.0.1, one process per GPU) before
+    this process makes any GPU call; rank 0's JSON line goes to our stdout.
+    Non-zero exit if fewer than N devices are visible or a rank fails."""
+    import socket
+    import subprocess
+    if not args.stub and os.environ.get("BIH_BENCH_SHARE_GPU") != "1":
+        import torch
+        n = torch.cuda.device_count()      # counts devices without initialising them
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {n} devices are visible", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.run(cmd, env=env)
+    if p.returncode != 0:
+        print(f"bench.py: {args.gpus}-rank run failed (exit {p.returncode})", file=sys.stderr)
+    return p.returncode
+
+
+def stub_worker(args, rank, world):
+    """The launcher's test worker: the group forms over gloo with the world
+    size asked for; rank 0 prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"stub": True, "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                          "rank_sum": t.item()}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def call_sizes(n, g):
+    """Frames per call when n frames are issued in calls of g (the last one takes the rest)."""
+    return [min(g, n - k) for k in range(0, n, g)]
+
+
+class Workload:
+    """One scene and image on this rank: the tree, the renderer, one output
+    buffer per stream in flight, and (strong decomposition at N > 1) one band
+    gather per stream and call size.  Every per-call device buffer is sized
+    before any timing (bih_reserve, gathers pre-built for every call size)."""
+
+    def __init__(self, C, tris, W, H, cam=None, shapes=(1,)):
+        self.C, self.W, self.H = C, W, H
+        torch, bihrt, a = C.torch, C.bihrt, C.args
+        self.tris = tris
+        self.d_tris = torch.from_numpy(tris).to(f"cuda:{C.local}")
+        self.arrays = bihrt.GPUArrayManager.from_device(self.d_tris.data_ptr(), tris.shape[0], device=C.local,
+                                                        stream=C.sptr)
+        self.info = self.arrays.info()
+        self.cam = cam if cam is not None else bihrt.camera_reference(W, H)
+        self.r = bihrt.Renderer(self.arrays, W, H, spp=a.spp, seed=1984, camera=self.cam)
+        self.mrows = C.tiling.max_rows(H, a.band, C.world)
+        G = C.G
+        self.outs = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") for _ in range(C.F)]
+        self.gathers, self.frame_img = {}, None
+        if C.world > 1:
+            packed = bool(a.gather_packed) and a.spp == 4 and W % 8 == 0
+            for j in range(C.F):
+                for m in sorted(set(shapes)):
+                    self.gathers[(j, m)] = C.tiling.BandGather(C.dist, H, W, a.band, C.rank, C.world,
+                                                               torch.device("cuda", C.local), frames=m,
+                                                               packed=packed)
+            self.frame_img = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") if C.rank == 0 else None
+                              for _ in range(C.F)]
+        # every per-call buffer of both decompositions' call shapes, up front
+        rows_all = C.tiling.band_rows(H, a.band, 0, 1)
+        self.arrays.reserve(W, H, a.spp, rows_all, G)
+        if C.world > 1:
+            self.arrays.reserve(W, H, a.spp, C.tiling.band_rows(H, a.band, C.rank, C.world), G)
+        torch.cuda.synchronize()
+
+    def plan(self, mode, g):
+        """(rows of this rank, frame of step k from `base`, frames per step job-wide)"""
+        C, a = self.C, self.C.args
+        if mode == "weak" or C.world == 1:
+            return (C.tiling.band_rows(self.H, a.band, 0, 1),
+                    (lambda base, k: C.tiling.frame_of_step(base, k, C.rank, C.world, g)), C.world)
+        return C.tiling.band_rows(self.H, a.band, C.rank, C.world), (lambda base, k: base + k), 1
+
+    def step(self, mode, rows, c, frame, traverse, ev=None, rebuild=False, nf=None, m=1):
+        """One render call (call index c): frames frame .. frame+m-1."""
+        C = self.C
+        nf = nf or C.F
+        j = c % nf
+        s = C.streams[j]
+        o = self.outs[j].data_ptr()
+        strong = mode == "strong" and C.world > 1
+        # frames of a call packed at the rank's padded rows (the gather sends them as one block)
+        stride = (self.mrows if strong else self.H) * self.W
+        r = self.r
+
+        def render():
+            if m == 1:
+                r.render_device(o, frame, rows=rows, traverse=traverse, stream=s.cuda_stream)
+            elif traverse == C.bihrt.TRAVERSE_ANYHIT:
+                r.render_device_frames(o, frame, m, stride, rows=rows, stream=s.cuda_stream)
+            else:
+                for f in range(m):
+                    r.render_device(o + 4 * f * stride, frame + f, rows=rows, traverse=traverse,
+                                    stream=s.cuda_stream)
+
+        if ev is None and not rebuild and not strong:
+            render()     # the render alone: no torch work on the stream, no stream context
+            return
+        with C.torch.cuda.stream(s):
+            if rebuild:
+                self.arrays.rebuild()
+            if ev is not None:
+                ev[0].record(s)
+            render()
+            if ev is not None:
+                ev[1].record(s)
+            if strong:
+                # call c's gather runs on stream j while call c+1 renders on j+1
+                self.gathers[(j, m)](self.outs[j], self.frame_img[j])
+
+    def timed(self, mode, traverse, base, rebuild=False, nf=None, g=None, rows=None, steps=None):
+        """Times exactly `steps` frames per rank (args.steps), in calls of g
+        frames (the last call takes the rest).  Untimed first: args.warmup
+        frames in calls of g, then one call of every timed call size the
+        warm-up did not issue.  Frames run on without a gap from the warm-up
+        into the timed calls.  Returns (max-over-ranks seconds, kernel ms per
+        frame or None, frames per step job-wide)."""
+        C, a = self.C, self.C.args
+        g = g or C.G
+        steps = steps or a.steps
+        rows_p, frame_of, fps = self.plan(mode, g)
+        rows = rows or rows_p
+        calls = call_sizes(steps, g)
+        warm = call_sizes(a.warmup, g)
+        warm += [m for m in sorted(set(calls)) if m not in warm]
+        k = c = 0
+        for m in warm:
+            self.step(mode, rows, c, frame_of(base, k), traverse, rebuild=rebuild, nf=nf, m=m)
+            k, c = k + m, c + 1
+        C.sync_all()
+        # per-call torch events only when asked (--step-events): recording them
+        # costs host time per call, which the row-band shares feel
+        evs = [(C.torch.cuda.Event(enable_timing=True), C.torch.cuda.Event(enable_timing=True))
+               for _ in calls] if a.step_events else []
+        t0 = time.perf_counter()
+        for i, m in enumerate(calls):
+            self.step(mode, rows, c, frame_of(base, k), traverse, evs[i] if evs else None, rebuild=rebuild,
+                      nf=nf, m=m)
+            k, c = k + m, c + 1
+        C.sync_all()
+        el = C.max_over_ranks(time.perf_counter() - t0)
+        kms = [x.elapsed_time(y) / m for (x, y), m in zip(evs, calls)] if evs else []
+        return el, (sum(kms) / len(kms) if kms else None), fps
+
+    def close(self):
+        self.arrays.close()
+        del self.d_tris
+
+
+class Ctx:
+    pass
 
 
 def main():
     args = parse()
+    if args.gpus and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.stub:
+        stub_worker(args, rank, world)
+        return
     import numpy as np
     import torch
 
@@ -112,91 +310,33 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         if shared:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = dist.get_backend()
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     import bihrt
-    from bihrt.tiling import BandGather, band_rows, frame_of_step, max_rows
+    from bihrt import tiling
 
+    C = Ctx()
+    C.args, C.rank, C.world, C.local, C.dist, C.torch, C.bihrt, C.tiling = (args, rank, world, local, dist,
+                                                                             torch, bihrt, tiling)
     W, H, SPP = args.width, args.height, args.spp
-    # explicit streams: the build and untimed work on streams[0]; frame k of a
+    # explicit streams: the build and untimed work on streams[0]; call k of a
     # timed leg on streams[k % in_flight] with its own output buffers, so that
-    # consecutive frames overlap (libbih_amd orders what they share)
-    F = max(1, args.in_flight)
-    streams = [torch.cuda.Stream() for _ in range(F)]
+    # consecutive calls overlap (libbih_amd orders what they share)
+    C.F = F = max(1, args.in_flight)
+    C.G = G = max(1, args.group)
+    C.streams = streams = [torch.cuda.Stream() for _ in range(F)]
     stream = streams[0]
     torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-
-    # scene: generated on the host (deterministic), resident in HBM before timing
-    tris = bihrt.scenes.soup(args.tris, seed=1)
-    d_tris = torch.from_numpy(tris).to(f"cuda:{local}")
-    arrays = bihrt.GPUArrayManager.from_device(d_tris.data_ptr(), tris.shape[0], device=local,
-                                               stream=sptr)
-    info = arrays.info()
-    cam = bihrt.camera_reference(W, H)
-    r = bihrt.Renderer(arrays, W, H, spp=SPP, seed=1984, camera=cam)
-    # weak: this rank renders whole frames; strong: its bands of every frame.
-    # A render call covers G consecutive frames (--group, bih_render_device_frames):
-    # frame f of a call at out + f * stride, stride = the rank's padded rows.
-    G = max(1, args.group)
-    mrows = max_rows(H, args.band, world)
-    outs = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") for _ in range(F)]
-    out = outs[0]
-    if world > 1:
-        # one gather (and receive buffer on rank 0) per call in flight; a call's
-        # G frames travel as one message
-        packed = bool(args.gather_packed) and SPP == 4 and W % 8 == 0
-        gathers = [BandGather(dist, H, W, args.band, rank, world, torch.device("cuda", local), frames=G,
-                              packed=packed)
-                   for _ in range(F)]
-        frame_img = [torch.zeros(G * H * W, dtype=torch.int32, device="cuda") if rank == 0 else None
-                     for _ in range(F)]
-    trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
-
-    def plan(mode, g=G):
-        """(rows of this rank, first frame of the call at step k from `base`, frames per step job-wide)"""
-        if mode == "weak" or world == 1:
-            return (band_rows(H, args.band, 0, 1),
-                    (lambda base, k: frame_of_step(base, k, rank, world, g)), world)
-        return band_rows(H, args.band, rank, world), (lambda base, k: base + k), 1
-
-    def step(mode, rows, k, frame, traverse, ev=None, rebuild=False, nf=F, m=1):
-        """One render call: frames frame .. frame+m-1 (call index k)."""
-        j = k % nf
-        s = streams[j]
-        o = outs[j].data_ptr()
-        # frames of a call packed at the rank's padded rows (the gather sends them as one block)
-        stride = (mrows if (mode == "strong" and world > 1) else H) * W
-
-        def render():
-            if m == 1:
-                r.render_device(o, frame, rows=rows, traverse=traverse, stream=s.cuda_stream)
-            elif traverse == bihrt.TRAVERSE_ANYHIT:
-                r.render_device_frames(o, frame, m, stride, rows=rows, stream=s.cuda_stream)
-            else:
-                for f in range(m):
-                    r.render_device(o + 4 * f * stride, frame + f, rows=rows, traverse=traverse,
-                                    stream=s.cuda_stream)
-
-        if ev is None and not rebuild and not (mode == "strong" and world > 1):
-            render()     # the render alone: no torch work on the stream, no stream context
-            return
-        with torch.cuda.stream(s):
-            if rebuild:
-                arrays.rebuild()
-            if ev is not None:
-                ev[0].record(s)
-            render()
-            if ev is not None:
-                ev[1].record(s)
-            if mode == "strong" and world > 1:
-                # call k's gather runs on stream j while call k+1 renders on j+1
-                gathers[j](outs[j], frame_img[j])
+    C.sptr = sptr = stream.cuda_stream
 
     def sync_all():
         if dist is not None:
@@ -209,41 +349,33 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def timed(mode, traverse, base, rebuild=False, nf=F, g=G):
-        """Times exactly args.steps frames per rank (calls of g frames; the
-        last call takes the remainder)."""
-        rows, frame_of, fps = plan(mode, g)
-        for k in range(0, args.warmup, g):
-            step(mode, rows, k // g, frame_of(base, k), traverse, rebuild=rebuild, nf=nf,
-                 m=min(g, args.warmup - k))
-        sync_all()
-        # per-call torch events only when asked (--step-events): recording them
-        # costs host time per call, which the row-band shares feel
-        ncalls = (args.steps + g - 1) // g
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(ncalls)] if args.step_events else []
-        k0 = ((args.warmup + g - 1) // g) * g
-        t0 = time.perf_counter()
-        for c, k in enumerate(range(0, args.steps, g)):
-            step(mode, rows, (k0 + k) // g, frame_of(base, k0 + k), traverse,
-                 evs[c] if evs else None, rebuild=rebuild, nf=nf, m=min(g, args.steps - k))
-        sync_all()
-        el = max_over_ranks(time.perf_counter() - t0)
-        kms = [a.elapsed_time(b) / g for a, b in evs] if evs else []
-        return el, (sum(kms) / len(kms) if kms else None), fps
+    C.sync_all, C.max_over_ranks = sync_all, max_over_ranks
+    # every call size a leg issues (gathers are built for each up front)
+    shapes = set(call_sizes(args.steps, G)) | set(call_sizes(args.warmup, G)) | {1, G}
+
+    # scene: generated on the host (deterministic), resident in HBM before timing
+    tris = bihrt.scenes.soup(args.tris, seed=1)
+    wl = Workload(C, tris, W, H, shapes=shapes)
+    r, arrays, info, cam = wl.r, wl.arrays, wl.info, wl.cam
+    out = wl.outs[0]
+    trav = bihrt.TRAVERSE_ANYHIT if args.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
 
     mode = args.mode if world > 1 else "weak"
-    rows, frame_of, _ = plan(mode)
+    rows, frame_of, _ = wl.plan(mode, G)
     rays_per_frame = W * H * SPP
-    elapsed, kernel_ms, fps = timed(mode, trav, 0)
+    allocs0 = arrays.info().device_allocs
+    elapsed, kernel_ms, fps = wl.timed(mode, trav, 0)
     value = fps * rays_per_frame * args.steps / elapsed
+    # the headline's own warm-up may build per-camera structures; its timed
+    # calls must not allocate (bih_reserve sized every per-call buffer)
+    allocs_headline = arrays.info().device_allocs - allocs0
 
     if args.headline_only:
         args.no_reference_leg = args.no_rebuild_leg = True
     ref_leg = None
     if not args.no_reference_leg:
         other = bihrt.TRAVERSE_REFERENCE if trav == bihrt.TRAVERSE_ANYHIT else bihrt.TRAVERSE_ANYHIT
-        el2, kms2, fps2 = timed(mode, other, 1000)
+        el2, kms2, fps2 = wl.timed(mode, other, 1000)
         ref_leg = {"traverse": "reference" if other == bihrt.TRAVERSE_REFERENCE else "anyhit",
                    "value": fps2 * rays_per_frame * args.steps / el2,
                    "ms_per_step": 1e3 * el2 / args.steps,
@@ -252,39 +384,37 @@ def main():
     # one frame at a time (frame latency): informational when frames overlap
     serial_leg = None
     if F > 1 and not args.headline_only:
-        el5, kms5, fps5 = timed(mode, trav, 4000, nf=1)
+        el5, kms5, fps5 = wl.timed(mode, trav, 4000, nf=1, g=1)
         serial_leg = {"value": fps5 * rays_per_frame * args.steps / el5, "unit": "rays/s",
                       "ms_per_step": 1e3 * el5 / args.steps, "kernel_ms": kms5,
-                      "note": "in_flight 1: each frame starts after the previous one ends"}
+                      "note": "in_flight 1, one frame per call: each frame starts after the previous one ends"}
 
     # N = 1: the strong decomposition's per-rank work at --share-world GPUs.
     # Rank q of Q renders the interleaved bands band_rows(H, B, q, Q) of every
-    # frame; each share is timed alone here (same in-flight pipelining as the
-    # headline).  Projected per-GPU efficiency = full-frame ms / (Q x slowest
-    # share ms): what the row tiling costs per GPU before the gather.
+    # frame; each share is timed alone here, with the same call shape and
+    # pipelining as the full frame it is compared with (measured again right
+    # before the shares, so both see the same box state).  Projected per-GPU
+    # efficiency = full-frame ms / (Q x slowest share ms): what the row tiling
+    # costs per GPU before the gather.
     share_leg = None
     Q = args.share_world
     if world == 1 and Q > 1 and not args.headline_only:
-        full_ms = 1e3 * elapsed / args.steps
+        for q in range(Q):
+            arrays.reserve(W, H, SPP, tiling.band_rows(H, args.band, q, Q), G)
+        elf, _, _ = wl.timed("weak", trav, 7000)
+        full_ms = 1e3 * elf / args.steps
         shares = []
         for q in range(Q):
-            rows_q = band_rows(H, args.band, q, Q)
-            for k in range(0, args.warmup, G):
-                step("weak", rows_q, k // G, 7000 + k, trav, m=min(G, args.warmup - k))
-            sync_all()
-            k0 = ((args.warmup + G - 1) // G) * G
-            t0 = time.perf_counter()
-            for k in range(0, args.steps, G):
-                step("weak", rows_q, (k0 + k) // G, 7000 + k0 + k, trav, m=min(G, args.steps - k))
-            sync_all()
-            shares.append(1e3 * (time.perf_counter() - t0) / args.steps)
+            els, _, _ = wl.timed("weak", trav, 8000 + 1000 * q, rows=tiling.band_rows(H, args.band, q, Q))
+            shares.append(1e3 * els / args.steps)
         share_leg = {"world": Q, "band": args.band, "share_ms_per_step": shares,
                      "full_frame_ms_per_step": full_ms,
                      "projected_efficiency": full_ms / (Q * max(shares)),
                      "note": f"each of the {Q} ranks' interleaved {args.band}-row bands rendered alone "
-                             "on this GPU, frames in flight as the headline; efficiency = full ms / "
-                             f"({Q} x slowest share ms); excludes the gather to rank 0 "
-                             f"({H * W * 4 * (Q - 1) // Q / 1e6:.1f} MB over xGMI per frame)"}
+                             f"on this GPU, {G} frames per call and {F} calls in flight as the full frame "
+                             f"timed beside it; efficiency = full ms / ({Q} x slowest share ms); excludes "
+                             f"the gather to rank 0 ({H * W * 4 * (Q - 1) // Q / 1e6:.1f} MB over xGMI per "
+                             "frame, 8x less packed)"}
 
     # config C2 (BASELINE.json configs[1]): a ~70k-triangle mesh at 1920x1080.
     # The Stanford bunny is not available offline; the stand-in is the
@@ -292,68 +422,52 @@ def main():
     # frame sequence and calls as the headline
     c2_leg = None
     if world == 1 and not args.headline_only:
-        tt = bihrt.scenes.torus()
-        d_tt = torch.from_numpy(tt).to(f"cuda:{local}")
-        a2 = bihrt.GPUArrayManager.from_device(d_tt.data_ptr(), tt.shape[0], device=local, stream=sptr)
-        r2 = bihrt.Renderer(a2, W, H, spp=SPP, seed=1984, camera=cam)
-        rows2 = band_rows(H, args.band, 0, 1)
-
-        def c2_call(k, f0, m):
-            s2 = streams[k % F]
-            r2.render_device_frames(outs[k % F].data_ptr(), f0, m, H * W, rows=rows2, stream=s2.cuda_stream)
-
-        for k in range(0, args.warmup, G):
-            c2_call(k // G, k, min(G, args.warmup - k))
-        sync_all()
-        k0 = ((args.warmup + G - 1) // G) * G
-        t0 = time.perf_counter()
-        for k in range(0, args.steps, G):
-            c2_call((k0 + k) // G, k0 + k, min(G, args.steps - k))
-        sync_all()
-        el2 = time.perf_counter() - t0
+        w2 = Workload(C, bihrt.scenes.torus(), W, H, cam=cam, shapes=shapes)
+        el2, _, _ = w2.timed("weak", bihrt.TRAVERSE_ANYHIT, 0)
         c2_leg = {"config": "C2 stand-in: 69,432-triangle closed torus (bunny unavailable offline), 1920x1080, "
-                            "4 spp, any-hit, frames per call as the headline",
-                  "tris": int(tt.shape[0]), "value": rays_per_frame * args.steps / el2, "unit": "rays/s",
+                            "4 spp, any-hit, call shape as the headline",
+                  "tris": int(w2.tris.shape[0]), "value": rays_per_frame * args.steps / el2, "unit": "rays/s",
                   "ms_per_step": 1e3 * el2 / args.steps,
                   "note": "parity: tests/test_gpu_parity.py::test_c2_torus_1080p (oracle rows, exact walk)"}
-        a2.close()
-        del d_tt
+        w2.close()
+        del w2
+
+    # config C5 (BASELINE.json configs[4]): the 10M-triangle soup at
+    # 3840x2160 with the headline's call shape; at N > 1 the headline's
+    # decomposition (row bands of every frame + one gather to rank 0 per call)
+    c5_leg = None
+    if args.c5 and not args.headline_only:
+        t5 = bihrt.scenes.soup(args.c5_tris, seed=1)
+        W5, H5 = 3840, 2160
+        w5 = Workload(C, t5, W5, H5, shapes=shapes)
+        el5, _, fps5 = w5.timed(mode, bihrt.TRAVERSE_ANYHIT, 0)
+        w5.arrays.rebuild()
+        torch.cuda.synchronize()
+        b5 = w5.arrays.info().build_ms
+        st5 = w5.arrays.bins_stats()
+        c5_leg = {"config": f"C5: {args.c5_tris}-triangle soup (splitmix64 seed 1), {W5}x{H5}, {SPP} spp, "
+                            "any-hit, call shape as the headline",
+                  "tris": int(t5.shape[0]), "value": fps5 * W5 * H5 * SPP * args.steps / el5, "unit": "rays/s",
+                  "ms_per_step": 1e3 * el5 / args.steps, "n_gpus": world, "scaling": mode,
+                  "parallelism": parallelism(mode, args.band, world),
+                  "build_ms": w5.info.build_ms, "rebuild_ms": b5,
+                  "bins": {"usable": bool(st5.usable), "list_entries": int(st5.list_entries)},
+                  "note": "parity: tests/test_gpu_parity.py::test_10m_4k_* (oracle rows, exact walk)"}
+        w5.close()
+        del w5, t5
+        torch.cuda.synchronize()
 
     # config C4 (BASELINE.json configs[3]): 8-bounce Whitted mirror rays at
     # 3840x2160 on the same soup and tree (bih_render_whitted_device)
     whitted_leg = None
     if world == 1 and args.whitted_frames > 0 and not args.headline_only:
-        WW, WH = 3840, 2160
-        rw = bihrt.Renderer(arrays, WW, WH, spp=SPP, seed=1984)
-        wout = torch.zeros(WW * WH, dtype=torch.int32, device="cuda")
-        whits = torch.zeros(WW * WH * SPP, dtype=torch.int32, device="cuda")
-        rw.render_whitted_device(wout.data_ptr(), 0, hits_ptr=whits.data_ptr(), stream=sptr)
-        torch.cuda.synchronize()
-        traced = int(torch.clamp(whits.to(torch.int64) + 1, max=9).sum())
-        hist = torch.bincount(whits.view(-1), minlength=10).tolist()
-        del whits
-        rw.set_timing(True)
-        t0 = time.perf_counter()
-        for k in range(args.whitted_frames):
-            rw.render_whitted_device(wout.data_ptr(), 1 + k, stream=sptr)
-        torch.cuda.synchronize()
-        wel = (time.perf_counter() - t0) / args.whitted_frames
-        wk, _ = rw.last_render_times()
-        rw.set_timing(False)
-        whitted_leg = {"config": "C4: 1M soup, 3840x2160, 4 spp, 8 bounces of mirror rays",
-                       "ms_per_frame": 1e3 * wel, "primary_rays_per_s": WW * WH * SPP / wel,
-                       "rays_traced_per_frame": traced, "rays_traced_per_s": traced / wel,
-                       "trace_kernels_ms": wk, "hit_histogram": hist, "frames": args.whitted_frames,
-                       "note": "k_wh_gen + 9 x k_wh_trace (closest hit, per-lane walk, ballot/mbcnt "
-                               "compaction of live rays between bounces) + k_wh_shade; bit-exact vs the "
-                               "oracle (tests/test_whitted.py)"}
-        del wout
+        whitted_leg = whitted(args, bihrt, torch, arrays, SPP, sptr)
 
     # N > 1: the other decomposition, informational
     side_leg = None
     if world > 1 and not args.headline_only:
         other_mode = "strong" if mode == "weak" else "weak"
-        el4, kms4, fps4 = timed(other_mode, trav, 3000)
+        el4, kms4, fps4 = wl.timed(other_mode, trav, 3000)
         side_leg = {"mode": other_mode,
                     "scaling": other_mode,
                     "value": fps4 * rays_per_frame * args.steps / el4, "unit": "rays/s",
@@ -361,7 +475,7 @@ def main():
                     "parallelism": parallelism(other_mode, args.band, world)}
 
     # a camera that moves every frame: the per-camera structures (primary-ray
-    # records, frustum bins, tile queue) are rebuilt inside every step
+    # records, frustum bins and tile queue) are rebuilt inside every step
     moving_leg = None
     if not args.no_rebuild_leg:
         from bihrt import Camera
@@ -374,15 +488,16 @@ def main():
                 c[j] += d[j]
                 c[3 + j] += d[j]
             cams.append(Camera.from_list(c))
-        rows_m, frame_of_m, fps_m = plan(mode)
-        for k in range(args.warmup):
+        rows_m, frame_of_m, fps_m = wl.plan(mode, 1)
+        for k in range(max(args.warmup, len(cams))):
             r.camera = cams[k % len(cams)]
-            step(mode, rows_m, k, frame_of_m(6000, k), trav)
+            wl.step(mode, rows_m, k, frame_of_m(6000, k), trav)
+        k0 = max(args.warmup, len(cams))
         sync_all()
         t0 = time.perf_counter()
-        for k in range(args.steps):
-            r.camera = cams[(args.warmup + k) % len(cams)]
-            step(mode, rows_m, args.warmup + k, frame_of_m(6000, args.warmup + k), trav)
+        for k in range(k0, k0 + args.steps):
+            r.camera = cams[k % len(cams)]
+            wl.step(mode, rows_m, k, frame_of_m(6000, k), trav)
         sync_all()
         el6 = max_over_ranks(time.perf_counter() - t0)
         r.camera = cam
@@ -395,7 +510,7 @@ def main():
     # Renderer.cpp:415-503): time rebuild + render per step as well
     rebuild_leg = None
     if not args.no_rebuild_leg:
-        el3, _, fps3 = timed(mode, trav, 2000, rebuild=True, g=1)
+        el3, _, fps3 = wl.timed(mode, trav, 2000, rebuild=True, g=1)
         rebuild_leg = {"value": fps3 * rays_per_frame * args.steps / el3, "unit": "rays/s",
                        "ms_per_step": 1e3 * el3 / args.steps,
                        "build_ms": arrays.info().build_ms,
@@ -404,13 +519,13 @@ def main():
 
     # the dominant kernel's launch duration: HIP events the library records
     # on the render stream right around the render kernel (bih_last_render_ms),
-    # over isolated launches (each frame synchronised before the next) -- the
+    # over isolated launches (each call synchronised before the next) -- the
     # figure rocprofv3's kernel trace reports for the same kernel
     # (the headline's launches: a call of G frames, one k_render_bins launch)
     kms_iso, tails_iso = [], []
     r.set_timing(True)
     for k in range(args.kernel_samples):
-        step(mode, rows, k, frame_of(5000, k * G), trav, nf=1, m=G)
+        wl.step(mode, rows, k, frame_of(5000, k * G), trav, nf=1, m=G)
         torch.cuda.synchronize()
         km, tm = r.last_render_times()
         kms_iso.append(km)
@@ -427,6 +542,7 @@ def main():
                     stream=sptr)
     torch.cuda.synchronize()
     sums = st.view(-1, 3).to(torch.int64).sum(0)
+    del st
     if dist is not None and mode == "strong":
         dist.all_reduce(sums)
     n_node, n_leaf, n_tri = [int(x) for x in sums.tolist()]
@@ -435,30 +551,38 @@ def main():
     launch_rays = rows.nrows * W * SPP * (G if trav == 0 else 1)   # rays of one headline launch
     # per-launch duration of the kernel: with frames in flight a launch's
     # events also count the time it queues behind the other stream's frame,
-    # so the isolated launches of the one-in-flight leg give the duration
-    # (what rocprofv3 reports for `--headline-only --in-flight 1`)
+    # so the isolated launches give the duration (what rocprofv3 reports for
+    # `--headline-only --in-flight 1`)
     launch_ms = kernel_launch_ms if kernel_launch_ms else (serial_leg["kernel_ms"] if serial_leg else kernel_ms)
     work_gbs = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9
     achieved = traffic["bytes_per_launch"] / (launch_ms * 1e-3) / 1e9 if traffic else None
 
     bst = arrays.bins_stats()
-    # algorithmic bytes of one k_render_bins launch:
-    # every list entry of the frame read once (48 B: 3 edge functions + pixel
-    # mask), one 64-B intersector record per packet-level intersector call,
-    # the XORWOW state (20 B) and the framebuffer word (4 B) per pixel
+    # algorithmic bytes of one k_render_bins launch: every list entry of the
+    # frame read once per frame (48 B: 3 edge functions + pixel mask), one 64-B
+    # intersector record per packet-level intersector call, the XORWOW state
+    # (20 B) and the framebuffer word (4 B) per pixel; and the compulsory
+    # bytes of the same launch (what must cross HBM at least once when the
+    # list stays cached across the launch's frames: list + records + RNG in
+    # and out once, a framebuffer per frame)
     alg = None
     bc = (traffic or {}).get("bin_counters")
     if bc and trav == 0 and bst.usable and launch_ms:
         pix = rows.nrows * W
         gl = G if trav == 0 else 1       # frames per k_render_bins launch
         alg_bytes = gl * (48 * int(bst.list_entries) + 64 * bc["mt"] + 24 * pix)
+        comp_bytes = 48 * int(bst.list_entries) + 64 * bc["mt"] + 2 * 20 * pix + gl * 4 * pix
         alg = {"bytes_per_launch": alg_bytes, "frames_per_launch": gl,
                "terms": {"list_entries": int(bst.list_entries), "intersector_calls": bc["mt"],
                          "pixels": pix, "entries_pretested": bc["entries"], "live_lanes": bc["lanes"],
                          "live_packets": bc["packets"]},
                "formula": "frames per launch x (48 x list entries + 64 x intersector calls + "
                           "(20 + 4) x pixels), per-frame terms of one frame (tools/fast_counters.py)",
-               "gbs": alg_bytes / (launch_ms * 1e-3) / 1e9}
+               "gbs": alg_bytes / (launch_ms * 1e-3) / 1e9,
+               "compulsory_bytes_per_launch": comp_bytes,
+               "compulsory_formula": "48 x list entries + 64 x intersector calls + 2 x 20 x pixels "
+                                     "(XORWOW in, out) + frames per launch x 4 x pixels",
+               "compulsory_gbs": comp_bytes / (launch_ms * 1e-3) / 1e9}
     bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
             "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
             "entry_bytes": 48,
@@ -466,10 +590,16 @@ def main():
                     "triangles whose edge pre-test a sample of the tile can pass"}
 
     cpu = None
-    parity_rows = None
+    parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu, parity_rows = cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np)
+        cpu, parity = cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np)
 
+    rccl = None
+    if backend == "nccl":
+        try:
+            rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
+        except Exception:
+            rccl = None
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -493,21 +623,24 @@ def main():
                 "parallelism": parallelism(mode, args.band, world),
                 "frames_in_flight": F,
                 "frames_per_call": G,
+                "calls": call_sizes(args.steps, G),
+                "warmup_calls": call_sizes(args.warmup, G) + [m for m in sorted(set(call_sizes(args.steps, G)))
+                                                              if m not in call_sizes(args.warmup, G)],
             },
+            "world_size": world,
+            "backend": backend,
+            "rccl_version": rccl,
+            "device_allocs_in_headline": allocs_headline,
             "kernel_ms": kernel_ms,
             "build_ms": info.build_ms,
             # roofline of the dominant kernel: HBM is the only roofline this
-            # integer/f32 pointer-chasing path has (no MFMA work).  `achieved`
-            # is the bytes the launch moves across HBM/fabric (rocprofv3
-            # FETCH_SIZE x2 + WRITE_SIZE, separate PMC passes) over the
-            # launch duration; what limits the kernel is `limiter`, not HBM.
-            # The reference algorithm's work priced in SURVEY 8d bytes is
-            # `work_equivalent` (the any-hit shortcut skips most of it).
+            # integer/f32 path has (no MFMA work).  `achieved` = the launch's
+            # algorithmic bytes over its duration; `traffic` =
+            # the HBM bytes the PMC counters measured per launch (the list stays
+            # in cache across the launch's frames, so traffic is far below the
+            # algorithmic bytes); `frac_compulsory` prices the bytes that must
+            # cross HBM once per launch.  What limits the kernel is `limiter`.
             "roofline": {
-                # achieved = algorithmic bytes per launch / launch duration
-                # (DESIGN.md 4.4); traffic = the HBM bytes the PMC counters
-                # measured per launch (the list stays in cache across the
-                # launch's frames, so traffic is far below the algorithmic bytes)
                 "bound": "hbm", "achieved": alg["gbs"] if alg else achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (alg["gbs"] if alg else achieved) / HBM_PEAK_GBS
                         if (alg or achieved is not None) else None,
@@ -517,6 +650,7 @@ def main():
                                     if achieved is not None else "traffic not measured"),
                 "algorithmic": alg,
                 "frac_algorithmic": alg["gbs"] / HBM_PEAK_GBS if alg else None,
+                "frac_compulsory": alg["compulsory_gbs"] / HBM_PEAK_GBS if alg else None,
                 "achieved_measured": achieved,
                 "frac_measured": achieved / HBM_PEAK_GBS if achieved is not None else None,
                 "launch_ms": launch_ms,
@@ -526,7 +660,7 @@ def main():
                                      f"(bih_last_render_times), mean of {len(kms_iso)} isolated launches "
                                      f"of the headline's calls ({G if trav == 0 else 1} frames each)")
                                     if kernel_launch_ms else "headline leg",
-                "limiter": "scalar-unit issue and memory latency of the packet walk, not HBM "
+                "limiter": "instruction issue and memory latency of the list walk, not HBM "
                            "(DESIGN.md section 4: SQ counters)",
                 "kernel": (traffic or {}).get("kernel") or
                           ("k_render_bins (any-hit: frustum-bin list walk; k_render_fallback finishes "
@@ -556,13 +690,44 @@ def main():
             "band_share": share_leg,
             "whitted_c4": whitted_leg,
             "c2_torus": c2_leg,
+            "c5_10m_4k": c5_leg,
         }
-        if parity_rows is not None:
-            res["parity_sample_rows_equal"] = parity_rows
+        if parity is not None:
+            res["parity_timed_call_shape"] = parity
+            res["parity_sample_rows_equal"] = parity["all_equal"]
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def whitted(args, bihrt, torch, arrays, SPP, sptr):
+    """Config C4: frames of 8-bounce mirror rays at 3840x2160 on the bench soup."""
+    WW, WH = 3840, 2160
+    rw = bihrt.Renderer(arrays, WW, WH, spp=SPP, seed=1984)
+    wout = torch.zeros(WW * WH, dtype=torch.int32, device="cuda")
+    whits = torch.zeros(WW * WH * SPP, dtype=torch.int32, device="cuda")
+    rw.render_whitted_device(wout.data_ptr(), 0, hits_ptr=whits.data_ptr(), stream=sptr)
+    torch.cuda.synchronize()
+    traced = int(torch.clamp(whits.to(torch.int64) + 1, max=9).sum())
+    hist = torch.bincount(whits.view(-1), minlength=10).tolist()
+    del whits
+    rw.set_timing(True)
+    t0 = time.perf_counter()
+    for k in range(args.whitted_frames):
+        rw.render_whitted_device(wout.data_ptr(), 1 + k, stream=sptr)
+    torch.cuda.synchronize()
+    wel = (time.perf_counter() - t0) / args.whitted_frames
+    wk, _ = rw.last_render_times()
+    rw.set_timing(False)
+    del wout
+    return {"config": "C4: 1M soup, 3840x2160, 4 spp, 8 bounces of mirror rays",
+            "ms_per_frame": 1e3 * wel, "primary_rays_per_s": WW * WH * SPP / wel,
+            "rays_traced_per_frame": traced, "rays_traced_per_s": traced / wel,
+            "trace_kernels_ms": wk, "hit_histogram": hist, "frames": args.whitted_frames,
+            "note": "k_wh_gen + 9 x k_wh_trace (closest hit, per-lane walk, ballot/mbcnt "
+                    "compaction of live rays between bounces) + k_wh_shade; bit-exact vs the "
+                    "oracle (tests/test_whitted.py)"}
 
 
 def parallelism(mode, band, world):
@@ -594,7 +759,7 @@ def cpu_threads(args):
     return n, aff, omp
 
 
-def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
+def cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np):
     """The oracle (strict-IEEE C restatement of the reference's render path,
     oracle/bih_oracle.c) timed on the host, on bounded row samples of frame 0
     of the same workload:
@@ -606,8 +771,11 @@ def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
       host_debug_serial -- the reference's own serial host loop and rules
                  (DebugRender / CPUTraverseTree, Renderer.cpp:202-412,
                  MODE_HOST_DEBUG), one thread: config C1's semantics.
-    Also checks those rows of the GPU frame bit-exactly (all four walks give
-    the same pixels)."""
+    Then the parity of the timed call shape: one call of G frames through the
+    path the headline times (bih_render_device_frames, frames 0..G-1), its
+    frame 0 compared with the rows the four CPU legs rendered, frames 7 and
+    G-1 with oracle rows (cudaRender carries the XORWOW state across frames,
+    CUDAKernels.cu:411-419)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     threads, aff, omp = cpu_threads(args)
@@ -619,7 +787,7 @@ def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
         nrows = math.ceil((H - row0) / step)
         img, st = ot.render(W, H, spp=SPP, frame=0, rows=(row0, nrows, step), mode=mode,
                             threads=nthreads)
-        imgs.append((row0, step, img))
+        imgs.append((0, row0, step, img))
         legs[name] = {"value": st.rays / st.render_seconds, "unit": "rays/s", "cores": st.threads,
                       "seconds": st.render_seconds, "rays": st.rays,
                       "sample": f"rows {row0}::{step} of frame 0 ({nrows} rows x {W} px x {SPP} spp)",
@@ -631,12 +799,21 @@ def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
     leg("serial", oracle.MODE_GPU_REF, args.cpu_serial_row_step, 1)
     leg("host_debug_serial", oracle.MODE_HOST_DEBUG, args.cpu_debug_row_step, 1,
         row0=args.cpu_debug_row_step // 2)
-    # GPU frame 0, untimed, same rows
-    full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    r.render_device(full.data_ptr(), 0, traverse=trav, stream=torch.cuda.current_stream().cuda_stream)
+    G = max(1, args.group)
+    ps = args.parity_row_step
+    for f in sorted({min(7, G - 1), G - 1} - {0}):
+        img, _ = ot.render(W, H, spp=SPP, frame=f, rows=(0, math.ceil(H / ps), ps),
+                           mode=oracle.MODE_GPU_ANYHIT, threads=threads)
+        imgs.append((f, 0, ps, img))
+    # the timed call shape, untimed: G frames in one call on the headline's stream 0
+    from bihrt.tiling import band_rows
+    wl.step("weak", band_rows(H, args.band, 0, 1), 0, 0, trav, m=G)
     torch.cuda.synchronize()
-    g = full.cpu().numpy().view(np.uint32).reshape(H, W)
-    same = all(np.array_equal(g[row0:H:step], img) for row0, step, img in imgs)
+    frames = wl.outs[0][: G * H * W].cpu().numpy().view(np.uint32).reshape(G, H, W)
+    checks = [{"frame": f, "rows": f"{row0}::{step}", "equal": bool(np.array_equal(frames[f][row0:H:step], img))}
+              for f, row0, step, img in imgs]
+    parity = {"call": f"bih_render_device_frames, frames 0..{G - 1} in one call", "checks": checks,
+              "all_equal": all(c["equal"] for c in checks)}
     main = legs["reference_walk"]
     res = {"value": main["value"], "unit": "rays/s", "cores": main["cores"], "kind": "port",
            "sample": main["sample"] + ", oracle/bih_oracle.c reference walk (TraverseTree rules), "
@@ -646,7 +823,7 @@ def cpu_baseline(args, tris, r, out, trav, W, H, SPP, torch, np):
            "omp_num_threads_env": omp or None,
            "threads_rule": "min(sched_getaffinity, OMP_NUM_THREADS) -- the box's CPU share",
            "legs": legs}
-    return res, same
+    return res, parity
 
 
 def measure_traffic(args):

@@ -19,8 +19,8 @@ import os
 import numpy as np
 
 from . import scenes  # noqa: F401
-from ._lib import (TRAVERSE_ANYHIT, TRAVERSE_REFERENCE, BihError, Camera, Framebuffer, Rows, Scene,
-                   TreeInfo, check, load)
+from ._lib import (PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_ITEM_TILES, PARAM_PAIR_CAP, TRAVERSE_ANYHIT,
+                   TRAVERSE_REFERENCE, BihError, Camera, Framebuffer, Rows, Scene, TreeInfo, check, load)
 from . import _lib
 
 SCREEN_WIDTH, SCREEN_HEIGHT, RAYS_PER_PIXEL, SEED = 640, 480, 4, 1984   # Constants.h:4-8, :458
@@ -75,6 +75,16 @@ class GPUArrayManager:
         inf = TreeInfo()
         check(load().bih_tree_get_info(self._tree, C.byref(inf)), "bih_tree_get_info")
         return inf
+
+    def set_param(self, param: int, value: int):
+        """bih_tree_set_param (PARAM_*): work-order and test knobs; none changes a pixel."""
+        check(load().bih_tree_set_param(self._tree, param, value), "bih_tree_set_param")
+
+    def reserve(self, w: int, h: int, spp: int, rows: Rows | None = None, max_frames: int = 1):
+        """bih_reserve: size every per-call buffer of renders of this shape (calls
+        of up to max_frames frames) now, so that a frame loop allocates nothing."""
+        check(load().bih_reserve(self._tree, w, h, spp, C.byref(rows) if rows is not None else None,
+                                 max_frames), "bih_reserve")
 
     def bins_stats(self):
         """Frustum bins of the current camera and image (bih_bins_get_stats)."""
@@ -255,4 +265,4 @@ def write_ppm(path: str, img: np.ndarray):
 
 __all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
            "camera_ray_bound", "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
-           "TRAVERSE_REFERENCE"]
+           "TRAVERSE_REFERENCE", "PARAM_ITEM_TILES", "PARAM_PAIR_CAP", "PARAM_BINS_CAP", "PARAM_FORCE_FALLBACK"]

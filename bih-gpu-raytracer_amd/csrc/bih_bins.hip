@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(kThreads) k_cam_tris(const float *__restrict__
     if (i == 0) {
         gcount[0] = gcount[1] = gcount[2] = 0u;
         gcount[4] = gcount[5] = 0u;
-        gcount[6] = 0u;   // pair-result positions (k_bin_count)
+        gcount[6] = gcount[7] = 0u;   // pair-result positions (k_bin_count), 64-bit
     }
     const unsigned long long mk = __ballot(al);
     if (lane == 0) {
@@ -742,7 +742,7 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
                                                         unsigned long long *__restrict__ blkcnt,
                                                         unsigned long long *__restrict__ total64,
                                                         uint32_t *__restrict__ pres, uint32_t pres_cap,
-                                                        uint32_t *__restrict__ pcount,
+                                                        unsigned long long *__restrict__ pcount,
                                                         uint32_t *__restrict__ pbase_out) {
     __shared__ unsigned long long s_cnt[kBlockTiles];
     __shared__ uint32_t s_rect[4];   // x0, x1, y0, y1 of the block's footprints
@@ -776,8 +776,10 @@ __global__ void __launch_bounds__(kThreads) k_bin_count(const uint2 *__restrict_
     auto reserve = [&](uint32_t tot) {
         uint32_t b = ~0u;
         if (pres && tot) {
-            b = atomicAdd(pcount, tot);
-            if (b > pres_cap || pres_cap - b < tot) b = ~0u;   // past the buffer: the fill recomputes
+            // a 64-bit cursor: the pairs of all blocks may pass 2^32 (a u32
+            // cursor would wrap and hand a later block an earlier block's range)
+            const unsigned long long b64 = atomicAdd(pcount, (unsigned long long)tot);
+            if (b64 <= pres_cap && pres_cap - b64 >= tot) b = (uint32_t)b64;   // else the fill recomputes
         }
         pbase_out[blockIdx.x] = b;
         return b;
@@ -1152,7 +1154,8 @@ int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uin
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt, b.cntq,
                            reinterpret_cast<unsigned long long *>(b.blkcnt),
-                           reinterpret_cast<unsigned long long *>(b.gcount + 4), b.pres, b.pres_cap, b.gcount + 6,
+                           reinterpret_cast<unsigned long long *>(b.gcount + 4), b.pres, b.pres_cap,
+                           reinterpret_cast<unsigned long long *>(b.gcount + 6),
                            b.pbase);
     }
     const hipError_t e = hipGetLastError();

@@ -755,10 +755,11 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kThreads - 1) / 
     } while (0)
 
 template <class T>
-static hipError_t dalloc(T **p, size_t count, size_t &bytes) {
+static hipError_t dalloc(T **p, size_t count, DeviceTree &t) {
     size_t b = count * sizeof(T);
     if (b == 0) b = 16;
-    bytes += b;
+    t.bytes += b;
+    ++t.allocs;
     return hipMalloc((void **)p, b);
 }
 
@@ -801,32 +802,31 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     const uint32_t max_parts =
         (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
     if (!t.hdr) {
-        size_t &b = t.bytes;
-        BIH_TRY(dalloc(&t.hdr, 1, b));
-        BIH_TRY(dalloc(&t.tri_lo, 3 * nn, b));
-        BIH_TRY(dalloc(&t.tri_hi, 3 * nn, b));
-        BIH_TRY(dalloc(&t.keys, nn, b));
-        BIH_TRY(dalloc(&t.vals, nn, b));
-        BIH_TRY(dalloc(&t.keys2, nn, b));
-        BIH_TRY(dalloc(&t.vals2, nn, b));
-        BIH_TRY(dalloc(&t.scan_tmp, nn + 1, b));
-        BIH_TRY(dalloc(&t.flags, nn + 1, b));
-        BIH_TRY(dalloc(&t.unique_mc, nn, b));
-        BIH_TRY(dalloc(&t.dup_cnt, nn, b));
-        BIH_TRY(dalloc(&t.first_idx, nn, b));
-        BIH_TRY(dalloc(&t.leaf_parent, nn, b));
-        BIH_TRY(dalloc(&t.clip, 2 * nn, b));
-        BIH_TRY(dalloc(&t.axis, nn, b));
-        BIH_TRY(dalloc(&t.children, 2 * nn, b));
-        BIH_TRY(dalloc(&t.parent, nn, b));
-        BIH_TRY(dalloc(&t.is_leaf, 2 * nn, b));
-        BIH_TRY(dalloc(&t.fit_rng, nn, b));
-        BIH_TRY(dalloc(&t.fit_seg, 6 * seg_capacity(nn), b));
-        BIH_TRY(dalloc(&t.nodes, nn, b));
-        BIH_TRY(dalloc(&t.tris_s, 9 * nn, b));
-        BIH_TRY(dalloc(&t.hist, hist_n, b));
-        BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, b));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, b));
+        BIH_TRY(dalloc(&t.hdr, 1, t));
+        BIH_TRY(dalloc(&t.tri_lo, 3 * nn, t));
+        BIH_TRY(dalloc(&t.tri_hi, 3 * nn, t));
+        BIH_TRY(dalloc(&t.keys, nn, t));
+        BIH_TRY(dalloc(&t.vals, nn, t));
+        BIH_TRY(dalloc(&t.keys2, nn, t));
+        BIH_TRY(dalloc(&t.vals2, nn, t));
+        BIH_TRY(dalloc(&t.scan_tmp, nn + 1, t));
+        BIH_TRY(dalloc(&t.flags, nn + 1, t));
+        BIH_TRY(dalloc(&t.unique_mc, nn, t));
+        BIH_TRY(dalloc(&t.dup_cnt, nn, t));
+        BIH_TRY(dalloc(&t.first_idx, nn, t));
+        BIH_TRY(dalloc(&t.leaf_parent, nn, t));
+        BIH_TRY(dalloc(&t.clip, 2 * nn, t));
+        BIH_TRY(dalloc(&t.axis, nn, t));
+        BIH_TRY(dalloc(&t.children, 2 * nn, t));
+        BIH_TRY(dalloc(&t.parent, nn, t));
+        BIH_TRY(dalloc(&t.is_leaf, 2 * nn, t));
+        BIH_TRY(dalloc(&t.fit_rng, nn, t));
+        BIH_TRY(dalloc(&t.fit_seg, 6 * seg_capacity(nn), t));
+        BIH_TRY(dalloc(&t.nodes, nn, t));
+        BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
+        BIH_TRY(dalloc(&t.hist, hist_n, t));
+        BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
+        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, t));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
         // tag): stale data in fresh memory must not pass for a predecessor's
         // published prefix; afterwards every word carries an older call's

@@ -91,8 +91,40 @@ struct CamSet {
     hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
 };
 
+// Per-tree parameters (bih_tree_set_param).  None changes a pixel.  Their
+// defaults come from the environment, read once per process (A/B scripts),
+// never on the render path.
+struct TreeParams {
+    uint32_t item_tiles = 65536u;     // BIH_PARAM_ITEM_TILES
+    uint32_t pair_cap = 0xFFFFFFFFu;  // BIH_PARAM_PAIR_CAP (~0: sized from N)
+    uint64_t bins_cap = 0;            // BIH_PARAM_BINS_CAP (0: no cap)
+    uint32_t force_fallback = 0;      // BIH_PARAM_FORCE_FALLBACK
+};
+static const TreeParams &env_params() {
+    static const TreeParams p = [] {
+        TreeParams q;
+        if (const char *v = getenv("BIH_ITEM_TILES")) q.item_tiles = (uint32_t)strtoul(v, nullptr, 10);
+        if (const char *v = getenv("BIH_PAIR_CAP")) q.pair_cap = (uint32_t)strtoul(v, nullptr, 10);
+        if (const char *v = getenv("BIH_BINS_CAP")) q.bins_cap = (uint64_t)strtoull(v, nullptr, 10);
+        if (const char *v = getenv("BIH_BINS_FORCE_FALLBACK")) q.force_fallback = v[0] == '1';
+        return q;
+    }();
+    return p;
+}
+#if BIH_DEBUG_KNOBS
+static uint32_t dbg_bits() {
+    static const uint32_t d = [] {
+        const char *v = getenv("BIH_DBG");
+        return v ? (uint32_t)atoi(v) & ~4u : 0u;
+    }();
+    return d;
+}
+#endif
+
 struct bih_tree {
     bih::DeviceTree t;
+    TreeParams prm = env_params();
+    uint64_t allocs = 0;             // hipMalloc calls of the render side (+ t.allocs: the builder's)
     hipStream_t stream = nullptr;
     // ev0/ev1: the render kernel's start and end (bih_last_render_ms); evd:
     // everything the render issued is done (ordering of slot reuse, rebuilds)
@@ -157,6 +189,14 @@ struct bih_tree {
 };
 
 namespace {
+
+// Every device allocation of a tree goes through here (bih_tree_info.device_allocs).
+template <class T>
+hipError_t tree_malloc(bih_tree *tr, T **p, size_t bytes) {
+    const hipError_t e = hipMalloc((void **)p, bytes);
+    if (e == hipSuccess) ++tr->allocs;
+    return e;
+}
 
 struct DeviceGuard {
     int prev = -1;
@@ -243,7 +283,7 @@ int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &
         if (tr->chunk_buf) (void)hipFree(tr->chunk_buf);
         tr->chunk_buf = nullptr;
         tr->chunk_cap = 0;
-        hipError_t e = hipMalloc((void **)&tr->chunk_buf, (size_t)kSlots * 2 * n * sizeof(uint32_t));
+        hipError_t e = tree_malloc(tr, &tr->chunk_buf, (size_t)kSlots * 2 * n * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip((int)e);
         tr->chunk_cap = n;
         memset(tr->chunk_key, 0, sizeof tr->chunk_key);
@@ -409,7 +449,7 @@ int bih_build(const bih_scene *scene, int device, bih_tree **out) {
     tr->t.n = scene->n_tris;
     tr->host_v = scene->v;
     size_t bytes = (size_t)scene->n_tris * 36;
-    hipError_t e = hipMalloc((void **)&tr->t.v, bytes ? bytes : 16);
+    hipError_t e = tree_malloc(tr, &tr->t.v, bytes ? bytes : 16);
     if (e == hipSuccess) {
         tr->t.owns_v = true;
         tr->t.bytes += bytes;
@@ -523,6 +563,7 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
                           (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
     info->build_ms = tr->build_ms;
+    info->device_allocs = tr->allocs + tr->t.allocs;
     return BIH_OK;
 }
 
@@ -568,27 +609,85 @@ static uint32_t *rng_buf(const bih_tree *tr, int k) {
 // 2*spp draws per frame; a short gap runs the generators forward, anything
 // else re-seeds with a skip-ahead).  Runs on `st` after the renders that
 // read rng_cur before (see bih_render_device).
+// Waits for every render in flight through the tree (they may read a buffer
+// that is about to be replaced).
+static int drain_renders(bih_tree *tr) {
+    for (int k = 0; k < kSlots; ++k)
+        if (tr->used[k]) {
+            hipError_t e = hipEventSynchronize(tr->evd[k]);
+            if (e != hipSuccess) return map_hip((int)e);
+        }
+    return BIH_OK;
+}
+
+// The XORWOW ring (kRngBufs x 5 planes) and the per-slot accumulators for P
+// pixels; a new ring holds no state (the next render seeds it).
+static int ensure_rng(bih_tree *tr, size_t P, hipStream_t st) {
+    if (P <= tr->rng_cap) return BIH_OK;
+    int rc = drain_renders(tr);
+    if (rc) return rc;
+    if (tr->rng) (void)hipFree(tr->rng);
+    tr->rng = nullptr;
+    tr->rng_cap = 0;
+    const size_t words = P * (5 * kRngBufs + kSlots);
+    hipError_t e = tree_malloc(tr, &tr->rng, words * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(tr->rng + 5 * kRngBufs * P, 0, kSlots * P * sizeof(uint32_t), st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_cap = P;
+    tr->rng_cur = 0;
+    tr->rng_valid = false;
+    return BIH_OK;
+}
+
+// The persistent render kernels' work words and stack spill areas.
+static int ensure_work(bih_tree *tr) {
+    if (tr->work) return BIH_OK;
+    tr->spill_per_slot = bih::spill_words(bih::wave_grid_blocks(tr->t.device));
+    hipError_t e = tree_malloc(tr, &tr->work, kSlots * bih::kWorkWords * sizeof(uint32_t));
+    if (e == hipSuccess) e = tree_malloc(tr, &tr->spill, kSlots * tr->spill_per_slot * sizeof(uint32_t));
+    return map_hip((int)e);
+}
+
+// The frustum-bin kernel's queue state: per slot two sets, zero (each
+// launch zeroes the other set for the slot's next launch).
+static int ensure_qcount(bih_tree *tr) {
+    if (tr->q_count) return BIH_OK;
+    const size_t bytes = (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t);
+    hipError_t e = tree_malloc(tr, &tr->q_count, bytes);
+    if (e == hipSuccess) e = hipMemset(tr->q_count, 0, bytes);
+    return map_hip((int)e);
+}
+
+// kSlots x `need` units of `unit` words (fallback records, split start
+// states), grown after every render in flight.
+static int ensure_per_slot(bih_tree *tr, uint32_t **buf, size_t *cap, size_t need, size_t unit) {
+    if (*cap >= need) return BIH_OK;
+    int rc = drain_renders(tr);
+    if (rc) return rc;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    hipError_t e = tree_malloc(tr, buf, (size_t)kSlots * need * unit * sizeof(uint32_t));
+    if (e != hipSuccess) return map_hip((int)e);
+    *cap = need;
+    return BIH_OK;
+}
+
+// Armed after prepare_rng: unless disarmed (the render was issued), the
+// ring's state is dropped so that the next render re-seeds.
+struct RngGuard {
+    bih_tree *tr;
+    bool armed = true;
+    ~RngGuard() {
+        if (armed) tr->rng_valid = false;
+    }
+};
+
 static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, uint64_t seed,
                        const bih_rows &rows, hipStream_t st) {
     const size_t P = (size_t)rows.nrows * w;
-    if (P > tr->rng_cap) {
-        for (int k = 0; k < kSlots; ++k)
-            if (tr->used[k]) {
-                hipError_t e = hipEventSynchronize(tr->evd[k]);   // in-flight readers
-                if (e != hipSuccess) return map_hip((int)e);
-            }
-        if (tr->rng) (void)hipFree(tr->rng);
-        tr->rng = nullptr;
-        tr->rng_cap = 0;
-        const size_t words = P * (5 * kRngBufs + kSlots);
-        hipError_t e = hipMalloc((void **)&tr->rng, words * sizeof(uint32_t));
-        if (e == hipSuccess)
-            e = hipMemsetAsync(tr->rng + 5 * kRngBufs * P, 0, kSlots * P * sizeof(uint32_t), st);
-        if (e != hipSuccess) return map_hip((int)e);
-        tr->rng_cap = P;
-        tr->rng_cur = 0;
-        tr->rng_valid = false;
-    }
+    int rc = ensure_rng(tr, P, st);
+    if (rc) return rc;
     const bool same_px = tr->rng_valid && tr->key_w == w && tr->key_spp == spp &&
                          tr->key_seed == seed && tr->key_row0 == rows.row0 &&
                          tr->key_nrows == rows.nrows && tr->key_bh == rows.band_h &&
@@ -690,8 +789,7 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
     // pair results (k_bin_count -> k_bin_fill): 4 B per (triangle, tile)
     // pair; blocks past the buffer recompute in the fill
     uint32_t pres_cap = (uint32_t)std::min<uint64_t>(4ull * n + (1u << 20), 0x3FFFFFFFull);
-    if (const char *v = getenv("BIH_PAIR_CAP"))   // tests: blocks past a small buffer recompute
-        pres_cap = std::min<uint32_t>(pres_cap, (uint32_t)strtoul(v, nullptr, 10));
+    pres_cap = std::min<uint32_t>(pres_cap, tr->prm.pair_cap);   // tests: blocks past a small buffer recompute
     const size_t s_pres = al((size_t)pres_cap * 4);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
                         s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt + s_pbase + s_pres;
@@ -701,7 +799,7 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
         if (c.bins_mem) (void)hipFree(c.bins_mem);
         c.bins_mem = nullptr;
         c.bins_mem_cap = 0;
-        e = hipMalloc((void **)&c.bins_mem, need);
+        e = tree_malloc(tr, &c.bins_mem, need);
         if (e != hipSuccess) return map_hip((int)e);
         c.bins_mem_cap = need;
         c.bins_layout = 0;
@@ -751,8 +849,7 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
         const char *v = getenv("BIH_BINS_SYNC");
         return v && v[0] == '1';
     }();
-    size_t cap_test = 0;
-    if (const char *v = getenv("BIH_BINS_CAP")) cap_test = (size_t)strtoull(v, nullptr, 10);
+    const size_t cap_test = (size_t)tr->prm.bins_cap;
     const bool speculative = c.bin_list_cap > 0 && !always_sync && !c.bins_regrow;
     if (speculative) {
         const size_t cap = cap_test ? std::min(cap_test, c.bin_list_cap) : c.bin_list_cap;
@@ -784,7 +881,7 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
             if (c.bin_list) (void)hipFree(c.bin_list);   // st waited for every render
             c.bin_list = nullptr;
             c.bin_list_cap = 0;
-            e = hipMalloc((void **)&c.bin_list, cap * kEntryBytes);
+            e = tree_malloc(tr, &c.bin_list, cap * kEntryBytes);
             if (e != hipSuccess) {
                 (void)hipGetLastError();   // not sticky: this camera renders without bins
                 c.bin_list = nullptr;
@@ -829,6 +926,23 @@ static void resolve_bins(CamSet &c, bool block) {
     }
 }
 
+// A camera set's tile-queue memory for `ntiles` tiles (its renders in
+// flight may read the old one).
+static int ensure_queue_mem(bih_tree *tr, CamSet &c, uint32_t ntiles) {
+    const size_t need = bih::bin_queue_bytes(ntiles);
+    if (c.q_cap >= need) return BIH_OK;
+    int rc = drain_renders(tr);
+    if (rc) return rc;
+    if (c.q_mem) (void)hipFree(c.q_mem);
+    c.q_mem = nullptr;
+    c.q_cap = 0;
+    c.q_valid = false;
+    hipError_t e = tree_malloc(tr, &c.q_mem, need);
+    if (e != hipSuccess) return map_hip((int)e);
+    c.q_cap = need;
+    return BIH_OK;
+}
+
 // The render kernel's tile queue for this launch's rows (launch_bin_queue):
 // rebuilt when the bins or the rows change, after every render that may
 // still read the old one.
@@ -840,27 +954,13 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     const uint32_t ntiles = tiles_x * ((rows.nrows + th - 1) / th);
     const size_t nrec = (size_t)ntiles * nframes;   // fallback records: one per packet at most
     const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, c.gen};
-    if (!tr->q_count) {
-        hipError_t e = hipMalloc((void **)&tr->q_count, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
-        if (e == hipSuccess)
-            e = hipMemset(tr->q_count, 0, (size_t)kSlots * 2 * bih::kBinSetWords * sizeof(uint32_t));
-        if (e != hipSuccess) return map_hip((int)e);
-    }
+    int rc = ensure_qcount(tr);
+    if (rc) return rc;
     if (!c.q_valid || memcmp(key, c.q_key, sizeof key) != 0) {
-        int rc = wait_set_readers(tr, ci, st);
+        rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
-        const size_t need = bih::bin_queue_bytes(ntiles);
-        if (c.q_cap < need) {
-            for (int k = 0; k < kSlots; ++k)
-                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
-            if (c.q_mem) (void)hipFree(c.q_mem);
-            c.q_mem = nullptr;
-            c.q_cap = 0;
-            c.q_valid = false;
-            hipError_t e = hipMalloc((void **)&c.q_mem, need);
-            if (e != hipSuccess) return map_hip((int)e);
-            c.q_cap = need;
-        }
+        rc = ensure_queue_mem(tr, c, ntiles);
+        if (rc) return rc;
         int le = bih::launch_bin_queue(c.bins.off, c.bins.gcount + 1, c.bins.bins_x, tiles_x, ntiles, rows.row0,
                                        rows.band_h, rows.band_step, th, c.q_mem, &c.q_list, &c.q_hdr,
                                        st);
@@ -868,16 +968,8 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
         memcpy(c.q_key, key, sizeof key);
         c.q_valid = true;
     }
-    if (tr->fbq_cap < nrec) {
-        for (int k = 0; k < kSlots; ++k)
-            if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
-        if (tr->fb_mem) (void)hipFree(tr->fb_mem);
-        tr->fb_mem = nullptr;
-        tr->fbq_cap = 0;
-        hipError_t e = hipMalloc((void **)&tr->fb_mem, (size_t)kSlots * nrec * 8 * sizeof(uint32_t));
-        if (e != hipSuccess) return map_hip((int)e);
-        tr->fbq_cap = nrec;
-    }
+    rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, nrec, 8);
+    if (rc) return rc;
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
     a.bin_queue = c.q_list;
     a.bin_qhdr = c.q_hdr;
@@ -885,15 +977,32 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     // pixels, so only a BIH_DEBUG_KNOBS=1 build reads them) and the fallback
     // test mode (routes packets to the exact walk: same pixels)
 #if BIH_DEBUG_KNOBS
-    if (const char *d = getenv("BIH_DBG")) a.dbg = (uint32_t)atoi(d) & ~4u;
+    a.dbg = dbg_bits();
 #endif
-    if (const char *d = getenv("BIH_BINS_FORCE_FALLBACK"))
-        if (d[0] == '1') a.dbg |= 4u;
+    if (tr->prm.force_fallback) a.dbg |= 4u;
     // (q_par[slot] flips once the launch that zeroes the other set is issued)
     const uint32_t par = tr->q_par[slot];
     a.bin_heads = tr->q_count + (size_t)(2 * slot + par) * bih::kBinSetWords;
     a.bin_heads_next = tr->q_count + (size_t)(2 * slot + (par ^ 1u)) * bih::kBinSetWords;
     return BIH_OK;
+}
+
+// Frames per k_render_bins item (*fpi) and item splits (*nsplit) of an
+// nframes launch over a w x nrows image: every frame of the launch in one
+// item when the launch has many tiles (the list is walked nframes times while
+// it is cached), fewer when it has few (a rank's bands of the frame), so the
+// items keep outnumbering the resident waves.  BIH_PARAM_ITEM_TILES is the
+// tile count below which an item's frames are split; it changes the order of
+// the work, never a pixel.
+static void item_split(const bih_tree *tr, uint32_t w, uint32_t nrows, uint32_t spp, uint32_t nframes,
+                       uint32_t *fpi, uint32_t *nsplit) {
+    uint32_t tw = 0, th = 0;
+    tile_shape(spp, &tw, &th);
+    const uint64_t ntiles = (uint64_t)((w + tw - 1) / tw) * ((nrows + th - 1) / th);
+    uint64_t ns = ntiles ? (tr->prm.item_tiles + ntiles / 2) / ntiles : nframes;
+    ns = std::max<uint64_t>(1, std::min<uint64_t>(ns, nframes));
+    *fpi = (uint32_t)((nframes + ns - 1) / ns);
+    *nsplit = (nframes + *fpi - 1) / *fpi;
 }
 
 // nframes > 1 (bih_render_device_frames): frames frame .. frame+nframes-1 in
@@ -935,12 +1044,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     }
     CamSet &c = tr->cs[ci];
     resolve_bins(c, false);
-    if (!tr->work) {
-        tr->spill_per_slot = bih::spill_words(bih::wave_grid_blocks(tr->t.device));
-        hipError_t e = hipMalloc((void **)&tr->work, kSlots * bih::kWorkWords * sizeof(uint32_t));
-        if (e == hipSuccess)
-            e = hipMalloc((void **)&tr->spill, kSlots * tr->spill_per_slot * sizeof(uint32_t));
-        if (e != hipSuccess) return map_hip((int)e);
+    {
+        const int rw = ensure_work(tr);
+        if (rw) return rw;
     }
     // Dependencies (f = this render, S = kSlots):
     //  - slot: render f-S used this tile queue and spill area, and read rng
@@ -972,12 +1078,12 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             if (rc) return rc;
         }
         if (grow) {
-            for (int k = 0; k < kSlots; ++k)
-                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
+            rc = drain_renders(tr);
+            if (rc) return rc;
             if (c.prim) (void)hipFree(c.prim);
             c.prim = nullptr;
             c.prim_cap = 0;
-            e = hipMalloc((void **)&c.prim, need);
+            e = tree_malloc(tr, &c.prim, need);
             if (e != hipSuccess) return map_hip((int)e);
             c.prim_cap = need;
             c.prim_valid = false;
@@ -1051,30 +1157,20 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // after this launch's last (CUDAKernels.cu:419)
     rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
+    // next_frame now points past this launch while rng_cur still holds its
+    // first frame's state: a failure before the launch is issued makes the
+    // next call re-seed instead of rendering from stale state
+    RngGuard rng_guard{tr};
     const size_t P = (size_t)rows.nrows * w;
     const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
     a.nframes = nframes;
     a.out_stride = out_stride;
     if (use_bins && nframes > 1) {
-        // frames per k_render_bins item: every frame of the launch when the
-        // launch has many tiles (the list is walked nframes times while it is
-        // cached), fewer when it has few (a rank's bands of the frame), so the
-        // items keep outnumbering the resident waves (BIH_ITEM_TILES: the tile
-        // count below which an item's frames are split; A/B and tests: it
-        // changes the order of the work, never a pixel)
-        uint32_t item_tiles = 65536u;
-        if (const char *v = getenv("BIH_ITEM_TILES")) item_tiles = (uint32_t)strtoul(v, nullptr, 10);
-        // (A/B, 1M soup at 1080p, 16 frames per call: one item of 16 frames
+        // frames per k_render_bins item (item_split; A/B, 1M soup at 1080p, 16 frames per call: one item of 16 frames
         // per tile 0.047 ms per frame, two of 8 0.051; a rank's eighth of the
         // bands, 8 frames per call: items of 8 frames 0.0107 ms per frame, of
         // 2 0.0078; 16 per call, items of 4: 0.0069)
-        uint32_t tw = 0, th = 0;
-        tile_shape(spp, &tw, &th);
-        const uint64_t ntiles = (uint64_t)((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
-        uint64_t ns = ntiles ? (item_tiles + ntiles / 2) / ntiles : nframes;
-        ns = std::max<uint64_t>(1, std::min<uint64_t>(ns, nframes));
-        a.fpi = (uint32_t)((nframes + ns - 1) / ns);
-        a.nsplit = (nframes + a.fpi - 1) / a.fpi;
+        item_split(tr, w, rows.nrows, spp, nframes, &a.fpi, &a.nsplit);
     } else {
         a.fpi = nframes;
         a.nsplit = 1;
@@ -1084,17 +1180,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // per slot: this render reads them, the slot's next one rewrites them)
     uint32_t *split = nullptr;
     if (a.nsplit > 1) {
-        const size_t words = (size_t)(a.nsplit - 1) * 5 * P;
-        if (tr->rsplit_cap < words) {
-            for (int k = 0; k < kSlots; ++k)
-                if (tr->used[k]) (void)hipEventSynchronize(tr->evd[k]);
-            if (tr->rsplit) (void)hipFree(tr->rsplit);
-            tr->rsplit = nullptr;
-            tr->rsplit_cap = 0;
-            e = hipMalloc((void **)&tr->rsplit, (size_t)kSlots * words * sizeof(uint32_t));
-            if (e != hipSuccess) return map_hip((int)e);
-            tr->rsplit_cap = words;
-        }
+        rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(a.nsplit - 1) * 5 * P, 1);
+        if (rc) return rc;
         split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
         a.rng_split = split;
     }
@@ -1197,6 +1284,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;                 // frame+1's state
+    rng_guard.armed = false;
     return BIH_OK;
 }
 
@@ -1230,6 +1318,63 @@ int bih_render_device_frames(const bih_tree *ctr, const bih_camera *cam, uint32_
     return BIH_OK;
 }
 
+int bih_reserve(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_rows *rows_in, uint32_t max_frames) {
+    if (!tr || w == 0 || h == 0 || spp == 0 || max_frames == 0 || max_frames > 64) return BIH_ERR_INVALID;
+    const bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
+    if (rows.nrows == 0) return BIH_OK;
+    if (rows.band_h == 0 || rows.band_step == 0 || (uint64_t)h * w > 0xFFFFFFFFull) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    const size_t P = (size_t)rows.nrows * w;
+    int rc = ensure_rng(tr, P, tr->stream);
+    if (!rc) rc = ensure_work(tr);
+    if (!rc) rc = ensure_qcount(tr);
+    if (rc) return rc;
+    // the frustum-bin path: tile queues of every camera set, fallback records
+    // (one per packet and frame at most), the start states of item splits
+    uint32_t tw = 0, th = 0;
+    tile_shape(spp, &tw, &th);
+    const uint32_t ntiles = ((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
+    for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles);
+    if (!rc) rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, (size_t)ntiles * max_frames, 8);
+    uint32_t fpi = 1, nsplit = 1;
+    item_split(tr, w, rows.nrows, spp, max_frames, &fpi, &nsplit);
+    if (!rc && nsplit > 1) rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(nsplit - 1) * 5 * P, 1);
+    if (rc) return rc;
+    return map_hip((int)hipStreamSynchronize(tr->stream));
+}
+
+int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
+    if (!tr) return BIH_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(tr->mu);
+    switch (param) {
+    case BIH_PARAM_ITEM_TILES:
+        if (value == 0 || value > 0xFFFFFFFFull) return BIH_ERR_INVALID;
+        tr->prm.item_tiles = (uint32_t)value;
+        return BIH_OK;
+    case BIH_PARAM_PAIR_CAP: {
+        const uint32_t v = (uint32_t)std::min<uint64_t>(value, 0xFFFFFFFFull);
+        if (v == tr->prm.pair_cap) return BIH_OK;
+        tr->prm.pair_cap = v;
+        break;
+    }
+    case BIH_PARAM_BINS_CAP:
+        if (value == tr->prm.bins_cap) return BIH_OK;
+        tr->prm.bins_cap = value;
+        break;
+    case BIH_PARAM_FORCE_FALLBACK:
+        if (value > 1) return BIH_ERR_INVALID;
+        tr->prm.force_fallback = (uint32_t)value;
+        return BIH_OK;
+    default:
+        return BIH_ERR_INVALID;
+    }
+    // the bins of every camera set were built under the old cap: rebuilt by
+    // their next render
+    for (CamSet &c : tr->cs) c.bins_valid = false;
+    return BIH_OK;
+}
+
 int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32_t w, uint32_t h,
                               uint32_t spp, uint32_t frame, uint64_t seed, const bih_rows *rows_in,
                               uint32_t *d_out, uint32_t *d_hits, void *stream) {
@@ -1256,6 +1401,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     }
     rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
+    RngGuard rng_guard{tr};
     const size_t P = (size_t)rows.nrows * w;
     const uint64_t rays = (uint64_t)P * spp;
     const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
@@ -1267,7 +1413,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
         if (tr->wh_mem) (void)hipFree(tr->wh_mem);
         tr->wh_mem = nullptr;
         tr->wh_rays = 0;
-        e = hipMalloc((void **)&tr->wh_mem, bih::whitted_bytes(rays));
+        e = tree_malloc(tr, &tr->wh_mem, bih::whitted_bytes(rays));
         if (e != hipSuccess) return map_hip((int)e);
         tr->wh_rays = rays;
     }
@@ -1310,6 +1456,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;
+    rng_guard.armed = false;
     return BIH_OK;
 }
 
@@ -1328,7 +1475,7 @@ int bih_render_whitted(const bih_scene *scene, const bih_tree *ctr, const bih_ca
             if (tr->fb) (void)hipFree(tr->fb);
             tr->fb = nullptr;
             tr->fb_cap = 0;
-            hipError_t e = hipMalloc((void **)&tr->fb, P * 4);
+            hipError_t e = tree_malloc(tr, &tr->fb, P * 4);
             if (e != hipSuccess) return map_hip((int)e);
             tr->fb_cap = P;
         }
@@ -1542,7 +1689,7 @@ static int render_host(const bih_scene *scene, const bih_tree *ctr, const bih_ca
             if (tr->fb) (void)hipFree(tr->fb);
             tr->fb = nullptr;
             tr->fb_cap = 0;
-            hipError_t e = hipMalloc((void **)&tr->fb, P * 4);
+            hipError_t e = tree_malloc(tr, &tr->fb, P * 4);
             if (e != hipSuccess) return map_hip((int)e);
             tr->fb_cap = P;
         }

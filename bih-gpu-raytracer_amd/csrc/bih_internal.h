@@ -41,8 +41,8 @@ constexpr int kLdsStack = BIH_LDS_STACK;
 constexpr uint32_t kSlotStrideWords = 32;
 constexpr uint32_t kWorkWords = 64 + kSlotStrideWords * 1024 + 64;   // + histograms (counter builds)
 constexpr uint32_t kHistWord = 64 + kSlotStrideWords * 1024;
-constexpr uint32_t kBinGlobalMax = 4096;
-constexpr uint32_t kBinEntryF4 = 3;               // list entry: 3 x float4 = 48 bytes (bih_bins.hip)          // longer global lists: no bins (the shortcut walk)
+constexpr uint32_t kBinGlobalMax = 4096;          // longer global lists: no bins (the shortcut walk)
+constexpr uint32_t kBinEntryF4 = 3;               // list entry: 3 x float4 = 48 bytes (bih_bins.hip)
 constexpr uint32_t kBinsUnusable = 0xFFFFFFFFu;   // bins status: lists not built (k_bin_status)
 constexpr uint32_t kBinSetWords = (16 + 1024) * 32;   // k_render_bins queue state per set
 #ifndef BIH_BUCKETS
@@ -172,6 +172,7 @@ struct DeviceTree {
     uint32_t n = 0, u = 0;
     uint64_t content = 0;          // TreeHeader::content of the last build
     size_t bytes = 0;
+    uint64_t allocs = 0;           // hipMalloc calls made for this tree (bih_tree_info.device_allocs)
     float *v = nullptr;            // input soup f32[9N] (device copy)
     bool owns_v = false;
     TreeHeader *hdr = nullptr;

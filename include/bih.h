@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BIH_ABI_VERSION 1
+#define BIH_ABI_VERSION 2   /* 2: bih_tree_info.device_allocs, bih_reserve, bih_tree_set_param */
 
 /* error codes */
 #define BIH_OK               0
@@ -98,6 +98,9 @@ typedef struct bih_tree_info {
     int device;
     uint64_t device_bytes;                /* device memory held by the tree    */
     double build_ms;                      /* device time of the last build     */
+    uint64_t device_allocs;               /* device allocations the tree made so
+                                             far (a steady-state frame loop adds
+                                             none: see bih_reserve)              */
 } bih_tree_info;
 
 /* Canonical arrays for parity checks (reference buffer names in brackets). */
@@ -179,12 +182,41 @@ int bih_render_device_frames(const bih_tree *tree, const bih_camera *camera, uin
                              const bih_rows *rows, uint32_t *d_out, uint64_t out_stride, void *stream);
 int bih_sync(const bih_tree *tree, void *stream);
 
+/* Sizes, ahead of time, every per-call device buffer that renders of this
+ * shape need (w x h image, spp, rows = NULL for the whole frame, calls of up to
+ * max_frames frames through bih_render_device_frames): the XORWOW ring, the
+ * per-slot tile-queue state, fallback records and frame-split start states.
+ * After it (and after one render with each camera) a frame loop of that shape
+ * allocates nothing (bih_tree_info.device_allocs stays put).  The reference
+ * allocates these once in Renderer::CreateCUDABuffers (src/Renderer.cpp:
+ * 762-797); here they also depend on the call shape, hence the explicit call.
+ * Renders of a larger shape still grow the buffers on demand. */
+int bih_reserve(bih_tree *tree, uint32_t w, uint32_t h, uint32_t spp, const bih_rows *rows,
+                uint32_t max_frames);
+
+/* Per-tree parameters.  None changes a pixel; they only reorder work or
+ * force the exact-walk fallback, for A/B runs and tests.  Defaults are read
+ * once per process from the environment variable of the same name
+ * (BIH_ITEM_TILES, ...), never on the render path. */
+#define BIH_PARAM_ITEM_TILES      1  /* tile count below which a multi-frame
+                                        launch splits an item's frames (65536) */
+#define BIH_PARAM_PAIR_CAP        2  /* (triangle, tile) pair-result slots of
+                                        the bins build (tests: 0 = recompute)  */
+#define BIH_PARAM_BINS_CAP        3  /* cap on bin list entries (tests: force
+                                        the overflow path; 0 = none)           */
+#define BIH_PARAM_FORCE_FALLBACK  4  /* 1: every live packet of a frustum-bin
+                                        render takes the exact walk (tests)    */
+int bih_tree_set_param(bih_tree *tree, int param, uint64_t value);
+
 /* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)
  * reflection per primary ray.  The reference has primary rays only
  * (Color, src/CUDAKernels.cu:370-389), so these semantics are this
  * library's own, stated in DESIGN.md section 4.5 and restated by the oracle
- * (ob_render_whitted): closest hit = min (t, sorted index) over the reference
- * walk's visit set; P = O + tD, n = cross(e1, e2), R = D - (2 D.n / n.n) n;
+ * (ob_render_whitted): closest hit = min (t, sorted index) over the triangles
+ * a front-to-back walk tests -- the reference walk's decisions and order
+ * (TraverseTree, :227-368) until the first hit, after which a stacked node
+ * entered beyond the best hit (tMin > best) is popped unvisited and tMax is
+ * clamped to the best hit; P = O + tD, n = cross(e1, e2), R = D - (2 D.n / n.n) n;
  * secondary hits need t > 1e-4; a sample's shade halves towards (255,255,0)
  * per hit and ends at (20,20,40) on a miss (or (255,255,0) after 8 bounces).
  * Same primary rays, RNG draws and framebuffer format as bih_render.

@@ -40,7 +40,7 @@ def test_camera_reference_matches_oracle(bihrt_mod, oracle_mod):
 
 def test_errors_without_device(bihrt_mod):
     L = bihrt_mod._lib.load()
-    assert L.bih_abi_version() == 1
+    assert L.bih_abi_version() == 2
     assert L.bih_strerror(-2).decode().startswith("no HIP device")
     assert L.bih_strerror(12345).decode() == "unknown error"
     cam = bihrt_mod.Camera()
@@ -57,6 +57,10 @@ def test_errors_without_device(bihrt_mod):
     assert L.bih_build(C.byref(sc), 0, C.byref(t)) == -6
     assert L.bih_render(None, None, None, None) == -1
     assert L.bih_render_device(None, None, 1, 1, 1, 0, 0, None, 0, None, None, None) == -1
+    assert L.bih_reserve(None, 1920, 1080, 4, None, 16) == -1
+    assert L.bih_tree_set_param(None, bihrt_mod.PARAM_ITEM_TILES, 1) == -1
+    # the tree-info struct carries the allocation counter (ABI 2)
+    assert bihrt_mod._lib.TreeInfo.device_allocs.offset + 8 == C.sizeof(bihrt_mod._lib.TreeInfo)
 
 
 def test_no_cpu_fallback_in_product():

@@ -414,7 +414,7 @@ def test_anyhit_shortcut_matches_exact_walk(scene, gpu, bihrt_mod):
 @pytest.mark.parametrize("scene", ["soup200k", "grazing_dense", "cornell"])
 def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
     """k_render_fallback (the exact walk for packets the frustum-bin kernel
-    leaves undecided) on every live packet: BIH_BINS_FORCE_FALLBACK=1 sends
+    leaves undecided) on every live packet: PARAM_FORCE_FALLBACK sends
     each one there; every pixel equals the exact walk's, on one stream and
     with frames in flight on three."""
     import torch
@@ -426,7 +426,7 @@ def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
     g = bihrt_mod.GPUArrayManager(tris)
     w, h = 480, 270
     ref = [_device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_REFERENCE) for f in range(4)]
-    monkeypatch.setenv("BIH_BINS_FORCE_FALLBACK", "1")
+    g.set_param(bihrt_mod.PARAM_FORCE_FALLBACK, 1)
     for f in (0, 3):
         a = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_ANYHIT)
         assert np.array_equal(a, ref[f]), (scene, f, int((a != ref[f]).sum()))
@@ -445,11 +445,11 @@ def test_bins_fallback_matches_exact_walk(scene, gpu, bihrt_mod, monkeypatch):
 def test_pair_results_past_buffer_recompute(cap, gpu, bihrt_mod, monkeypatch):
     """k_bin_fill takes each (triangle, tile) pair's class, pixel mask and
     bucket from k_bin_count's pair buffer; count blocks past the buffer
-    (BIH_PAIR_CAP caps it: 0 = every block, 5000 = most) leave them to be
+    (PARAM_PAIR_CAP caps it: 0 = every block, 5000 = most) leave them to be
     computed again by the fill.  Every frame equals the reference walk's."""
     tris = bihrt_mod.scenes.soup(200_000, seed=11)
-    monkeypatch.setenv("BIH_PAIR_CAP", cap)
     g = bihrt_mod.GPUArrayManager(tris)
+    g.set_param(bihrt_mod.PARAM_PAIR_CAP, int(cap))
     w, h = 480, 270
     for f in (0, 2):
         a = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_ANYHIT)
@@ -587,7 +587,7 @@ def test_camera_change_mid_sequence_on_streams(nstreams, order, gpu, bihrt_mod):
 def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
     """Camera changes build the frustum bins without a host round trip into
     the list buffer of an earlier camera (bih_capi.cpp build_bins): when the
-    lists do not fit (BIH_BINS_CAP forces it) the device status word sends
+    lists do not fit (PARAM_BINS_CAP forces it) the device status word sends
     every live packet to the exact walk, the host notices afterwards
     (resolve_bins) and the next render rebuilds a sized list.  Every frame
     equals the reference walk's."""
@@ -606,10 +606,7 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
             (4, 3, None, True), (5, 0, "1000", False), (6, 0, None, True), (7, 1, None, True)]
     out = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     for f, c, cap, usable in plan:
-        if cap is None:
-            monkeypatch.delenv("BIH_BINS_CAP", raising=False)
-        else:
-            monkeypatch.setenv("BIH_BINS_CAP", cap)
+        g.set_param(bihrt_mod.PARAM_BINS_CAP, 0 if cap is None else int(cap))
         r.camera = cams[c]
         out.fill_(-1)
         r.render_device(out.data_ptr(), f)
@@ -623,7 +620,6 @@ def test_bins_without_sync_overflow_falls_back(gpu, bihrt_mod, monkeypatch):
         r.sync()
         b = out.cpu().numpy().view(np.uint32).reshape(h, w)
         assert np.array_equal(a, b), (f, c, cap, int((a != b).sum()))
-    monkeypatch.delenv("BIH_BINS_CAP", raising=False)
     g.close()
 
 
@@ -646,14 +642,14 @@ def test_render_device_frames_equals_single_frames(case, gpu, bihrt_mod, oracle_
     rows = band_rows(h, 8, 1, 3) if case.startswith("bands") else None
     nrows = rows.nrows if rows is not None else h
     if case == "force_fallback":
-        monkeypatch.setenv("BIH_BINS_FORCE_FALLBACK", "1")
-    # frames per k_render_bins item (BIH_ITEM_TILES, bih_capi.cpp): the
-    # default splits this small image's 5 frames into 5 items per tile; 1
-    # puts all 5 in one item, 16320 (about 2x the tiles) 3 + 2
+        g.set_param(bihrt_mod.PARAM_FORCE_FALLBACK, 1)
+    # frames per k_render_bins item (PARAM_ITEM_TILES, bih_capi.cpp
+    # item_split): the default splits this small image's 5 frames into 5 items
+    # per tile; 1 puts all 5 in one item, 16320 (about 2x the tiles) 3 + 2
     if case.endswith("items_all_frames"):
-        monkeypatch.setenv("BIH_ITEM_TILES", "1")
+        g.set_param(bihrt_mod.PARAM_ITEM_TILES, 1)
     elif case.endswith("items_3_frames"):
-        monkeypatch.setenv("BIH_ITEM_TILES", "16320")
+        g.set_param(bihrt_mod.PARAM_ITEM_TILES, 16320)
     r = bihrt_mod.Renderer(g, w, h, spp=spp)
     ref = []
     for f in range(7):
@@ -677,3 +673,76 @@ def test_render_device_frames_equals_single_frames(case, gpu, bihrt_mod, oracle_
     if rows is None and spp == 4:
         img, _ = oracle_mod.OracleTree(tris).render(w, h, frame=3)
         assert np.array_equal(b[3 * stride: 3 * stride + h * w].reshape(h, w), img)
+
+
+@pytest.fixture(scope="module")
+def soup1m(bihrt_mod, oracle_mod):
+    tris = bihrt_mod.scenes.soup(1_000_000, seed=1)
+    return tris, oracle_mod.OracleTree(tris)
+
+
+@pytest.mark.parametrize("layout", ["frame", "bands_rank3_of8"])
+def test_headline_call_shape_equals_oracle(layout, gpu, bihrt_mod, oracle_mod, soup1m):
+    """The bench's own call: bih_render_device_frames with 16 frames on the 1M
+    soup at 1920x1080 (one k_render_bins launch; per-lane XORWOW state kept in
+    LDS across the frames of an item).  Frames 0, 7 and 15 equal the oracle on
+    every 16th row; the state then carries into the next call (cudaRender's
+    persistent curandState, CUDAKernels.cu:411-419; the frame loop of
+    App.cpp:174-186).  `bands_rank3_of8`: rank 3's interleaved 8-row bands of
+    an 8-GPU split (few tiles: the item's frames are split, start states from
+    k_rng_advance)."""
+    import torch
+    from bihrt.tiling import band_rows, rows_of_rank
+    tris, ot = soup1m
+    w, h, G = 1920, 1080, 16
+    d = torch.from_numpy(tris).cuda()
+    g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
+    rows = band_rows(h, 8, 3, 8) if layout.startswith("bands") else band_rows(h, 8, 0, 1)
+    ys = rows_of_rank(h, 8, 3, 8) if layout.startswith("bands") else np.arange(h)
+    r = bihrt_mod.Renderer(g, w, h)
+    g.reserve(w, h, 4, rows, G)
+    stride = rows.nrows * w
+    buf = torch.full((2 * G * stride,), -1, dtype=torch.int32, device="cuda")
+    r.render_device_frames(buf.data_ptr(), 0, G, stride, rows=rows)
+    r.render_device_frames(buf.data_ptr() + 4 * G * stride, G, G, stride, rows=rows)   # frames 16..31
+    r.sync()
+    fr = buf.cpu().numpy().view(np.uint32).reshape(2 * G, rows.nrows, w)
+    assert g.bins_stats().usable
+    pick = np.arange(0, ys.size, 16)                   # every 16th local row
+    for f in (0, 7, 15, 16, 31):
+        ref = np.stack([ot.render(w, h, frame=f, rows=(int(y), 1, 1), mode=oracle_mod.MODE_GPU_ANYHIT,
+                                  threads=0)[0][0] for y in ys[pick]])
+        assert np.array_equal(fr[f][pick], ref), (layout, f, int((fr[f][pick] != ref).sum()))
+    assert not np.array_equal(fr[0], fr[15])           # the jitter moves between frames
+
+
+def test_steady_frame_loop_allocates_nothing(gpu, bihrt_mod):
+    """After bih_reserve and one call per camera, a frame loop of 16- and
+    4-frame calls on three streams (the bench's headline shape) makes no
+    device allocation (bih_tree_info.device_allocs stays put)."""
+    import torch
+    tris = bihrt_mod.scenes.soup(200_000, seed=3)
+    w, h, G = 960, 540, 16
+    g = bihrt_mod.GPUArrayManager(tris)
+    g.reserve(w, h, 4, None, G)
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.zeros(G * h * w, dtype=torch.int32, device="cuda") for _ in range(3)]
+    r.render_device_frames(outs[0].data_ptr(), 0, 5, h * w, stream=streams[0].cuda_stream)   # camera structures
+    torch.cuda.synchronize()
+    a0 = g.info().device_allocs
+    f = 5
+    for k, m in enumerate([16, 4, 16, 16, 4, 1, 16]):
+        r.render_device_frames(outs[k % 3].data_ptr(), f, m, h * w, stream=streams[k % 3].cuda_stream)
+        f += m
+    torch.cuda.synchronize()
+    assert g.info().device_allocs == a0
+    # without the reservation the first 16-frame call grows the per-call buffers
+    g2 = bihrt_mod.GPUArrayManager(tris)
+    r2 = bihrt_mod.Renderer(g2, w, h)
+    r2.render_device_frames(outs[0].data_ptr(), 0, 5, h * w)
+    r2.sync()
+    b0 = g2.info().device_allocs
+    r2.render_device_frames(outs[1].data_ptr(), 5, 16, h * w)
+    r2.sync()
+    assert g2.info().device_allocs > b0
