@@ -720,11 +720,31 @@ def whitted(args, bihrt, torch, arrays, SPP, sptr):
     wel = (time.perf_counter() - t0) / args.whitted_frames
     wk, _ = rw.last_render_times()
     rw.set_timing(False)
+    # work of one more frame (untimed, counters on): per bounce the rays, the
+    # nodes their walks entered and the triangles they tested; algorithmic
+    # bytes = 16 B per node record + 36 B per triangle record ({v0, e1, e2})
+    # + 28 B per ray read from its queue and, for rays that hit, written to
+    # the next one -- over the trace kernels' time (wk)
+    arrays.set_param(bihrt.PARAM_WHITTED_COUNTERS, 1)
+    rw.render_whitted_device(wout.data_ptr(), 1 + args.whitted_frames, stream=sptr)
+    work = rw.whitted_work()
+    arrays.set_param(bihrt.PARAM_WHITTED_COUNTERS, 0)
+    torch.cuda.synchronize()
     del wout
+    nodes, tris_t, rays = sum(work["nodes"]), sum(work["tris"]), sum(work["rays"])
+    alg = 16 * nodes + 36 * tris_t + 28 * rays + 28 * sum(work["rays"][1:])
+    work_leg = {"per_bounce": work, "nodes_per_ray": nodes / max(1, rays), "tris_per_ray": tris_t / max(1, rays),
+                "algorithmic_bytes": alg,
+                "formula": "16 x nodes + 36 x triangles tested + 28 x rays read + 28 x rays written",
+                "algorithmic_gbs": alg / (wk * 1e-3) / 1e9 if wk else None,
+                "frac_of_hbm_peak": alg / (wk * 1e-3) / 1e9 / HBM_PEAK_GBS if wk else None,
+                "note": "records are re-read from L2/MALL far more than from HBM (the tree and soup are "
+                        "52 MB): the bound is the per-lane gather rate of the walk, not HBM bandwidth"}
     return {"config": "C4: 1M soup, 3840x2160, 4 spp, 8 bounces of mirror rays",
             "ms_per_frame": 1e3 * wel, "primary_rays_per_s": WW * WH * SPP / wel,
             "rays_traced_per_frame": traced, "rays_traced_per_s": traced / wel,
             "trace_kernels_ms": wk, "hit_histogram": hist, "frames": args.whitted_frames,
+            "work": work_leg,
             "note": "k_wh_gen + 9 x k_wh_trace (closest hit, per-lane walk, ballot/mbcnt "
                     "compaction of live rays between bounces) + k_wh_shade; bit-exact vs the "
                     "oracle (tests/test_whitted.py)"}

@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 from . import scenes  # noqa: F401
-from ._lib import (PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_ITEM_TILES, PARAM_PAIR_CAP, TRAVERSE_ANYHIT,
+from ._lib import (PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_ITEM_TILES, PARAM_PAIR_CAP, PARAM_WHITTED_COUNTERS,
+                   TRAVERSE_ANYHIT,
                    TRAVERSE_REFERENCE, BihError, Camera, Framebuffer, Rows, Scene, TreeInfo, check, load)
 from . import _lib
 
@@ -200,6 +201,15 @@ class Renderer:
                                                C.c_void_p(out_ptr), C.c_void_p(hits_ptr or 0),
                                                C.c_void_p(stream or 0)), "bih_render_whitted_device")
 
+    def whitted_work(self) -> dict:
+        """Per bounce d = 0..8 of the last Whitted render (run with
+        PARAM_WHITTED_COUNTERS on): rays traced, BIH nodes entered, triangles
+        tested (bih_whitted_work)."""
+        n = 9
+        rays, nodes, tris = (C.c_uint32 * n)(), (C.c_uint64 * n)(), (C.c_uint64 * n)()
+        check(load().bih_whitted_work(self.arrays.handle, rays, nodes, tris), "bih_whitted_work")
+        return {"rays": list(rays), "nodes": list(nodes), "tris": list(tris)}
+
     def sync(self, stream: int | None = None):
         check(load().bih_sync(self.arrays.handle, C.c_void_p(stream or 0)), "bih_sync")
 
@@ -265,4 +275,5 @@ def write_ppm(path: str, img: np.ndarray):
 
 __all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
            "camera_ray_bound", "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
-           "TRAVERSE_REFERENCE", "PARAM_ITEM_TILES", "PARAM_PAIR_CAP", "PARAM_BINS_CAP", "PARAM_FORCE_FALLBACK"]
+           "TRAVERSE_REFERENCE", "PARAM_ITEM_TILES", "PARAM_PAIR_CAP", "PARAM_BINS_CAP", "PARAM_FORCE_FALLBACK",
+           "PARAM_WHITTED_COUNTERS"]

@@ -22,7 +22,7 @@ ERRORS = {
     -8: "BIH_ERR_IO", -9: "BIH_ERR_PARSE",
 }
 TRAVERSE_ANYHIT, TRAVERSE_REFERENCE = 0, 1
-PARAM_ITEM_TILES, PARAM_PAIR_CAP, PARAM_BINS_CAP, PARAM_FORCE_FALLBACK = 1, 2, 3, 4   # bih_tree_set_param
+PARAM_ITEM_TILES, PARAM_PAIR_CAP, PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_WHITTED_COUNTERS = 1, 2, 3, 4, 5   # bih_tree_set_param
 (ARR_MORTON_SORTED, ARR_TRI_INDEX, ARR_UNIQUE_MC, ARR_DUP_COUNT, ARR_FIRST_IDX, ARR_LEAF_PARENT,
  ARR_CLIP, ARR_AXIS, ARR_CHILDREN, ARR_IS_LEAF, ARR_PARENT, ARR_TRI_LO, ARR_TRI_HI) = range(13)
 
@@ -137,11 +137,12 @@ def load():
     L.bih_bins_get_stats.argtypes = [vp, C.POINTER(BinsStats)]
     L.bih_reserve.argtypes = [vp, u32, u32, u32, C.POINTER(Rows), u32]
     L.bih_tree_set_param.argtypes = [vp, i32, u64]
+    L.bih_whitted_work.argtypes = [vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64)]
     for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
                  "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_last_render_times", "bih_set_timing",
                  "bih_render_whitted_device", "bih_render_whitted", "bih_render_device_frames",
-                 "bih_bins_get_stats", "bih_reserve", "bih_tree_set_param"):
+                 "bih_bins_get_stats", "bih_reserve", "bih_tree_set_param", "bih_whitted_work"):
         getattr(L, name).restype = i32
     _lib = L
     return L

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <utility>
 #include <float.h>
 
 #include "bih_internal.h"
@@ -253,13 +254,8 @@ __device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
     return v;
 }
 
-__global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ lo,
-                                                     const float *__restrict__ hi,
-                                                     const TreeHeader *__restrict__ hdr, uint32_t n,
-                                                     uint32_t *__restrict__ keys,
-                                                     uint32_t *__restrict__ vals) {
-    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ uint32_t morton_code(const float *__restrict__ lo, const float *__restrict__ hi,
+                                                const TreeHeader *__restrict__ hdr, uint32_t i) {
     float q[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -269,9 +265,39 @@ __global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ l
         float x = (num / den) * 1024.0f;
         q[a] = fminf(fmaxf(x, 0.0f), 1023.0f);
     }
-    keys[i] = expand_bits((uint32_t)q[0]) * 4 + expand_bits((uint32_t)q[1]) * 2 +
-              expand_bits((uint32_t)q[2]);
-    vals[i] = i;
+    return expand_bits((uint32_t)q[0]) * 4 + expand_bits((uint32_t)q[1]) * 2 + expand_bits((uint32_t)q[2]);
+}
+
+// Radix sort digits: 3 passes of 10 bits cover the 30-bit codes.
+constexpr int kRdBits = 10;
+constexpr uint32_t kRdBins = 1u << kRdBits;
+constexpr int kRdPasses = 3;
+
+// Block b's tile [b kRsTile, (b+1) kRsTile): codes and indices, and the tile's
+// counts of the first digit (hist[digit * nblocks + b], k_rs_scatter10's
+// layout) -- the first pass's histogram without a pass of its own.
+__global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ lo,
+                                                     const float *__restrict__ hi,
+                                                     const TreeHeader *__restrict__ hdr, uint32_t n,
+                                                     uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals,
+                                                     uint32_t *__restrict__ hist, uint32_t nblocks) {
+    __shared__ uint32_t h[kRdBins];
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) h[k] = 0u;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+#pragma unroll 4
+    for (int r = 0; r < kRsItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+        if (i < n) {
+            const uint32_t key = morton_code(lo, hi, hdr, (uint32_t)i);
+            keys[i] = key;
+            vals[i] = (uint32_t)i;
+            atomicAdd(&h[key & (kRdBins - 1u)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -326,10 +352,12 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     }
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
-    if (threadIdx.x == 0) {
-        const uint32_t prefix = dev::lookback_prefix(status, tile, tag, tot);
-        s_prefix = prefix;
-        if (tile == gridDim.x - 1 && total_out) *total_out = prefix + tot;
+    if (threadIdx.x < 64) {
+        const uint32_t prefix = dev::lookback_prefix_wave(status, tile, tag, tot, threadIdx.x);
+        if (threadIdx.x == 0) {
+            s_prefix = prefix;
+            if (tile == gridDim.x - 1 && total_out) *total_out = prefix + tot;
+        }
     }
     __syncthreads();
     uint32_t run = s_prefix + ex;
@@ -354,102 +382,154 @@ hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// Stable LSD radix sort of (key, value), 8-bit digits; 30-bit keys need
-// 4 passes.  Stability = thrust::stable_sort_by_key semantics.
+// Stable LSD radix sort of (key, value): 3 passes of 10-bit digits over the
+// 30-bit codes (thrust::stable_sort_by_key semantics, Renderer.cpp:441-445).
+// A pass is the digit counts of every block tile (k_morton for the first
+// digit, k_rs_hist10 after), one exclusive scan over them (digit-major:
+// every tile's start for every digit), and k_rs_scatter10.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_rs_hist(const uint32_t *__restrict__ keys, uint32_t n,
-                                                      int shift, uint32_t *__restrict__ hist,
-                                                      uint32_t nblocks) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+__global__ void __launch_bounds__(kThreads) k_rs_hist10(const uint32_t *__restrict__ keys, uint32_t n,
+                                                        int shift, uint32_t *__restrict__ hist,
+                                                        uint32_t nblocks) {
+    __shared__ uint32_t h[kRdBins];
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) h[k] = 0u;
     __syncthreads();
-    uint64_t base = (uint64_t)blockIdx.x * kRsTile;
-#pragma unroll 4
-    for (int k = 0; k < kRsItems; ++k) {
-        uint64_t i = base + (uint64_t)k * kThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+    uint32_t key[kRsItems];
+#pragma unroll
+    for (int r = 0; r < kRsItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+        key[r] = i < n ? keys[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRsItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[(key[r] >> shift) & (kRdBins - 1u)], 1u);
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
 }
 
-__global__ void __launch_bounds__(kThreads) k_rs_scatter(const uint32_t *__restrict__ kin,
-                                                         const uint32_t *__restrict__ vin, uint32_t n,
-                                                         int shift,
-                                                         const uint32_t *__restrict__ hist_scan,
-                                                         uint32_t nblocks, uint32_t *__restrict__ kout,
-                                                         uint32_t *__restrict__ vout) {
-    __shared__ uint32_t run[256];
-    __shared__ uint32_t wcnt[4][256];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    run[tid] = hist_scan[(uint64_t)tid * nblocks + blockIdx.x];
+// Each wave of the block owns a contiguous quarter of the tile (kRsItems
+// rounds of 64), so the pass is stable: the waves' per-digit counts are
+// ranked once (tile start from the scan + the earlier waves' counts), then
+// each wave walks its rounds with no block barrier -- per round the lanes of
+// one digit find each other by 10 ballots, the group's first lane advances
+// the wave's digit cursor with one LDS atomic and the group reads its base
+// from that lane.
+__global__ void __launch_bounds__(kThreads) k_rs_scatter10(const uint32_t *__restrict__ kin,
+                                                           const uint32_t *__restrict__ vin, uint32_t n,
+                                                           int shift, const uint32_t *__restrict__ hist_scan,
+                                                           uint32_t nblocks, uint32_t *__restrict__ kout,
+                                                           uint32_t *__restrict__ vout) {
+    __shared__ uint32_t cnt[kThreads / 64][kRdBins];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint32_t k = tid; k < (kThreads / 64) * kRdBins; k += kThreads) (&cnt[0][0])[k] = 0u;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRsTile + (uint64_t)wave * 64u * kRsItems;
+    uint32_t key[kRsItems], val[kRsItems];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    for (int r = 0; r < kRsItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * 64u + lane;
+        key[r] = i < n ? kin[i] : 0u;
+        val[r] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRsItems; ++r) {
+        const uint64_t i = base + (uint64_t)r * 64u + lane;
+        if (i < n) atomicAdd(&cnt[wave][(key[r] >> shift) & (kRdBins - 1u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = tid; d < kRdBins; d += kThreads) {
+        uint32_t run = hist_scan[(uint64_t)d * nblocks + blockIdx.x];
+#pragma unroll
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            const uint32_t c = cnt[w][d];
+            cnt[w][d] = run;
+            run += c;
+        }
+    }
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
-    uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+#pragma unroll
     for (int r = 0; r < kRsItems; ++r) {
-        uint64_t i = base + (uint64_t)r * kThreads + tid;
-        bool valid = i < n;
-        uint32_t key = valid ? kin[i] : 0u;
-        uint32_t val = valid ? vin[i] : 0u;
-        uint32_t dg = (key >> shift) & 255u;
+        const uint64_t i = base + (uint64_t)r * 64u + lane;
+        const bool valid = i < n;
+        const uint32_t dg = (key[r] >> shift) & (kRdBins - 1u);
         unsigned long long peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            bool bit = (dg >> b) & 1u;
-            unsigned long long bb = __ballot(bit);
+        for (int b = 0; b < kRdBits; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const unsigned long long bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        uint32_t rank = __popcll(peers & lt);
-        if (valid && rank == 0) wcnt[wave][dg] = __popcll(peers);
-        __syncthreads();
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        uint32_t off = 0;
+        if (valid && rank == 0u) off = atomicAdd(&cnt[wave][dg], (uint32_t)__popcll(peers));
+        const uint32_t leader = valid ? (uint32_t)__builtin_ctzll(peers) : lane;
+        off = (uint32_t)__shfl((int)off, (int)leader, 64);
         if (valid) {
-            uint32_t off = run[dg] + rank;
-            for (int w = 0; w < wave; ++w) off += wcnt[w][dg];
-            kout[off] = key;
-            vout[off] = val;
+            kout[off + rank] = key[r];
+            vout[off + rank] = val[r];
         }
-        __syncthreads();
-        run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Runs of equal codes in one pass (reduce_by_key + unique_by_key_copy,
+// Renderer.cpp:450-472): a run starts where the code changes; the start
+// flags are scanned with the decoupled look-back (k_scan_onepass's), and
+// each run's first element writes its code and first index, each element
+// the leaf it falls in (DeviceTree::tri_leaf), and each run's last element
+// its end (k_karras turns ends into counts).  The last tile writes U.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ keys, uint32_t n,
+                                                   unsigned long long *status, uint32_t tag,
+                                                   uint32_t *__restrict__ umc, int32_t *__restrict__ first,
+                                                   uint32_t *__restrict__ run_end, uint32_t *__restrict__ leaf_of,
+                                                   TreeHeader *hdr) {
+    __shared__ uint32_t lds[4];
+    __shared__ uint32_t s_prefix;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint32_t key[kScanItems + 1];   // key[0] = the code before this thread's first element
+    key[0] = (base > 0 && base - 1 < n) ? keys[base - 1] : 0u;
+    uint32_t flags = 0, sum = 0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
-        __syncthreads();
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t i = base + k;
+        key[k + 1] = i < n ? keys[i] : 0u;
+        const bool f = i < n && (i == 0 || key[k + 1] != key[k]);
+        flags |= (f ? 1u : 0u) << k;
+        sum += f ? 1u : 0u;
     }
-}
-
-// ---------------------------------------------------------------------------
-// Runs of equal codes: flags, scan, compaction (reduce_by_key +
-// unique_by_key_copy, Renderer.cpp:450-472).
-// ---------------------------------------------------------------------------
-__global__ void k_run_flags(const uint32_t *__restrict__ keys, uint32_t n, uint32_t *__restrict__ flags) {
-    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
-}
-
-// pos = the exclusive scan of the flags; rewritten in place to the leaf of
-// each sorted triangle (pos + flag - 1: DeviceTree::tri_leaf)
-__global__ void k_run_compact(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ flags,
-                              uint32_t *pos, uint32_t n,
-                              uint32_t *__restrict__ umc, int32_t *__restrict__ first) {
-    uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t f = flags[i], p = pos[i];
-    if (f) {
-        umc[p] = keys[i];
-        first[p] = (int32_t)i;
+    const uint32_t nxt = (base + kScanItems < n) ? keys[base + kScanItems] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
+    if (threadIdx.x < 64) {
+        const uint32_t prefix = dev::lookback_prefix_wave(status, tile, tag, tot, threadIdx.x);
+        if (threadIdx.x == 0) {
+            s_prefix = prefix;
+            if (tile == gridDim.x - 1) hdr->n_unique = prefix + tot;
+        }
     }
-    pos[i] = p + f - 1u;
-}
-
-__global__ void k_run_counts(const int32_t *__restrict__ first, const TreeHeader *__restrict__ hdr,
-                             uint32_t n, uint32_t *__restrict__ cnt, int32_t *__restrict__ leaf_parent) {
-    uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-    uint32_t U = hdr->n_unique;
-    if (k >= U) return;
-    int32_t e = (k + 1 < U) ? first[k + 1] : (int32_t)n;
-    cnt[k] = (uint32_t)(e - first[k]);
-    leaf_parent[k] = -1;
+    __syncthreads();
+    uint32_t run = s_prefix + ex;   // runs started before element base
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t i = base + k;
+        if (i >= n) break;
+        const bool f = (flags >> k) & 1u;
+        if (f) {
+            umc[run] = key[k + 1];
+            first[run] = (int32_t)i;
+        }
+        run += f ? 1u : 0u;
+        const uint32_t leaf = run - 1u;
+        leaf_of[i] = leaf;
+        const uint32_t after = k + 1 < kScanItems ? key[k + 2] : nxt;
+        if (i + 1 == n || after != key[k + 1]) run_end[leaf] = (uint32_t)(i + 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -457,6 +537,8 @@ __global__ void k_run_counts(const int32_t *__restrict__ first, const TreeHeader
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict__ umc,
                                                      const TreeHeader *__restrict__ hdr,
+                                                     const int32_t *__restrict__ first,
+                                                     uint32_t *__restrict__ dup_cnt,
                                                      int32_t *__restrict__ children,
                                                      uint8_t *__restrict__ is_leaf,
                                                      int32_t *__restrict__ axis_out,
@@ -465,6 +547,9 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
                                                      int2 *__restrict__ node_rng) {
     const int U = (int)hdr->n_unique;
     uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
+    // leaf idx's triangle count (m_duplicatesCnts): k_runs left the run's end
+    if (idx < (uint32_t)U) dup_cnt[idx] -= (uint32_t)first[idx];
+    if (U == 1 && idx == 0) leaf_parent[0] = -1;   // no internal node (U >= 2: every leaf gets a parent below)
     if (U < 2 || idx > (uint32_t)(U - 2)) return;
     if (idx == 0) parent[0] = -1;   // the root; every other node is written as a child below
     uint32_t cur = umc[idx];
@@ -798,7 +883,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     const uint32_t n = t.n;
     const uint64_t nn = n ? n : 1;
     const uint32_t rs_blocks = (uint32_t)((nn + kRsTile - 1) / kRsTile);
-    const uint64_t hist_n = 256ull * rs_blocks;
+    const uint64_t hist_n = (uint64_t)kRdBins * rs_blocks;
     const uint32_t max_parts =
         (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
     if (!t.hdr) {
@@ -810,7 +895,6 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.keys2, nn, t));
         BIH_TRY(dalloc(&t.vals2, nn, t));
         BIH_TRY(dalloc(&t.scan_tmp, nn + 1, t));
-        BIH_TRY(dalloc(&t.flags, nn + 1, t));
         BIH_TRY(dalloc(&t.unique_mc, nn, t));
         BIH_TRY(dalloc(&t.dup_cnt, nn, t));
         BIH_TRY(dalloc(&t.first_idx, nn, t));
@@ -847,28 +931,36 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                            t.tri_hi, t.hdr, t.prep_part);
         hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
                            t.hdr, n, t.prep_part, prep_blocks);
-        hipLaunchKernelGGL(k_morton, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi,
-                           t.hdr, n, t.keys, t.vals);
-        // 4 stable passes over 30-bit keys
+        hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
+                           t.vals, t.hist, rs_blocks);
+        // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
+        // counted the first digit); the sorted pairs end in keys2 / vals2,
+        // which then become keys / vals
         uint32_t *ka = t.keys, *va = t.vals, *kb = t.keys2, *vb = t.vals2;
-        for (int shift = 0; shift < 32; shift += 8) {
-            hipLaunchKernelGGL(k_rs_hist, dim3(rs_blocks), dim3(kThreads), 0, st, ka, n, shift,
-                               t.hist, rs_blocks);
+        for (int p = 0; p < kRdPasses; ++p) {
+            const int shift = kRdBits * p;
+            if (p > 0)
+                hipLaunchKernelGGL(k_rs_hist10, dim3(rs_blocks), dim3(kThreads), 0, st, ka, n, shift, t.hist,
+                                   rs_blocks);
             BIH_TRY(exclusive_scan(t.hist, t.hist, (uint32_t)hist_n, t.partials, nullptr, st));
-            hipLaunchKernelGGL(k_rs_scatter, dim3(rs_blocks), dim3(kThreads), 0, st, ka, va, n, shift,
-                               t.hist, rs_blocks, kb, vb);
+            hipLaunchKernelGGL(k_rs_scatter10, dim3(rs_blocks), dim3(kThreads), 0, st, ka, va, n, shift, t.hist,
+                               rs_blocks, kb, vb);
             uint32_t *tk = ka, *tv = va;
             ka = kb; va = vb; kb = tk; vb = tv;
         }
-        // after 4 passes the result is back in t.keys / t.vals
-        hipLaunchKernelGGL(k_run_flags, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.keys, n, t.flags);
-        BIH_TRY(exclusive_scan(t.flags, t.scan_tmp, n, t.partials, &t.hdr->n_unique, st));
-        hipLaunchKernelGGL(k_run_compact, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.keys, t.flags,
-                           t.scan_tmp, n, t.unique_mc, t.first_idx);
-        hipLaunchKernelGGL(k_run_counts, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.first_idx,
-                           t.hdr, n, t.dup_cnt, t.leaf_parent);
-        hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr,
-                           t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
+        static_assert(kRdPasses % 2 == 1, "an odd pass count leaves the result in keys2 / vals2");
+        std::swap(t.keys, t.keys2);
+        std::swap(t.vals, t.vals2);
+        // runs: codes, first indices, ends (k_karras: counts), leaf of each
+        // sorted triangle, U
+        {
+            const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+            hipLaunchKernelGGL(k_runs, dim3(nb), dim3(kThreads), 0, st, t.keys, n,
+                               reinterpret_cast<unsigned long long *>(t.partials), next_scan_tag(), t.unique_mc,
+                               t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr);
+        }
+        hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr, t.first_idx,
+                           t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
         const uint64_t cap = seg_capacity(nn);
         // (also the sorted triangle records when U >= 2: every leaf run)
         hipLaunchKernelGGL(k_seg_leaf, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.v,

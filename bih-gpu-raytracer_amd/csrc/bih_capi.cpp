@@ -99,6 +99,7 @@ struct TreeParams {
     uint32_t pair_cap = 0xFFFFFFFFu;  // BIH_PARAM_PAIR_CAP (~0: sized from N)
     uint64_t bins_cap = 0;            // BIH_PARAM_BINS_CAP (0: no cap)
     uint32_t force_fallback = 0;      // BIH_PARAM_FORCE_FALLBACK
+    uint32_t wh_counters = 0;         // BIH_PARAM_WHITTED_COUNTERS
 };
 static const TreeParams &env_params() {
     static const TreeParams p = [] {
@@ -186,6 +187,8 @@ struct bih_tree {
     // config C4 (bih_whitted.hip): two ray queues, counters and per-sample hits
     char *wh_mem = nullptr;
     size_t wh_rays = 0;              // queue capacity (rays)
+    uint64_t wh_last_rays = 0;       // rays of the last Whitted render (its buffer layout)
+    int wh_last_slot = -1;           // its slot (evd), when it ran with work counters
 };
 
 namespace {
@@ -1366,6 +1369,10 @@ int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
         if (value > 1) return BIH_ERR_INVALID;
         tr->prm.force_fallback = (uint32_t)value;
         return BIH_OK;
+    case BIH_PARAM_WHITTED_COUNTERS:
+        if (value > 1) return BIH_ERR_INVALID;
+        tr->prm.wh_counters = (uint32_t)value;
+        return BIH_OK;
     default:
         return BIH_ERR_INVALID;
     }
@@ -1387,7 +1394,9 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     uint64_t ylast = rows.row0 + (lr / rows.band_h) * (uint64_t)rows.band_h * rows.band_step +
                      (lr % rows.band_h);
     if (ylast >= h) return BIH_ERR_INVALID;
-    if ((uint64_t)h * w * spp > 0xFFFFFFFFull) return BIH_ERR_TOO_LARGE;   // u32 ray ids
+    // u32 ray ids, and k_wh_trace_dyn's u32 fetch counter overshoots the ray
+    // count by at most one 64-ray fetch per wave of its grid (<= 2^20 lanes)
+    if ((uint64_t)h * w * spp > 0xFFFFFFFFull - (1ull << 20)) return BIH_ERR_TOO_LARGE;
     DeviceGuard g(tr->t.device);
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
@@ -1441,9 +1450,12 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     a.rng_in = rng_buf(tr, cur);
     a.out = d_out;
     const int slot = tr->slot;
+    const bool count = tr->prm.wh_counters != 0;
     rc = bih::launch_whitted(a, tr->wh_mem, rays, d_hits, st, tr->timing ? tr->ev0[slot] : nullptr,
-                             tr->timing ? tr->ev1[slot] : nullptr);
+                             tr->timing ? tr->ev1[slot] : nullptr, count);
     if (rc) return map_hip(rc);
+    tr->wh_last_rays = rays;
+    tr->wh_last_slot = count ? slot : -1;
     if (tr->timing) {
         e = hipEventRecord(tr->ev2[slot], st);
         if (e != hipSuccess) return map_hip((int)e);
@@ -1457,6 +1469,26 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     tr->slot = (slot + 1) % kSlots;
     tr->rng_cur = nxt;
     rng_guard.armed = false;
+    return BIH_OK;
+}
+
+int bih_whitted_work(const bih_tree *ctr, uint32_t rays[BIH_WHITTED_BOUNCES + 1],
+                     uint64_t nodes[BIH_WHITTED_BOUNCES + 1], uint64_t tris[BIH_WHITTED_BOUNCES + 1]) {
+    bih_tree *tr = const_cast<bih_tree *>(ctr);
+    if (!tr || !rays || !nodes || !tris) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    // the last Whitted render, with counters on, and no Whitted render since
+    if (tr->wh_last_slot < 0 || !tr->wh_mem) return BIH_ERR_INVALID;
+    hipError_t e = hipEventSynchronize(tr->evd[tr->wh_last_slot]);
+    if (e != hipSuccess) return map_hip((int)e);
+    unsigned long long w[2 * (BIH_WHITTED_BOUNCES + 1)];
+    const int rc = bih::whitted_work(tr->wh_mem, tr->wh_last_rays, rays, w, tr->stream);
+    if (rc) return map_hip(rc);
+    for (int d = 0; d <= BIH_WHITTED_BOUNCES; ++d) {
+        nodes[d] = w[2 * d];
+        tris[d] = w[2 * d + 1];
+    }
     return BIH_OK;
 }
 

@@ -110,5 +110,49 @@ __device__ __forceinline__ uint32_t lookback_prefix(unsigned long long *status, 
     return prefix;
 }
 
+// The same look-back by one whole wave (all 64 lanes call it, `lane` =
+// 0..63; every lane returns the prefix): lane j reads predecessor j + 1 of
+// the current window, so one round trip covers 64 predecessors.  The window
+// sums the values of its leading run of published words up to the nearest
+// inclusive prefix; an unpublished word (stale tag or flag 0) ends the run
+// and the window restarts there.  Same words, same values as lookback_prefix.
+__device__ __forceinline__ uint32_t lookback_prefix_wave(unsigned long long *status, uint32_t tile,
+                                                         uint32_t tag, uint32_t tot, uint32_t lane) {
+    if (tile == 0) {
+        if (lane == 0)
+            __hip_atomic_store(status, scan_word(tag, kScanPre, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0u;
+    }
+    if (lane == 0)
+        __hip_atomic_store(status + tile, scan_word(tag, kScanAgg, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t prefix = 0;
+    uint32_t j = tile;   // predecessors j-1, j-2, .. remain (wave-uniform)
+    for (;;) {
+        const bool in = lane < j;
+        unsigned long long w = 0ull;
+        if (in) w = __hip_atomic_load(status + (j - 1u - lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = (uint32_t)(w >> 32);
+        const bool ok = in && (hi >> 2) == tag && (hi & 3u) != 0u;
+        const unsigned long long pre = __ballot(ok && (hi & 3u) == kScanPre);
+        const unsigned long long bad = __ballot(!ok);   // lanes past tile 0 are never reached (tile 0 is a prefix)
+        // lanes [0, end) are summed: up to the nearest prefix when none before it is unpublished
+        const uint32_t fp = pre ? (uint32_t)__builtin_ctzll(pre) : 64u;
+        const uint32_t fb = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+        const bool done = fp < fb;
+        const uint32_t end = done ? fp + 1u : fb;
+        uint32_t v = lane < end ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        prefix += v;
+        if (done) break;
+        j -= end;
+        if (end == 0u) __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0)
+        __hip_atomic_store(status + tile, scan_word(tag, kScanPre, prefix + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return prefix;
+}
+
 }  // namespace dev
 }  // namespace bih

@@ -181,7 +181,7 @@ struct DeviceTree {
     uint32_t *keys2 = nullptr, *vals2 = nullptr;    // sort ping-pong
     uint32_t *scan_tmp = nullptr;                   // scan scratch; after the build the leaf of
                                                     // each sorted triangle (k_run_compact)
-    uint32_t *flags = nullptr;                      // u32[N+1]
+    uint32_t *flags = nullptr;                      // (unused since round 4: k_runs)
     uint32_t *unique_mc = nullptr, *dup_cnt = nullptr;
     int32_t *first_idx = nullptr, *leaf_parent = nullptr;
     float *clip = nullptr;
@@ -209,7 +209,8 @@ const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host()
 // per sample.
 size_t whitted_bytes(uint64_t rays);
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
-                   void *ev_k1);
+                   void *ev_k1, bool count);
+int whitted_work(const void *mem, uint64_t rays, uint32_t ray_counts[9], unsigned long long work[18], void *stream);
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)

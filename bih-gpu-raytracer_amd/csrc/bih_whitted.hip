@@ -45,6 +45,7 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
 constexpr uint32_t kWCounts = 32;       // counter words: [0..9] rays per queue, [16..25] rays taken (k_wh_trace_dyn)
 constexpr uint32_t kWFetch = 16;
+constexpr uint32_t kWWorkWords = 18;    // work counters: {nodes, triangles} per bounce, u64 (k_wh_trace_dyn<true>)
 
 struct WScene {
     const uint4 *nodes;
@@ -235,10 +236,11 @@ struct WQueue {
 
 // counts[0..9]: rays in queue d (d = bounce depth)
 __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, uint32_t *counts,
-                                                uint8_t *hits) {
+                                                uint8_t *hits, uint32_t *sort_hist) {
     const uint64_t P = (uint64_t)a.nrows * a.w;
     const uint64_t rays = P * a.spp;
     const uint64_t gid = (uint64_t)blockIdx.x * kWT + threadIdx.x;
+    if (gid < 4096u) sort_hist[gid] = 0u;   // k_wh_sort_* (4096 buckets; zeroed again by each scan)
     if (gid == 0) {
         counts[0] = (uint32_t)rays;
         for (uint32_t k = 1; k < kWCounts; ++k) counts[k] = 0u;
@@ -375,9 +377,13 @@ __device__ __forceinline__ bool wray_start(const WScene &s, WRay &r) {
     r.tMax = tMax;
     return true;
 }
-// one iteration of closest_walk's loop; true when the walk has ended
-__device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, const WStack &stk) {
+// one iteration of closest_walk's loop; true when the walk has ended.
+// COUNT: nodes entered (cn) and triangles tested (ct) for the work counters.
+template <bool COUNT>
+__device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, const WStack &stk, uint32_t &cn,
+                                          uint32_t &ct) {
     auto leaf = [&](uint32_t b, uint32_t e) {
+        if (COUNT) ct += e - b;
         for (uint32_t i = b; i < e; ++i) {
             float t;
             if (mt_t(s.tris + 9ull * i, r.o[0], r.o[1], r.o[2], r.d[0], r.d[1], r.d[2], t_lo, t) &&
@@ -395,6 +401,7 @@ __device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, 
         return false;
     }
     if (best < r.tMax) r.tMax = best;
+    if (COUNT) ++cn;
     const uint4 nd = s.nodes[r.cur];
     const uint32_t ax = (nd.z >> 27) & 3u;
     const float org = pick3(ax, r.o[0], r.o[1], r.o[2]), inv = pick3(ax, r.ix, r.iy, r.iz);
@@ -445,8 +452,11 @@ __device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, 
     }
     return false;
 }
+template <bool COUNT>
 __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
-                                                      uint32_t *counts, uint8_t *hits, uint32_t *spill) {
+                                                      uint32_t *counts, uint8_t *hits, uint32_t *spill,
+                                                      unsigned long long *work) {
+    uint32_t cn = 0, ct = 0;   // COUNT: nodes entered, triangles tested by this lane
     __shared__ uint32_t s_node[kWLds * kWT];
     __shared__ float s_min[kWLds * kWT];
     __shared__ float s_max[kWLds * kWT];
@@ -472,7 +482,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
             uint32_t first = 0;
             if (lane == 0) first = atomicAdd(fetch, k);
             first = __builtin_amdgcn_readfirstlane(first);
-            if (first + k >= n) more = false;
+            if ((uint64_t)first + k >= n) more = false;   // u64: no wrap of first + k
             if (!has) {
                 const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
@@ -493,7 +503,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
         }
         bool fin = false;
         if (has)
-            for (int k = 0; k < BIH_WH_STEPS && !fin; ++k) fin = wray_step(sc, r, t_lo, stk);
+            for (int k = 0; k < BIH_WH_STEPS && !fin; ++k) fin = wray_step<COUNT>(sc, r, t_lo, stk, cn, ct);
         const bool hit = fin && r.bi != kNoHit;
         if (hit) hits[r.sid] = (uint8_t)(depth + 1);
         // the mirror ray (oracle whitted_path), then compaction into qout
@@ -529,7 +539,117 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
         }
         if (fin) has = false;
     }
+    if (COUNT) {   // work[2 depth] += nodes, work[2 depth + 1] += triangles (per wave, u64)
+        unsigned long long n64 = cn, t64 = ct;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            n64 += __shfl_xor(n64, off, 64);
+            t64 += __shfl_xor(t64, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(work + 2 * depth, n64);
+            atomicAdd(work + 2 * depth + 1, t64);
+        }
+    }
 }
+
+// Ray order of a bounce queue (round 4).  The rays of queue d+1 arrive in the
+// order their waves finished, so neighbouring lanes start unrelated walks.
+// Before bounce d+1 the queue is reordered by a key of origin cell (3 bits of
+// the scene box per axis, Morton-interleaved) x direction octant: lanes and
+// waves of one XCD then walk neighbouring subtrees, and the node / triangle
+// lines they share stay in that XCD's L2.  A counting sort (k_wh_sort_count,
+// k_wh_sort_scan, k_wh_sort_scatter); the order within a bucket is arbitrary.
+// No result depends on the queue order (each ray carries its sample id and
+// its walk is its own), so the pixels and hit counts are unchanged.
+constexpr uint32_t kWSortBits = 3;                              // cells per axis: 8
+constexpr uint32_t kWSortBuckets = 8u << (3 * kWSortBits);      // x 8 octants = 4096
+constexpr uint32_t kWSortChunk = 4096;                          // rays per sort block (16 per thread)
+__device__ __forceinline__ uint32_t wh_cell(float o, float lo, float hi) {
+    const float q = (o - lo) / (hi - lo) * (float)(1u << kWSortBits);
+    // NaN and out-of-box origins clamp (any key is correct, only the order changes)
+    return q >= 1.0f ? (q < (float)((1u << kWSortBits) - 1u) ? (uint32_t)q : (1u << kWSortBits) - 1u) : 0u;
+}
+__device__ __forceinline__ uint32_t wh_sort_key(const WScene &s, const WQueue &q, uint64_t i) {
+    uint32_t cell = 0;
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t v = wh_cell(q.p[c * q.cap + i], s.slo[c], s.shi[c]);
+        for (uint32_t b = 0; b < kWSortBits; ++b) cell |= ((v >> b) & 1u) << (3 * b + (2 - c));
+    }
+    const uint32_t oct = (q.p[3 * q.cap + i] < 0.0f ? 1u : 0u) | (q.p[4 * q.cap + i] < 0.0f ? 2u : 0u) |
+                         (q.p[5 * q.cap + i] < 0.0f ? 4u : 0u);
+    return (cell << 3) | oct;
+}
+// Per-block bucket counts of queue q's rays [blockIdx.x * chunk, +chunk) into
+// LDS; SCATTER = false adds them to the global histogram, true reserves each
+// non-zero bucket's range at its cursor and copies the rays to qout.
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_wh_sort_pass(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
+                                                      const uint32_t *counts, uint32_t *hist) {
+    __shared__ uint32_t s_cnt[kWSortBuckets];
+    __shared__ uint32_t s_base[SCATTER ? kWSortBuckets : 1];
+    const uint32_t n = counts[depth];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kWSortChunk;
+    if (c0 >= n) return;
+    for (uint32_t k = threadIdx.x; k < kWSortBuckets; k += 256) s_cnt[k] = 0u;
+    __syncthreads();
+    const WScene sc = load_wscene(a);
+    uint32_t key[kWSortChunk / 256], rank[kWSortChunk / 256];
+#pragma unroll
+    for (uint32_t r = 0; r < kWSortChunk / 256; ++r) {
+        const uint64_t i = c0 + r * 256 + threadIdx.x;
+        key[r] = i < n ? wh_sort_key(sc, qin, i) : 0u;
+        rank[r] = i < n ? atomicAdd(&s_cnt[key[r]], 1u) : 0u;
+    }
+    __syncthreads();
+    uint32_t *cur = hist + kWSortBuckets;   // [kWSortBuckets, 2 kWSortBuckets): scatter cursors
+    for (uint32_t k = threadIdx.x; k < kWSortBuckets; k += 256) {
+        const uint32_t c = s_cnt[k];
+        if (SCATTER) s_base[k] = c ? atomicAdd(cur + k, c) : 0u;
+        else if (c) atomicAdd(hist + k, c);
+    }
+    if (!SCATTER) return;
+    __syncthreads();
+    const uint32_t *sid_in = reinterpret_cast<const uint32_t *>(qin.p) + 6 * qin.cap;
+#pragma unroll
+    for (uint32_t r = 0; r < kWSortChunk / 256; ++r) {
+        const uint64_t i = c0 + r * 256 + threadIdx.x;
+        if (i >= n) continue;
+        const uint64_t j = s_base[key[r]] + rank[r];
+        float o[3], d[3];
+        for (int c = 0; c < 3; ++c) {
+            o[c] = qin.p[c * qin.cap + i];
+            d[c] = qin.p[(3 + c) * qin.cap + i];
+        }
+        qout.put(j, o, d, sid_in[i]);
+    }
+}
+// Bucket starts: cursors = exclusive scan of the histogram; the histogram is
+// zeroed for the next bounce's count (one block of 1024 threads, 4 buckets each).
+__global__ void __launch_bounds__(1024) k_wh_sort_scan(uint32_t *hist) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t v[4], sum = 0;
+    for (int k = 0; k < 4; ++k) {
+        v[k] = hist[4 * t + k];
+        sum += v[k];
+    }
+    uint32_t inc = sum;
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63u) s_w[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t k = 0; k < w; ++k) run += s_w[k];
+    for (int k = 0; k < 4; ++k) {
+        hist[kWSortBuckets + 4 * t + k] = run;
+        hist[4 * t + k] = 0u;
+        run += v[k];
+    }
+}
+static_assert(kWSortBuckets == 4 * 1024, "k_wh_sort_scan: 1024 threads x 4 buckets");
 
 // shade of a sample with h hits (oracle whitted_shade), f32
 __device__ __forceinline__ void wh_shade(uint32_t h, float &r, float &g, float &b) {
@@ -568,14 +688,34 @@ static uint32_t whitted_grid(uint64_t rays) {
     return (uint32_t)(need < cap ? need : cap);
 }
 
-// two queues of 7 planes, 16 counters, per-sample hits (u8), the stack spill
+// two queues of 7 planes, 16 counters, per-sample hits (u8), the stack
+// spill, the ray-order histogram and cursors
+static uint64_t whitted_spill_words(uint64_t rays) {
+    return (uint64_t)whitted_grid(rays) * kWT * (kWStack - kWLds) * 3;
+}
 size_t whitted_bytes(uint64_t rays) {
     const uint64_t q = 2 * 7 * rays * 4, hits = (rays + 255) & ~255ull;
-    return q + kWCounts * 4 + hits + (uint64_t)whitted_grid(rays) * kWT * (kWStack - kWLds) * 3 * 4;
+    return q + kWCounts * 4 + hits + whitted_spill_words(rays) * 4 + 2 * kWSortBuckets * 4 + kWWorkWords * 8;
+}
+// the work counters of the last launch_whitted with counters on (u64[2 x 9]:
+// nodes, triangles per bounce) and its rays per bounce (u32[9])
+int whitted_work(const void *mem, uint64_t rays, uint32_t ray_counts[9], unsigned long long work[18],
+                 void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const char *base = reinterpret_cast<const char *>(mem);
+    const uint32_t *counts = reinterpret_cast<const uint32_t *>(base + 14 * rays * 4);
+    const uint8_t *hits = reinterpret_cast<const uint8_t *>(counts + kWCounts);
+    const uint32_t *spill = reinterpret_cast<const uint32_t *>(hits + ((rays + 255) & ~255ull));
+    const unsigned long long *w =
+        reinterpret_cast<const unsigned long long *>(spill + whitted_spill_words(rays) + 2 * kWSortBuckets);
+    hipError_t e = hipMemcpyAsync(ray_counts, counts, 9 * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(work, w, 18 * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return (int)e;
 }
 
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
-                   void *ev_k1) {
+                   void *ev_k1, bool count) {
     const hipStream_t st = (hipStream_t)stream;
     if (rays == 0) return 0;
     float *base = reinterpret_cast<float *>(mem);
@@ -583,7 +723,14 @@ int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hi
     uint32_t *counts = reinterpret_cast<uint32_t *>(base + 14 * rays);
     uint8_t *hits = reinterpret_cast<uint8_t *>(counts + kWCounts);
     uint32_t *spill = reinterpret_cast<uint32_t *>(hits + ((rays + 255) & ~255ull));
-    hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits);
+    uint32_t *hist = spill + whitted_spill_words(rays);
+    unsigned long long *work = reinterpret_cast<unsigned long long *>(hist + 2 * kWSortBuckets);
+    if (count) {
+        const hipError_t ez = hipMemsetAsync(work, 0, kWWorkWords * 8, st);
+        if (ez != hipSuccess) return (int)ez;
+    }
+    hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits,
+                       hist);
     hipError_t e = ev_k0 ? hipEventRecord((hipEvent_t)ev_k0, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
     const uint32_t grid = whitted_grid(rays);
@@ -594,13 +741,31 @@ int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hi
         return !(e && e[0] == '1');
     }();
     const bool dyn = dyn_on && a.n_nodes > 0;
+    // ray order (k_wh_sort_*; BIH_WH_SORT=0 for A/B): queue d+1 is written to
+    // q1 and sorted back into q0, so every bounce reads q0
+    static const bool sort_on = [] {
+        const char *e = getenv("BIH_WH_SORT");
+        return !(e && e[0] == '0');
+    }();
+    const bool srt = sort_on && a.n_nodes > 0;
+    const uint32_t sort_blocks = (uint32_t)((rays + kWSortChunk - 1) / kWSortChunk);
     for (uint32_t d = 0; d <= 8; ++d) {
-        if (dyn)
-            hipLaunchKernelGGL(k_wh_trace_dyn, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0,
-                               (d & 1) ? q0 : q1, counts, hits, spill);
+        const WQueue &qi = (srt || !(d & 1)) ? q0 : q1, &qo = (srt || !(d & 1)) ? q1 : q0;
+        if (dyn && count)
+            hipLaunchKernelGGL(k_wh_trace_dyn<true>, dim3(grid), dim3(kWT), 0, st, a, d, qi, qo, counts, hits, spill,
+                               work);
+        else if (dyn)
+            hipLaunchKernelGGL(k_wh_trace_dyn<false>, dim3(grid), dim3(kWT), 0, st, a, d, qi, qo, counts, hits, spill,
+                               work);
         else
-            hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, (d & 1) ? q1 : q0,
-                               (d & 1) ? q0 : q1, counts, hits, spill);
+            hipLaunchKernelGGL(k_wh_trace, dim3(grid), dim3(kWT), 0, st, a, d, qi, qo, counts, hits, spill);
+        if (srt && d < 8) {
+            hipLaunchKernelGGL(k_wh_sort_pass<false>, dim3(sort_blocks), dim3(256), 0, st, a, d + 1, q1, q0,
+                               counts, hist);
+            hipLaunchKernelGGL(k_wh_sort_scan, dim3(1), dim3(1024), 0, st, hist);
+            hipLaunchKernelGGL(k_wh_sort_pass<true>, dim3(sort_blocks), dim3(256), 0, st, a, d + 1, q1, q0,
+                               counts, hist);
+        }
     }
     e = ev_k1 ? hipEventRecord((hipEvent_t)ev_k1, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;

@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define BIH_ABI_VERSION 2   /* 2: bih_tree_info.device_allocs, bih_reserve, bih_tree_set_param */
+#define BIH_ABI_VERSION 3   /* 2: bih_tree_info.device_allocs, bih_reserve, bih_tree_set_param;
+                               3: bih_whitted_work, BIH_PARAM_WHITTED_COUNTERS */
 
 /* error codes */
 #define BIH_OK               0
@@ -206,6 +207,9 @@ int bih_reserve(bih_tree *tree, uint32_t w, uint32_t h, uint32_t spp, const bih_
                                         the overflow path; 0 = none)           */
 #define BIH_PARAM_FORCE_FALLBACK  4  /* 1: every live packet of a frustum-bin
                                         render takes the exact walk (tests)    */
+#define BIH_PARAM_WHITTED_COUNTERS 5 /* 1: Whitted renders count the nodes and
+                                        triangles each bounce's walks visit
+                                        (bih_whitted_work; costs time)         */
 int bih_tree_set_param(bih_tree *tree, int param, uint64_t value);
 
 /* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)
@@ -228,6 +232,13 @@ int bih_render_whitted_device(const bih_tree *tree, const bih_camera *camera, ui
                               uint32_t *d_out, uint32_t *d_hits, void *stream);
 int bih_render_whitted(const bih_scene *scene, const bih_tree *tree, const bih_camera *camera,
                        bih_framebuffer *fb);
+/* Work of the last Whitted render, which must have run with
+ * BIH_PARAM_WHITTED_COUNTERS on (else BIH_ERR_INVALID): per bounce d = 0..8
+ * the rays traced, the BIH nodes their walks entered and the triangles they
+ * tested (the closest-hit walk of section 4.5; no counts for a one-leaf
+ * tree, whose walks have no nodes).  Waits for that render. */
+int bih_whitted_work(const bih_tree *tree, uint32_t rays[BIH_WHITTED_BOUNCES + 1],
+                     uint64_t nodes[BIH_WHITTED_BOUNCES + 1], uint64_t tris[BIH_WHITTED_BOUNCES + 1]);
 
 /* Per-render device timing (HIP events on the render stream around the main
  * render kernel and at the end of the render's device work), off by default:

@@ -40,7 +40,7 @@ def test_camera_reference_matches_oracle(bihrt_mod, oracle_mod):
 
 def test_errors_without_device(bihrt_mod):
     L = bihrt_mod._lib.load()
-    assert L.bih_abi_version() == 2
+    assert L.bih_abi_version() == 3
     assert L.bih_strerror(-2).decode().startswith("no HIP device")
     assert L.bih_strerror(12345).decode() == "unknown error"
     cam = bihrt_mod.Camera()

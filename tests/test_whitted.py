@@ -149,6 +149,37 @@ def test_whitted_matches_oracle(scene, gpu, bihrt_mod, oracle_mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["torus", "soup100k"])
+def test_whitted_work_counters_match_oracle(scene, gpu, bihrt_mod, oracle_mod):
+    """BIH_PARAM_WHITTED_COUNTERS: the rays traced, nodes entered and
+    triangles tested over all bounces equal the oracle's counters (the same
+    walk step for step), with the bounce-queue ray order on; the image is the
+    same as without counters."""
+    S = bihrt_mod.scenes
+    tris = S.torus() if scene == "torus" else S.soup(100_000, seed=2)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 160, 90
+    g.set_param(bihrt_mod.PARAM_WHITTED_COUNTERS, 1)
+    img, hits = _whitted_device(bihrt_mod, g, w, h, 1)
+    r = bihrt_mod.Renderer(g, w, h)
+    wk = r.whitted_work()
+    ref, st, dep = ot.render_whitted(w, h, frame=1, depths=True)
+    assert np.array_equal(img, ref) and np.array_equal(hits, dep)
+    assert sum(wk["rays"]) == st.slab_miss          # rays traced (oracle: slab_miss field)
+    assert sum(wk["nodes"]) == st.node_visits
+    assert sum(wk["tris"]) == st.tri_tests
+    # rays of bounce d = samples with at least d hits
+    for d in range(9):
+        assert wk["rays"][d] == int((dep >= d).sum()), d
+    g.set_param(bihrt_mod.PARAM_WHITTED_COUNTERS, 0)
+    img0, _ = _whitted_device(bihrt_mod, g, w, h, 1)
+    assert np.array_equal(img0, ref)
+    with pytest.raises(bihrt_mod.BihError):
+        r.whitted_work()                               # the last render had no counters
+
+
+@pytest.mark.gpu
 def test_whitted_1m_512x288_matches_oracle(gpu, bihrt_mod, oracle_mod):
     """C4's scene (1M-triangle soup) at 512x288, every pixel and every
     sample's hit count against the oracle."""
