@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 // Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
 // (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
-// by k_prep_final.  The build is a deterministic function of the soup, so an
+// by k_prep's last block (prep_final).  The build is a deterministic function of the soup, so an
 // unchanged hash after a rebuild means an unchanged tree, and the per-camera
 // structures derived from it (bih_capi.cpp finish_build) stay valid.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -77,111 +77,11 @@ __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float 
     M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
 }
 
-// k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
-// the scene AABB.  The reference folds triangles sequentially with
-// std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
-// as the lo of the LAST triangle attaining the minimum and sceneHi as the hi
-// of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
-// Ties only differ in the sign of zero; we reduce (value, index) keys.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
-                                                   float *__restrict__ lo, float *__restrict__ hi,
-                                                   TreeHeader *hdr,
-                                                   unsigned long long *__restrict__ part) {
-    unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
-    uint32_t bad = 0;
-    uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
-        const float *p = v + 9ull * i;
-        float q[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) q[k] = p[k];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) content_word(__float_as_uint(q[k]), 9u * i + (uint32_t)k, hx, hy);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
-            bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
-            float m, M;
-            axis_minmax(x0, x1, x2, m, M);
-            lo[3ull * i + a] = m;
-            hi[3ull * i + a] = M;
-            unsigned long long tie = 0xFFFFFFFFull - i;
-            unsigned long long km = ((unsigned long long)lt_key(m) << 32) | tie;
-            unsigned long long kM = ((unsigned long long)lt_key(M) << 32) | tie;
-            kmin[a] = km < kmin[a] ? km : kmin[a];   // smallest value, ties -> largest i
-            kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
-        }
-    }
-    // wave reduce, block reduce through LDS, one partial per block (the
-    // single-block k_prep_final folds them: no contended atomics)
-    __shared__ unsigned long long s_key[7][kThreads / 64];
-    __shared__ uint32_t s_bad[kThreads / 64];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        for (int off = 32; off > 0; off >>= 1) {
-            unsigned long long om = __shfl_xor(kmin[a], off);
-            unsigned long long oM = __shfl_xor(kmax[a], off);
-            kmin[a] = om < kmin[a] ? om : kmin[a];
-            kmax[a] = oM > kmax[a] ? oM : kmax[a];
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        hx ^= __shfl_xor(hx, off);
-        hy ^= __shfl_xor(hy, off);
-    }
-    const unsigned long long anybad = __ballot(bad);
-    const uint32_t wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            s_key[a][wv] = kmin[a];
-            s_key[3 + a][wv] = kmax[a];
-        }
-        s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
-        s_bad[wv] = anybad ? 1u : 0u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 7) {
-        const int a = threadIdx.x;
-        unsigned long long r = s_key[a][0];
-        for (uint32_t w = 1; w < kThreads / 64; ++w) {
-            const unsigned long long o = s_key[a][w];
-            r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
-        }
-        part[(size_t)a * gridDim.x + blockIdx.x] = r;
-    }
-    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
-        uint32_t b = 0;
-        for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
-        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
-    }
-}
-
-__global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
-    int a = threadIdx.x;
-    if (a < 3) {
-        hdr->scene_lo[a] = 0.f;
-        hdr->scene_hi[a] = 0.f;
-        hdr->lo_key[a] = ~0ull;
-        hdr->hi_key[a] = 0ull;
-    }
-    if (a == 0) {
-        hdr->n_tris = n;
-        hdr->n_unique = 0;
-        hdr->nonfinite = 0;
-        hdr->pad0 = 0;
-        hdr->content = 0ull;
-    }
-}
-
-
-__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
-                                                         const float *__restrict__ lo,
-                                                         const float *__restrict__ hi,
-                                                         TreeHeader *hdr, uint32_t n,
-                                                         const unsigned long long *__restrict__ part,
-                                                         uint32_t nparts) {
+// The fold of k_prep's per-block partials into the header (the scene AABB
+// with the reference's tie rules, the content hash, the non-finite flag):
+// run by k_prep's last block to finish (no launch of its own).
+__device__ void prep_final(const float *__restrict__ v, const float *lo, const float *hi, TreeHeader *hdr,
+                           uint32_t n, const unsigned long long *part, uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
     __shared__ unsigned long long s_red[8][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -241,6 +141,119 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
     hdr->scene_hi[a] = (seed < mx) ? mx : seed;
     hdr->n_tris = n;
 }
+
+// k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
+// the scene AABB.  The reference folds triangles sequentially with
+// std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
+// as the lo of the LAST triangle attaining the minimum and sceneHi as the hi
+// of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
+// Ties only differ in the sign of zero; we reduce (value, index) keys.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
+                                                   float *__restrict__ lo, float *__restrict__ hi,
+                                                   TreeHeader *hdr,
+                                                   unsigned long long *__restrict__ part) {
+    unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
+    uint32_t bad = 0;
+    uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const float *p = v + 9ull * i;
+        float q[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) content_word(__float_as_uint(q[k]), 9u * i + (uint32_t)k, hx, hy);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
+            bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
+            float m, M;
+            axis_minmax(x0, x1, x2, m, M);
+            lo[3ull * i + a] = m;
+            hi[3ull * i + a] = M;
+            unsigned long long tie = 0xFFFFFFFFull - i;
+            unsigned long long km = ((unsigned long long)lt_key(m) << 32) | tie;
+            unsigned long long kM = ((unsigned long long)lt_key(M) << 32) | tie;
+            kmin[a] = km < kmin[a] ? km : kmin[a];   // smallest value, ties -> largest i
+            kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
+        }
+    }
+    // wave reduce, block reduce through LDS, one partial per block (the
+    // last block folds them in prep_final: no contended atomics)
+    __shared__ unsigned long long s_key[7][kThreads / 64];
+    __shared__ uint32_t s_bad[kThreads / 64];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long om = __shfl_xor(kmin[a], off);
+            unsigned long long oM = __shfl_xor(kmax[a], off);
+            kmin[a] = om < kmin[a] ? om : kmin[a];
+            kmax[a] = oM > kmax[a] ? oM : kmax[a];
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        hx ^= __shfl_xor(hx, off);
+        hy ^= __shfl_xor(hy, off);
+    }
+    const unsigned long long anybad = __ballot(bad);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            s_key[a][wv] = kmin[a];
+            s_key[3 + a][wv] = kmax[a];
+        }
+        s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
+        s_bad[wv] = anybad ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        const int a = threadIdx.x;
+        unsigned long long r = s_key[a][0];
+        for (uint32_t w = 1; w < kThreads / 64; ++w) {
+            const unsigned long long o = s_key[a][w];
+            r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+        }
+        part[(size_t)a * gridDim.x + blockIdx.x] = r;
+    }
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by prep_final)
+        uint32_t b = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
+        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
+    }
+    // the last block to finish folds every block's partials (threadfence
+    // reduction: release before the arrival count, acquire after it); the
+    // count word after the partials is zero at allocation and reset here
+    __shared__ bool s_last;
+    __threadfence();
+    __syncthreads();
+    unsigned long long *arrivals = part + 8ull * kPrepBlocks;
+    if (threadIdx.x == 0) s_last = atomicAdd(arrivals, 1ull) == gridDim.x - 1ull;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (threadIdx.x == 0) *arrivals = 0ull;
+    prep_final(v, lo, hi, hdr, n, part, gridDim.x);
+}
+
+__global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
+    int a = threadIdx.x;
+    if (a < 3) {
+        hdr->scene_lo[a] = 0.f;
+        hdr->scene_hi[a] = 0.f;
+        hdr->lo_key[a] = ~0ull;
+        hdr->hi_key[a] = 0ull;
+    }
+    if (a == 0) {
+        hdr->n_tris = n;
+        hdr->n_unique = 0;
+        hdr->nonfinite = 0;
+        hdr->pad0 = 0;
+        hdr->content = 0ull;
+    }
+}
+
+
 
 // ---------------------------------------------------------------------------
 // k_morton: centre (App.cpp:128-131), normalise (:144-156), morton3D
@@ -770,6 +783,39 @@ __device__ __forceinline__ float seg_query(const float *__restrict__ seg, uint64
     return res;
 }
 
+// seg_query with every load issued before any is combined (the segment
+// nodes of a query follow from a, b and the level sizes alone, not from the
+// values loaded): one memory round trip per query instead of one per level.
+// Same nodes, and tmax / tmin are associative and commutative: the same
+// result bit for bit.  Levels: ceil(log2(nn)) + 1 <= 28 for nn <= 2^27.
+#ifndef BIH_FIT_PIPE
+#define BIH_FIT_PIPE 1
+#endif
+constexpr int kSegMaxLevels = 28;
+template <bool HI>
+__device__ __forceinline__ float seg_query_pipe(const float *__restrict__ seg, uint64_t nn, uint32_t a,
+                                                uint32_t b) {
+    const float ident = __uint_as_float(HI ? kMaxKeyBits : kMinKeyBits);
+    float x[2 * kSegMaxLevels];
+    uint32_t l = a, r = b + 1u;
+    uint64_t off = 0, size = nn;
+#pragma unroll
+    for (int lv = 0; lv < kSegMaxLevels; ++lv) {
+        const bool act = l < r;
+        const bool tl = act && (l & 1u), tr = act && (r & 1u);
+        x[2 * lv] = tl ? seg[off + l] : ident;
+        x[2 * lv + 1] = tr ? seg[off + r - 1u] : ident;
+        l = (l + (tl ? 1u : 0u)) >> 1;
+        r = (r - (tr ? 1u : 0u)) >> 1;
+        off += size;
+        size = (size + 1) / 2;
+    }
+    float res = ident;
+#pragma unroll
+    for (int k = 0; k < 2 * kSegMaxLevels; ++k) res = HI ? tmax(res, x[k]) : tmin(res, x[k]);
+    return res;
+}
+
 __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
                                                   const int2 *__restrict__ node_rng,
                                                   const int32_t *__restrict__ children,
@@ -782,8 +828,13 @@ __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__
     const int2 rg = node_rng[p];
     const uint32_t split = (uint32_t)children[2 * p];
     const int ax = axis[p];
+#if BIH_FIT_PIPE
+    const float lhi = seg_query_pipe<true>(seg + (3 + ax) * cap, nn, (uint32_t)rg.x, split);
+    const float rlo = seg_query_pipe<false>(seg + ax * cap, nn, split + 1u, (uint32_t)rg.y);
+#else
     const float lhi = seg_query<true>(seg + (3 + ax) * cap, nn, (uint32_t)rg.x, split);
     const float rlo = seg_query<false>(seg + ax * cap, nn, split + 1u, (uint32_t)rg.y);
+#endif
     clip[2 * p] = tmax(-FLT_MAX, lhi);          // initial values GPUArrayManager.cpp:79-80
     clip[2 * p + 1] = tmin(FLT_MAX, rlo);
 }
@@ -910,7 +961,8 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
         BIH_TRY(dalloc(&t.hist, hist_n, t));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, t));
+        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks + 1, t));   // + k_prep's arrival count
+        BIH_TRY(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, sizeof(unsigned long long), st));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
         // tag): stale data in fresh memory must not pass for a predecessor's
         // published prefix; afterwards every word carries an older call's
@@ -922,15 +974,13 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     BIH_TRY(hipEventCreate(&e1));
     BIH_TRY(hipEventRecord(e0, st));
 
-    // header reset (no triangles; otherwise k_prep_final writes the header)
+    // header reset (no triangles; otherwise k_prep's last block writes the header)
     if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
                            t.tri_hi, t.hdr, t.prep_part);
-        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
-                           t.hdr, n, t.prep_part, prep_blocks);
         hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
                            t.vals, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton

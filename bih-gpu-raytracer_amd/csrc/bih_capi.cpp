@@ -124,6 +124,13 @@ static uint32_t dbg_bits() {
 
 struct bih_tree {
     bih::DeviceTree t;
+    // Rebuilds write the other tree and swap (double buffering): renders of
+    // the current tree still in flight keep reading theirs while the next one
+    // is built.  gen counts swaps; slot_gen[k] = the generation render slot k
+    // read, so a rebuild waits only for the renders that read `back`.
+    bih::DeviceTree back;
+    uint32_t gen = 0;
+    uint32_t slot_gen[kSlots] = {};
     TreeParams prm = env_params();
     uint64_t allocs = 0;             // hipMalloc calls of the render side (+ t.allocs: the builder's)
     hipStream_t stream = nullptr;
@@ -309,16 +316,45 @@ int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &
     return BIH_OK;
 }
 
+// Orders `st` after every render in flight that read a tree of an older
+// generation than the current one (the buffers `back` holds).
+int wait_old_tree_readers(bih_tree *tr, hipStream_t st) {
+    for (int k = 0; k < kSlots; ++k)
+        if (tr->used[k] && tr->slot_gen[k] != tr->gen) {
+            hipError_t e = hipStreamWaitEvent(st, tr->evd[k], 0);
+            if (e != hipSuccess) return map_hip((int)e);
+        }
+    return BIH_OK;
+}
+
 int finish_build(bih_tree *tr) {
-    // a render launched through this tree may still read the buffers the
-    // build rewrites (it may run on another stream): order after it
-    int rc = wait_renders(tr, tr->stream);
-    if (rc) return rc;
     float ms = 0.f;
     const bool had = tr->built;
     const uint64_t old_content = tr->t.content;
     const uint32_t old_n = tr->t.n, old_u = tr->t.u;
-    int e = bih::build_tree_device(tr->t, tr->stream, &ms);
+    int e = 0;
+    if (!had) {
+        // first build (or after a failed one): in place, after every render
+        // launched through this tree (it may run on another stream)
+        int rc = wait_renders(tr, tr->stream);
+        if (rc) return rc;
+        e = bih::build_tree_device(tr->t, tr->stream, &ms);
+    } else {
+        // rebuild into `back` (allocated by its first build): only the
+        // renders that read it -- older generations -- are waited for; the
+        // renders of the current tree run on beside the build
+        int rc = wait_old_tree_readers(tr, tr->stream);
+        if (rc) return rc;
+        bih::DeviceTree &b = tr->back;
+        if (!b.owns_v) b.v = tr->t.v;   // the same soup (the owning copy is t's or b's)
+        b.n = tr->t.n;
+        b.device = tr->t.device;
+        e = bih::build_tree_device(b, tr->stream, &ms);
+        if (e == 0 || e == -1000) {
+            std::swap(tr->t, tr->back);
+            ++tr->gen;
+        }
+    }
     tr->build_ms = ms;
     tr->built = e == 0;
     // the per-pixel RNG state does not depend on the geometry: a rebuild (the
@@ -334,12 +370,14 @@ int finish_build(bih_tree *tr) {
             c.bins_valid = false;
         }
     if (e) return map_hip(e);
-    // renders issued on other streams order after the (re)build; tr->stream
-    // waited for every render above, so this also follows the last advance
-    hipError_t he = hipEventRecord(tr->ev_rng, tr->stream);
-    if (he == hipSuccess) he = hipEventRecord(tr->ev_tree, tr->stream);
+    // renders issued on other streams order after the (re)build (every
+    // render and camera build waits on ev_tree).  A first build waited for
+    // every render, so it also follows the last advance of the XORWOW ring;
+    // a rebuild did not, and leaves ev_rng to the renders
+    hipError_t he = hipEventRecord(tr->ev_tree, tr->stream);
+    if (he == hipSuccess && !had) he = hipEventRecord(tr->ev_rng, tr->stream);
     if (he != hipSuccess) return map_hip((int)he);
-    tr->rng_pending = true;
+    if (!had) tr->rng_pending = true;
     tr->tree_pending = true;
     return BIH_OK;
 }
@@ -509,6 +547,7 @@ void bih_free(bih_tree *tr) {
     for (CamSet &c : tr->cs)
         if (c.bins_pending) (void)hipEventSynchronize(c.ev_bins);
     bih::free_tree_device(tr->t);
+    bih::free_tree_device(tr->back);   // (the soup is freed by whichever tree owns it)
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
@@ -560,13 +599,13 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // records, and the per-slot tile queues, spill areas and chunk orders
     size_t cam = 0;
     for (const CamSet &c : tr->cs) cam += c.prim_cap + c.bins_mem_cap + c.bin_list_cap * kEntryBytes + c.q_cap;
-    info->device_bytes = tr->t.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
+    info->device_bytes = tr->t.bytes + tr->back.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
                           (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
     info->build_ms = tr->build_ms;
-    info->device_allocs = tr->allocs + tr->t.allocs;
+    info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
     return BIH_OK;
 }
 
@@ -1282,6 +1321,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
+    tr->slot_gen[slot] = tr->gen;
     tr->slot_cs[slot] = ci;
     tr->cs_cur = ci;
     tr->last_slot = slot;
@@ -1408,6 +1448,10 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
         hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
+    if (tr->tree_pending) {   // the last (re)build (a rebuild does not order ev_rng)
+        hipError_t e = hipStreamWaitEvent(st, tr->ev_tree, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
     RngGuard rng_guard{tr};
@@ -1464,6 +1508,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
+    tr->slot_gen[slot] = tr->gen;
     tr->slot_cs[slot] = -1;            // reads no camera set
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;

@@ -45,6 +45,7 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
 constexpr uint32_t kWCounts = 32;       // counter words: [0..9] rays per queue, [16..25] rays taken (k_wh_trace_dyn)
 constexpr uint32_t kWFetch = 16;
+constexpr uint32_t kWSortBucketsGen = 4096;   // = kWSortBuckets (below): k_wh_gen zeroes the histogram
 constexpr uint32_t kWWorkWords = 18;    // work counters: {nodes, triangles} per bounce, u64 (k_wh_trace_dyn<true>)
 
 struct WScene {
@@ -240,7 +241,8 @@ __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, ui
     const uint64_t P = (uint64_t)a.nrows * a.w;
     const uint64_t rays = P * a.spp;
     const uint64_t gid = (uint64_t)blockIdx.x * kWT + threadIdx.x;
-    if (gid < 4096u) sort_hist[gid] = 0u;   // k_wh_sort_* (4096 buckets; zeroed again by each scan)
+    // k_wh_sort_*'s histogram (zeroed again by each scan), whatever the grid
+    for (uint64_t k = gid; k < kWSortBucketsGen; k += (uint64_t)gridDim.x * kWT) sort_hist[k] = 0u;
     if (gid == 0) {
         counts[0] = (uint32_t)rays;
         for (uint32_t k = 1; k < kWCounts; ++k) counts[k] = 0u;
@@ -650,6 +652,7 @@ __global__ void __launch_bounds__(1024) k_wh_sort_scan(uint32_t *hist) {
     }
 }
 static_assert(kWSortBuckets == 4 * 1024, "k_wh_sort_scan: 1024 threads x 4 buckets");
+static_assert(kWSortBuckets == kWSortBucketsGen, "k_wh_gen zeroes every bucket");
 
 // shade of a sample with h hits (oracle whitted_shade), f32
 __device__ __forceinline__ void wh_shade(uint32_t h, float &r, float &g, float &b) {

@@ -37,14 +37,30 @@ def test_build_matches_oracle_edge(name, gpu, bihrt_mod, oracle_mod):
     _tree_equal(g.arrays(), ot)
 
 
-@pytest.mark.parametrize("n,seed", [(1000, 11), (70_000, 1), (300_000, 2), (1_000_000, 1),
-                                    (10_000_000, 1)])
+@pytest.mark.parametrize("n,seed", [(1000, 11), (4097, 3), (70_000, 1), (123_457, 5), (300_000, 2),
+                                    (1_000_000, 1), (10_000_000, 1)])
 def test_build_matches_oracle_soup(n, seed, gpu, bihrt_mod, oracle_mod):
     """Every canonical array bit-equal, up to SURVEY 8f-1's 10M triangles
     (where the segment tree of k_seg_up takes 3 launches)."""
     tris = bihrt_mod.scenes.soup(n, seed=seed)
     g = bihrt_mod.GPUArrayManager(tris)
     ot = oracle_mod.OracleTree(tris)
+    _tree_equal(g.arrays(), ot)
+
+
+def test_build_skewed_codes(gpu, bihrt_mod, oracle_mod):
+    """300k triangles packed into a tiny cluster plus two far corners: almost
+    every code shares its top digits (one radix bucket holds nearly all keys,
+    whole waves rank as one peer group) and many codes repeat (long runs)."""
+    rng = np.random.default_rng(7)
+    n = 300_000
+    c = rng.uniform(0.0, 1e-3, size=(n, 1, 3)).astype(np.float32)
+    tris = (c + rng.uniform(-1e-4, 1e-4, size=(n, 3, 3))).astype(np.float32)
+    tris[0] = np.array([[-5, -5, -5], [-4.9, -5, -5], [-5, -4.9, -5]], np.float32)
+    tris[n // 2] = np.array([[5, 5, 5], [4.9, 5, 5], [5, 4.9, 5]], np.float32)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    assert g.info().n_unique == ot.U < n // 4
     _tree_equal(g.arrays(), ot)
 
 
@@ -65,13 +81,20 @@ def test_build_torus(gpu, bihrt_mod, oracle_mod):
 
 
 def test_rebuild_deterministic(gpu, bihrt_mod):
+    """Rebuilds alternate between two tree buffers (double buffering): each
+    one, into either buffer, exports the first build's arrays byte for byte,
+    and the back buffer is allocated once."""
     tris = bihrt_mod.scenes.soup(50_000, seed=9)
     g = bihrt_mod.GPUArrayManager(tris)
     a = g.arrays()
-    g.rebuild()
-    b = g.arrays()
-    for k in TREE_KEYS:
-        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+    allocs = []
+    for _ in range(3):
+        g.rebuild()
+        b = g.arrays()
+        for k in TREE_KEYS:
+            assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+        allocs.append(g.info().device_allocs)
+    assert allocs[1] == allocs[0] == allocs[2]
 
 
 @pytest.mark.parametrize("name", ["cornell", "dodeca", "bih1_dodeca", "clustered", "signed_zero", "one_tri",
