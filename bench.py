@@ -257,6 +257,7 @@ class Workload:
             self.step(mode, rows, c, frame_of(base, k), traverse, rebuild=rebuild, nf=nf, m=m)
             k, c = k + m, c + 1
         C.sync_all()
+        allocs0 = self.arrays.info().device_allocs
         # per-call torch events only when asked (--step-events): recording them
         # costs host time per call, which the row-band shares feel
         evs = [(C.torch.cuda.Event(enable_timing=True), C.torch.cuda.Event(enable_timing=True))
@@ -268,6 +269,9 @@ class Workload:
             k, c = k + m, c + 1
         C.sync_all()
         el = C.max_over_ranks(time.perf_counter() - t0)
+        # device allocations inside the timed calls (bih_reserve sized every
+        # per-call buffer; the warm-up built the camera's structures): 0
+        self.timed_allocs = self.arrays.info().device_allocs - allocs0
         kms = [x.elapsed_time(y) / m for (x, y), m in zip(evs, calls)] if evs else []
         return el, (sum(kms) / len(kms) if kms else None), fps
 
@@ -363,12 +367,9 @@ def main():
     mode = args.mode if world > 1 else "weak"
     rows, frame_of, _ = wl.plan(mode, G)
     rays_per_frame = W * H * SPP
-    allocs0 = arrays.info().device_allocs
     elapsed, kernel_ms, fps = wl.timed(mode, trav, 0)
     value = fps * rays_per_frame * args.steps / elapsed
-    # the headline's own warm-up may build per-camera structures; its timed
-    # calls must not allocate (bih_reserve sized every per-call buffer)
-    allocs_headline = arrays.info().device_allocs - allocs0
+    allocs_headline = wl.timed_allocs
 
     if args.headline_only:
         args.no_reference_leg = args.no_rebuild_leg = True

@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 // Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
 // (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
-// by k_prep's last block (prep_final).  The build is a deterministic function of the soup, so an
+// by k_prep_final.  The build is a deterministic function of the soup, so an
 // unchanged hash after a rebuild means an unchanged tree, and the per-camera
 // structures derived from it (bih_capi.cpp finish_build) stay valid.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -77,11 +77,111 @@ __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float 
     M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
 }
 
-// The fold of k_prep's per-block partials into the header (the scene AABB
-// with the reference's tie rules, the content hash, the non-finite flag):
-// run by k_prep's last block to finish (no launch of its own).
-__device__ void prep_final(const float *__restrict__ v, const float *lo, const float *hi, TreeHeader *hdr,
-                           uint32_t n, const unsigned long long *part, uint32_t nparts) {
+// k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
+// the scene AABB.  The reference folds triangles sequentially with
+// std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
+// as the lo of the LAST triangle attaining the minimum and sceneHi as the hi
+// of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
+// Ties only differ in the sign of zero; we reduce (value, index) keys.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
+                                                   float *__restrict__ lo, float *__restrict__ hi,
+                                                   TreeHeader *hdr,
+                                                   unsigned long long *__restrict__ part) {
+    unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
+    uint32_t bad = 0;
+    uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const float *p = v + 9ull * i;
+        float q[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) content_word(__float_as_uint(q[k]), 9u * i + (uint32_t)k, hx, hy);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
+            bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
+            float m, M;
+            axis_minmax(x0, x1, x2, m, M);
+            lo[3ull * i + a] = m;
+            hi[3ull * i + a] = M;
+            unsigned long long tie = 0xFFFFFFFFull - i;
+            unsigned long long km = ((unsigned long long)lt_key(m) << 32) | tie;
+            unsigned long long kM = ((unsigned long long)lt_key(M) << 32) | tie;
+            kmin[a] = km < kmin[a] ? km : kmin[a];   // smallest value, ties -> largest i
+            kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
+        }
+    }
+    // wave reduce, block reduce through LDS, one partial per block (the
+    // single-block k_prep_final folds them: no contended atomics)
+    __shared__ unsigned long long s_key[7][kThreads / 64];
+    __shared__ uint32_t s_bad[kThreads / 64];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long om = __shfl_xor(kmin[a], off);
+            unsigned long long oM = __shfl_xor(kmax[a], off);
+            kmin[a] = om < kmin[a] ? om : kmin[a];
+            kmax[a] = oM > kmax[a] ? oM : kmax[a];
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        hx ^= __shfl_xor(hx, off);
+        hy ^= __shfl_xor(hy, off);
+    }
+    const unsigned long long anybad = __ballot(bad);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            s_key[a][wv] = kmin[a];
+            s_key[3 + a][wv] = kmax[a];
+        }
+        s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
+        s_bad[wv] = anybad ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        const int a = threadIdx.x;
+        unsigned long long r = s_key[a][0];
+        for (uint32_t w = 1; w < kThreads / 64; ++w) {
+            const unsigned long long o = s_key[a][w];
+            r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
+        }
+        part[(size_t)a * gridDim.x + blockIdx.x] = r;
+    }
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
+        uint32_t b = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
+        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
+    }
+}
+
+__global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
+    int a = threadIdx.x;
+    if (a < 3) {
+        hdr->scene_lo[a] = 0.f;
+        hdr->scene_hi[a] = 0.f;
+        hdr->lo_key[a] = ~0ull;
+        hdr->hi_key[a] = 0ull;
+    }
+    if (a == 0) {
+        hdr->n_tris = n;
+        hdr->n_unique = 0;
+        hdr->nonfinite = 0;
+        hdr->pad0 = 0;
+        hdr->content = 0ull;
+    }
+}
+
+
+__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
+                                                         const float *__restrict__ lo,
+                                                         const float *__restrict__ hi,
+                                                         TreeHeader *hdr, uint32_t n,
+                                                         const unsigned long long *__restrict__ part,
+                                                         uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
     __shared__ unsigned long long s_red[8][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -142,119 +242,6 @@ __device__ void prep_final(const float *__restrict__ v, const float *lo, const f
     hdr->n_tris = n;
 }
 
-// k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
-// the scene AABB.  The reference folds triangles sequentially with
-// std::minmax({lo, hi, sceneLo, sceneHi}) (App.cpp:133-137), so sceneLo ends
-// as the lo of the LAST triangle attaining the minimum and sceneHi as the hi
-// of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
-// Ties only differ in the sign of zero; we reduce (value, index) keys.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
-                                                   float *__restrict__ lo, float *__restrict__ hi,
-                                                   TreeHeader *hdr,
-                                                   unsigned long long *__restrict__ part) {
-    unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
-    uint32_t bad = 0;
-    uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
-        const float *p = v + 9ull * i;
-        float q[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) q[k] = p[k];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) content_word(__float_as_uint(q[k]), 9u * i + (uint32_t)k, hx, hy);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            float x0 = q[a], x1 = q[3 + a], x2 = q[6 + a];
-            bad |= (uint32_t)!isfinite(x0) | (uint32_t)!isfinite(x1) | (uint32_t)!isfinite(x2);
-            float m, M;
-            axis_minmax(x0, x1, x2, m, M);
-            lo[3ull * i + a] = m;
-            hi[3ull * i + a] = M;
-            unsigned long long tie = 0xFFFFFFFFull - i;
-            unsigned long long km = ((unsigned long long)lt_key(m) << 32) | tie;
-            unsigned long long kM = ((unsigned long long)lt_key(M) << 32) | tie;
-            kmin[a] = km < kmin[a] ? km : kmin[a];   // smallest value, ties -> largest i
-            kmax[a] = kM > kmax[a] ? kM : kmax[a];   // largest value, ties -> smallest i
-        }
-    }
-    // wave reduce, block reduce through LDS, one partial per block (the
-    // last block folds them in prep_final: no contended atomics)
-    __shared__ unsigned long long s_key[7][kThreads / 64];
-    __shared__ uint32_t s_bad[kThreads / 64];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        for (int off = 32; off > 0; off >>= 1) {
-            unsigned long long om = __shfl_xor(kmin[a], off);
-            unsigned long long oM = __shfl_xor(kmax[a], off);
-            kmin[a] = om < kmin[a] ? om : kmin[a];
-            kmax[a] = oM > kmax[a] ? oM : kmax[a];
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        hx ^= __shfl_xor(hx, off);
-        hy ^= __shfl_xor(hy, off);
-    }
-    const unsigned long long anybad = __ballot(bad);
-    const uint32_t wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            s_key[a][wv] = kmin[a];
-            s_key[3 + a][wv] = kmax[a];
-        }
-        s_key[6][wv] = ((unsigned long long)hy << 32) | hx;
-        s_bad[wv] = anybad ? 1u : 0u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 7) {
-        const int a = threadIdx.x;
-        unsigned long long r = s_key[a][0];
-        for (uint32_t w = 1; w < kThreads / 64; ++w) {
-            const unsigned long long o = s_key[a][w];
-            r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
-        }
-        part[(size_t)a * gridDim.x + blockIdx.x] = r;
-    }
-    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by prep_final)
-        uint32_t b = 0;
-        for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
-        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
-    }
-    // the last block to finish folds every block's partials (threadfence
-    // reduction: release before the arrival count, acquire after it); the
-    // count word after the partials is zero at allocation and reset here
-    __shared__ bool s_last;
-    __threadfence();
-    __syncthreads();
-    unsigned long long *arrivals = part + 8ull * kPrepBlocks;
-    if (threadIdx.x == 0) s_last = atomicAdd(arrivals, 1ull) == gridDim.x - 1ull;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (threadIdx.x == 0) *arrivals = 0ull;
-    prep_final(v, lo, hi, hdr, n, part, gridDim.x);
-}
-
-__global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
-    int a = threadIdx.x;
-    if (a < 3) {
-        hdr->scene_lo[a] = 0.f;
-        hdr->scene_hi[a] = 0.f;
-        hdr->lo_key[a] = ~0ull;
-        hdr->hi_key[a] = 0ull;
-    }
-    if (a == 0) {
-        hdr->n_tris = n;
-        hdr->n_unique = 0;
-        hdr->nonfinite = 0;
-        hdr->pad0 = 0;
-        hdr->content = 0ull;
-    }
-}
-
-
-
 // ---------------------------------------------------------------------------
 // k_morton: centre (App.cpp:128-131), normalise (:144-156), morton3D
 // (Renderer.cpp:127-136).  Writes (code, index) pairs for the sort.
@@ -289,19 +276,23 @@ constexpr int kRdPasses = 3;
 // Block b's tile [b kRsTile, (b+1) kRsTile): codes and indices, and the tile's
 // counts of the first digit (hist[digit * nblocks + b], k_rs_scatter10's
 // layout) -- the first pass's histogram without a pass of its own.
-__global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ lo,
+// A block of kRsBlock threads per tile: kRsTile / kRsBlock codes per thread.
+constexpr int kRsBlock = 1024;
+constexpr int kRsWaves = kRsBlock / 64;
+constexpr int kRsPer = kRsTile / kRsBlock;            // 4
+__global__ void __launch_bounds__(kRsBlock) k_morton(const float *__restrict__ lo,
                                                      const float *__restrict__ hi,
                                                      const TreeHeader *__restrict__ hdr, uint32_t n,
                                                      uint32_t *__restrict__ keys,
                                                      uint32_t *__restrict__ vals,
                                                      uint32_t *__restrict__ hist, uint32_t nblocks) {
     __shared__ uint32_t h[kRdBins];
-    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) h[k] = 0u;
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kRsBlock) h[k] = 0u;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
-#pragma unroll 4
-    for (int r = 0; r < kRsItems; ++r) {
-        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < kRsPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kRsBlock + threadIdx.x;
         if (i < n) {
             const uint32_t key = morton_code(lo, hi, hdr, (uint32_t)i);
             keys[i] = key;
@@ -310,7 +301,7 @@ __global__ void __launch_bounds__(kThreads) k_morton(const float *__restrict__ l
         }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kRsBlock) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -401,62 +392,63 @@ hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_
 // digit, k_rs_hist10 after), one exclusive scan over them (digit-major:
 // every tile's start for every digit), and k_rs_scatter10.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_rs_hist10(const uint32_t *__restrict__ keys, uint32_t n,
-                                                        int shift, uint32_t *__restrict__ hist,
-                                                        uint32_t nblocks) {
+__global__ void __launch_bounds__(kRsBlock) k_rs_hist10(const uint32_t *__restrict__ keys, uint32_t n,
+                                                         int shift, uint32_t *__restrict__ hist,
+                                                         uint32_t nblocks) {
     __shared__ uint32_t h[kRdBins];
-    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) h[k] = 0u;
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kRsBlock) h[k] = 0u;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
-    uint32_t key[kRsItems];
+    uint32_t key[kRsPer];
 #pragma unroll
-    for (int r = 0; r < kRsItems; ++r) {
-        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+    for (int r = 0; r < kRsPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kRsBlock + threadIdx.x;
         key[r] = i < n ? keys[i] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kRsItems; ++r) {
-        const uint64_t i = base + (uint64_t)r * kThreads + threadIdx.x;
+    for (int r = 0; r < kRsPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kRsBlock + threadIdx.x;
         if (i < n) atomicAdd(&h[(key[r] >> shift) & (kRdBins - 1u)], 1u);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kRdBins; k += kThreads) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
+    for (uint32_t k = threadIdx.x; k < kRdBins; k += kRsBlock) hist[(uint64_t)k * nblocks + blockIdx.x] = h[k];
 }
 
-// Each wave of the block owns a contiguous quarter of the tile (kRsItems
-// rounds of 64), so the pass is stable: the waves' per-digit counts are
-// ranked once (tile start from the scan + the earlier waves' counts), then
-// each wave walks its rounds with no block barrier -- per round the lanes of
-// one digit find each other by 10 ballots, the group's first lane advances
-// the wave's digit cursor with one LDS atomic and the group reads its base
-// from that lane.
-__global__ void __launch_bounds__(kThreads) k_rs_scatter10(const uint32_t *__restrict__ kin,
+// Each of the block's kRsWaves waves owns a contiguous part of the tile
+// (kRsPer rounds of 64), so the pass is stable: the waves' per-digit counts
+// are ranked once (tile start from the scan + the earlier waves' counts),
+// then each wave walks its rounds with no block barrier -- per round the
+// lanes of one digit find each other by 10 ballots, the group's first lane
+// advances the wave's digit cursor with one LDS atomic and the group reads
+// its base from that lane.  (256-thread blocks, one per tile: 0.026 ms per
+// pass at 1M, r04a -- one wave per SIMD walking 16 rounds.)
+__global__ void __launch_bounds__(kRsBlock) k_rs_scatter10(const uint32_t *__restrict__ kin,
                                                            const uint32_t *__restrict__ vin, uint32_t n,
                                                            int shift, const uint32_t *__restrict__ hist_scan,
                                                            uint32_t nblocks, uint32_t *__restrict__ kout,
                                                            uint32_t *__restrict__ vout) {
-    __shared__ uint32_t cnt[kThreads / 64][kRdBins];
+    __shared__ uint32_t cnt[kRsWaves][kRdBins];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    for (uint32_t k = tid; k < (kThreads / 64) * kRdBins; k += kThreads) (&cnt[0][0])[k] = 0u;
+    for (uint32_t k = tid; k < kRsWaves * kRdBins; k += kRsBlock) (&cnt[0][0])[k] = 0u;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kRsTile + (uint64_t)wave * 64u * kRsItems;
-    uint32_t key[kRsItems], val[kRsItems];
+    const uint64_t base = (uint64_t)blockIdx.x * kRsTile + (uint64_t)wave * 64u * kRsPer;
+    uint32_t key[kRsPer], val[kRsPer];
 #pragma unroll
-    for (int r = 0; r < kRsItems; ++r) {
+    for (int r = 0; r < kRsPer; ++r) {
         const uint64_t i = base + (uint64_t)r * 64u + lane;
         key[r] = i < n ? kin[i] : 0u;
         val[r] = i < n ? vin[i] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < kRsItems; ++r) {
+    for (int r = 0; r < kRsPer; ++r) {
         const uint64_t i = base + (uint64_t)r * 64u + lane;
         if (i < n) atomicAdd(&cnt[wave][(key[r] >> shift) & (kRdBins - 1u)], 1u);
     }
     __syncthreads();
-    for (uint32_t d = tid; d < kRdBins; d += kThreads) {
+    for (uint32_t d = tid; d < kRdBins; d += kRsBlock) {
         uint32_t run = hist_scan[(uint64_t)d * nblocks + blockIdx.x];
 #pragma unroll
-        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+        for (uint32_t w = 0; w < kRsWaves; ++w) {
             const uint32_t c = cnt[w][d];
             cnt[w][d] = run;
             run += c;
@@ -465,7 +457,7 @@ __global__ void __launch_bounds__(kThreads) k_rs_scatter10(const uint32_t *__res
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int r = 0; r < kRsItems; ++r) {
+    for (int r = 0; r < kRsPer; ++r) {
         const uint64_t i = base + (uint64_t)r * 64u + lane;
         const bool valid = i < n;
         const uint32_t dg = (key[r] >> shift) & (kRdBins - 1u);
@@ -789,7 +781,7 @@ __device__ __forceinline__ float seg_query(const float *__restrict__ seg, uint64
 // Same nodes, and tmax / tmin are associative and commutative: the same
 // result bit for bit.  Levels: ceil(log2(nn)) + 1 <= 28 for nn <= 2^27.
 #ifndef BIH_FIT_PIPE
-#define BIH_FIT_PIPE 1
+#define BIH_FIT_PIPE 0   // 1: slower (k_fit 0.048 vs 0.032 ms, r04a: 122 VGPRs, 4 waves)
 #endif
 constexpr int kSegMaxLevels = 28;
 template <bool HI>
@@ -961,8 +953,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
         BIH_TRY(dalloc(&t.hist, hist_n, t));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks + 1, t));   // + k_prep's arrival count
-        BIH_TRY(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, sizeof(unsigned long long), st));
+        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, t));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
         // tag): stale data in fresh memory must not pass for a predecessor's
         // published prefix; afterwards every word carries an older call's
@@ -974,14 +965,19 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     BIH_TRY(hipEventCreate(&e1));
     BIH_TRY(hipEventRecord(e0, st));
 
-    // header reset (no triangles; otherwise k_prep's last block writes the header)
+    // header reset (no triangles; otherwise k_prep_final writes the header)
     if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
                            t.tri_hi, t.hdr, t.prep_part);
-        hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kThreads), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
+        // (folding the partials in k_prep's last block instead -- a device-scope
+        // fence per block before the arrival count -- made k_prep 0.147 ms
+        // against 0.016 + 0.012 for the two launches: r04a)
+        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
+                           t.hdr, n, t.prep_part, prep_blocks);
+        hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
                            t.vals, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
         // counted the first digit); the sorted pairs end in keys2 / vals2,
@@ -990,10 +986,10 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         for (int p = 0; p < kRdPasses; ++p) {
             const int shift = kRdBits * p;
             if (p > 0)
-                hipLaunchKernelGGL(k_rs_hist10, dim3(rs_blocks), dim3(kThreads), 0, st, ka, n, shift, t.hist,
+                hipLaunchKernelGGL(k_rs_hist10, dim3(rs_blocks), dim3(kRsBlock), 0, st, ka, n, shift, t.hist,
                                    rs_blocks);
             BIH_TRY(exclusive_scan(t.hist, t.hist, (uint32_t)hist_n, t.partials, nullptr, st));
-            hipLaunchKernelGGL(k_rs_scatter10, dim3(rs_blocks), dim3(kThreads), 0, st, ka, va, n, shift, t.hist,
+            hipLaunchKernelGGL(k_rs_scatter10, dim3(rs_blocks), dim3(kRsBlock), 0, st, ka, va, n, shift, t.hist,
                                rs_blocks, kb, vb);
             uint32_t *tk = ka, *tv = va;
             ka = kb; va = vb; kb = tk; vb = tv;

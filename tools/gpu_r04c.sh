@@ -13,3 +13,7 @@ for s in 1 0; do
   BIH_WH_SORT=$s timeout -k 10 300 python3 $R/tools/time_whitted.py --frames 2 > $R/gpurun_out/${T}_wh_sort$s.json 2>/dev/null || exit 1
   echo "== wh sort=$s $(tail -1 $R/gpurun_out/${T}_wh_sort$s.json | cut -c1-300)"
 done
+for v in default fitpipe0; do
+  if [ $v = default ]; then L=""; else L="BIH_LIB=$R/bih-gpu-raytracer_amd/lib/variants/libbih_amd_$v.so"; fi
+  echo "== build $v $(env $L timeout -k 10 120 python3 $R/tools/prof_build.py --builds 20 2>/dev/null | tail -1)"
+done
