@@ -416,22 +416,30 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist10(const uint32_t *__restri
 
 // Each of the block's kRsWaves waves owns a contiguous part of the tile
 // (kRsPer rounds of 64), so the pass is stable: the waves' per-digit counts
-// are ranked once (tile start from the scan + the earlier waves' counts),
-// then each wave walks its rounds with no block barrier -- per round the
-// lanes of one digit find each other by 10 ballots, the group's first lane
-// advances the wave's digit cursor with one LDS atomic and the group reads
-// its base from that lane.  (256-thread blocks, one per tile: 0.026 ms per
-// pass at 1M, r04a -- one wave per SIMD walking 16 rounds.)
+// are ranked once, then each wave walks its rounds with no block barrier --
+// per round the lanes of one digit find each other by 10 ballots, the
+// group's first lane advances the wave's digit cursor with one LDS atomic
+// and the group reads its base from that lane.  The ranks are positions in
+// the tile sorted by digit (LDS); the sorted tile then goes out in order,
+// each digit's run to its place after the earlier tiles' (the scan), so
+// consecutive threads write consecutive words.  (Writing each element
+// straight to its global position -- up to 64 runs per store -- took
+// 0.024 ms per pass at 1M, r04b.)
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter10(const uint32_t *__restrict__ kin,
                                                            const uint32_t *__restrict__ vin, uint32_t n,
                                                            int shift, const uint32_t *__restrict__ hist_scan,
                                                            uint32_t nblocks, uint32_t *__restrict__ kout,
                                                            uint32_t *__restrict__ vout) {
-    __shared__ uint32_t cnt[kRsWaves][kRdBins];
+    __shared__ uint32_t cnt[kRsWaves][kRdBins];   // per wave and digit: count, then cursor
+    __shared__ uint32_t s_key[kRsTile], s_val[kRsTile];
+    __shared__ uint32_t s_lstart[kRdBins];        // digit d's first position in the sorted tile
+    __shared__ uint32_t s_gstart[kRdBins];        // its first position in the output
+    __shared__ uint32_t s_wsum[kRsWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint32_t k = tid; k < kRsWaves * kRdBins; k += kRsBlock) (&cnt[0][0])[k] = 0u;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kRsTile + (uint64_t)wave * 64u * kRsPer;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kRsTile;
+    const uint64_t base = tile0 + (uint64_t)wave * 64u * kRsPer;
     uint32_t key[kRsPer], val[kRsPer];
 #pragma unroll
     for (int r = 0; r < kRsPer; ++r) {
@@ -445,15 +453,31 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter10(const uint32_t *__res
         if (i < n) atomicAdd(&cnt[wave][(key[r] >> shift) & (kRdBins - 1u)], 1u);
     }
     __syncthreads();
-    for (uint32_t d = tid; d < kRdBins; d += kRsBlock) {
-        uint32_t run = hist_scan[(uint64_t)d * nblocks + blockIdx.x];
+    // digit d = tid: the waves' exclusive prefixes, the tile's total of d,
+    // and the tile-exclusive scan of the totals over the digits
+    static_assert(kRsBlock == kRdBins, "one thread per digit");
+    const uint32_t d = tid;
+    uint32_t tot = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < kRsWaves; ++w) {
-            const uint32_t c = cnt[w][d];
-            cnt[w][d] = run;
-            run += c;
-        }
+    for (uint32_t w = 0; w < kRsWaves; ++w) {
+        const uint32_t c = cnt[w][d];
+        cnt[w][d] = tot;
+        tot += c;
     }
+    uint32_t inc = tot;
+#pragma unroll
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63u) s_wsum[wave] = inc;
+    __syncthreads();
+    uint32_t lstart = inc - tot;
+    for (uint32_t w = 0; w < wave; ++w) lstart += s_wsum[w];
+    s_lstart[d] = lstart;
+    s_gstart[d] = hist_scan[(uint64_t)d * nblocks + blockIdx.x];
+#pragma unroll
+    for (uint32_t w = 0; w < kRsWaves; ++w) cnt[w][d] += lstart;
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -474,9 +498,18 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter10(const uint32_t *__res
         const uint32_t leader = valid ? (uint32_t)__builtin_ctzll(peers) : lane;
         off = (uint32_t)__shfl((int)off, (int)leader, 64);
         if (valid) {
-            kout[off + rank] = key[r];
-            vout[off + rank] = val[r];
+            s_key[off + rank] = key[r];
+            s_val[off + rank] = val[r];
         }
+    }
+    __syncthreads();
+    const uint32_t m = (uint32_t)(n - tile0 < (uint64_t)kRsTile ? n - tile0 : (uint64_t)kRsTile);
+    for (uint32_t j = tid; j < m; j += kRsBlock) {
+        const uint32_t k = s_key[j];
+        const uint32_t dg = (k >> shift) & (kRdBins - 1u);
+        const uint32_t o = s_gstart[dg] + (j - s_lstart[dg]);
+        kout[o] = k;
+        vout[o] = s_val[j];
     }
 }
 

@@ -6,7 +6,8 @@
 // the test oracle (ob_render_whitted) and DESIGN.md section 4.5:
 //   closest hit = min (t, sorted position) over the triangles the reference
 //   walk visits (TraverseTree's decisions, :227-368, RayTriangleIntersection
-//   :17-50), t_lo < t < FLT_MAX (t_lo = 0 for primary rays, 1e-4 after);
+//   :17-50), t_lo < t < FLT_MAX (t_lo = 0 for primary rays, 1e-4 after; a
+//   bounce's walk interval starts at max(box entry, t_lo));
 //   P = O + t*D, n = cross(e1, e2), k = (2*dot(D, n)) / dot(n, n), R = D - k*n;
 //   shade(d) = miss ? (20,20,40) : d == 8 ? (255,255,0) : 0.5*Y + 0.5*shade(d+1).
 // The (t, i) rule is order-independent, so any walk order over the same visit
@@ -147,6 +148,7 @@ __device__ void closest_walk(const WScene &s, float ox, float oy, float oz, floa
     if ((tMin > tzmax) || (tzmin > tMax)) return;
     if (tzmin > tMin) tMin = tzmin;
     if (tzmax < tMax) tMax = tzmax;
+    if (t_lo > 0.0f && tMin < t_lo) tMin = t_lo;   // a bounce's walk starts at its origin (oracle)
     if (s.U == 0) return;
     auto leaf = [&](uint32_t b, uint32_t e) {
         for (uint32_t i = b; i < e; ++i) {
@@ -353,7 +355,7 @@ struct WRay {
     float o[3], d[3], ix, iy, iz, tMin, tMax, bt;
     uint32_t sg, cur, sp, bi, sid;
 };
-__device__ __forceinline__ bool wray_start(const WScene &s, WRay &r) {
+__device__ __forceinline__ bool wray_start(const WScene &s, WRay &r, float t_lo) {
     r.bt = FLT_MAX;
     r.bi = kNoHit;
     r.cur = 0;
@@ -375,6 +377,7 @@ __device__ __forceinline__ bool wray_start(const WScene &s, WRay &r) {
     if ((tMin > tzmax) || (tzmin > tMax)) return false;
     if (tzmin > tMin) tMin = tzmin;
     if (tzmax < tMax) tMax = tzmax;
+    if (t_lo > 0.0f && tMin < t_lo) tMin = t_lo;   // a bounce's walk starts at its origin (oracle)
     r.tMin = tMin;
     r.tMax = tMax;
     return true;
@@ -495,7 +498,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
                         r.d[c] = qin.p[(3 + c) * qin.cap + i];
                     }
                     r.sid = sid_in[i];
-                    has = wray_start(sc, r);   // a ray that misses the scene box ends here: no hit
+                    has = wray_start(sc, r, t_lo);   // a ray that misses the scene box ends here: no hit
                 }
             }
         }

@@ -220,7 +220,9 @@ int bih_tree_set_param(bih_tree *tree, int param, uint64_t value);
  * a front-to-back walk tests -- the reference walk's decisions and order
  * (TraverseTree, :227-368) until the first hit, after which a stacked node
  * entered beyond the best hit (tMin > best) is popped unvisited and tMax is
- * clamped to the best hit; P = O + tD, n = cross(e1, e2), R = D - (2 D.n / n.n) n;
+ * clamped to the best hit; a bounce's walk interval starts at max(scene-box
+ * entry, 1e-4) (its origin lies inside the box: nothing behind it can be
+ * accepted); P = O + tD, n = cross(e1, e2), R = D - (2 D.n / n.n) n;
  * secondary hits need t > 1e-4; a sample's shade halves towards (255,255,0)
  * per hit and ends at (20,20,40) on a miss (or (255,255,0) after 8 bounces).
  * Same primary rays, RNG draws and framebuffer format as bih_render.

@@ -521,12 +521,17 @@ static int traverse_gpu_ref(const ob_tree *T, const ray_t *r, cnt_t *c, int anyh
  * closest-hit rule at its leaves and front-to-back culling: before each node
  * a node entered beyond the best hit so far (tMin > best) is popped, and tMax
  * is clamped to the best hit (tMax = min(tMax, best), best = +inf until the
- * first hit, so the walk is the reference's until then). */
+ * first hit, so the walk is the reference's until then).  A secondary ray
+ * (t_lo > 0) starts inside the scene box: its walk interval starts at t_lo
+ * (tMin = max(box entry, t_lo)) rather than at the box entry behind its
+ * origin, where no accepted hit can lie (round 4; primary rays, t_lo = 0,
+ * keep the reference's interval). */
 static void traverse_closest(const ob_tree *T, const ray_t *r, float t_lo, float *bt, int32_t *bi,
                              cnt_t *c) {
     *bt = FLT_MAX; *bi = -1;
     float tMin, tMax;
     if (!slab(T, r, &tMin, &tMax)) return;
+    if (t_lo > 0.0f && tMin < t_lo) tMin = t_lo;
     int U = T->n_unique;
     if (U <= 0) return;
     if (U == 1) { find_closest(T, r, 0, t_lo, bt, bi, c); return; }

@@ -93,6 +93,8 @@ int ob_render(const ob_tree *t, const float cam[12], uint32_t w, uint32_t h,
  *     t_lo < t < FLT_MAX (depth 0: t > 0 as FindNearestTriangle :212;
  *     bounces: t > 1e-4), where the walk culls front to back once it has a
  *     hit: before each node, pop if tMin > best, else tMax = min(tMax, best);
+ *     a bounce's walk interval starts at max(scene-box entry, 1e-4), not at
+ *     the box entry behind its origin (round 4);
  *   hit point P = O + t*D; n = cross(e1, e2) (glm order, e = v - v0 of the
  *     original triangle); k = (2*dot(D, n)) / dot(n, n); R = D - k*n;
  *   shade(d) = miss ? (20,20,40) : d == 8 ? (255,255,0)
