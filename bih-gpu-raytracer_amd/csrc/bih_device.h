@@ -26,6 +26,19 @@ __device__ __forceinline__ float xorwow_uniform(uint32_t v[5], uint32_t &d) {
     return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);   // _curand_uniform
 }
 
+// One XORWOW step without the float conversion: the 32-bit output
+// (curand(), the word xorwow_uniform converts); same state update.
+__device__ __forceinline__ uint32_t xorwow_next(uint32_t v[5], uint32_t &d) {
+    uint32_t t = v[0] ^ (v[0] >> 2);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+    d += kWeyl;
+    return v[4] + d;
+}
+__device__ __forceinline__ float xorwow_to_uniform(uint32_t x) {
+    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);   // _curand_uniform
+}
+
 // clamp + rgbToInt, CUDAKernels.cu:74-88
 __device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
     r = fmaxf(0.0f, fminf(255.0f, r));

@@ -1701,6 +1701,9 @@ __device__ __forceinline__ bool path_step(uint32_t val, uint32_t meta, float ix,
 }
 // The first 24 steps are requested at once (one round trip for most
 // leaves), the last 8 only by lanes whose path is longer.
+#ifndef BIH_PATH_BATCH
+#define BIH_PATH_BATCH 8
+#endif
 #ifndef BIH_PATH_FLAT
 #define BIH_PATH_FLAT 1
 #endif
@@ -1728,12 +1731,16 @@ __device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint
                                             float iy, float iz, float lo, float hi) {
     const uint4 *p = reinterpret_cast<const uint4 *>(path + 32ull * k);
     bool live = true, ok = false;
-    {
-        uint4 q[12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) q[j] = p[j];
+    for (int g = 0; g < 24 / BIH_PATH_BATCH; ++g) {
+        // BIH_PATH_BATCH steps per round trip (8: 3 rounds, 16 VGPRs of
+        // steps live instead of 48 -- that was k_render_bins' register peak:
+        // 98 VGPRs and 4 waves per SIMD, now 79 and 6)
+        uint4 q[BIH_PATH_BATCH / 2];
 #pragma unroll
-        for (int j = 0; j < 24; ++j) {
+        for (int j = 0; j < BIH_PATH_BATCH / 2; ++j) q[j] = p[g * (BIH_PATH_BATCH / 2) + j];
+#pragma unroll
+        for (int j = 0; j < BIH_PATH_BATCH; ++j) {
             const uint4 w = q[j >> 1];
             path_step_flat((j & 1) ? w.z : w.x, (j & 1) ? w.w : w.y, ix, iy, iz, lo, hi, live, ok);
         }
@@ -2035,16 +2042,19 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             if (valid) {
                 // the frame's 2*SPP draws on every lane (uniform control
                 // flow); rs ends at the next frame's state
-                float ru = 0.f, rv = 0.f;
+                // (the two words this sample takes are converted to floats,
+                // not all 2*SPP: curand_uniform of the same words)
+                uint32_t xu = 0u, xv = 0u;
                 uint32_t d = dfr, rs[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) rs[i] = s_rs[i][tid];
 #pragma unroll 8
                 for (uint32_t k = 0; k < 2u * SPP; ++k) {
-                    const float f = xorwow_uniform(rs, d);
-                    if (k == 2u * s) ru = f;
-                    if (k == 2u * s + 1u) rv = f;
+                    const uint32_t x = dev::xorwow_next(rs, d);
+                    if (k == 2u * s) xu = x;
+                    if (k == 2u * s + 1u) xv = x;
                 }
+                const float ru = dev::xorwow_to_uniform(xu), rv = dev::xorwow_to_uniform(xv);
                 if (fj + 1u < nf) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
