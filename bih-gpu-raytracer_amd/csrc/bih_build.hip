@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 // Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
 // (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
-// by k_prep_final.  The build is a deterministic function of the soup, so an
+// by k_prep's last block (prep_fold).  The build is a deterministic function of the soup, so an
 // unchanged hash after a rebuild means an unchanged tree, and the per-camera
 // structures derived from it (bih_capi.cpp finish_build) stay valid.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -71,7 +71,7 @@ __device__ __forceinline__ void content_word(uint32_t w, uint32_t i, uint32_t &x
 }
 
 // Triangle AABB on one axis with std::minmax's rules (App.cpp:103-142):
-// leftmost min, rightmost max (k_prep; k_seg_leaf recomputes it bit-equal).
+// leftmost min, rightmost max (k_prep; leaf_box recomputes it bit-equal).
 __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float &m, float &M) {
     m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
     M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
@@ -84,6 +84,8 @@ __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float 
 // of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
 // Ties only differ in the sign of zero; we reduce (value, index) keys.
 // ---------------------------------------------------------------------------
+__device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t n,
+                          const unsigned long long *part, uint32_t nparts);
 __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
                                                    float *__restrict__ lo, float *__restrict__ hi,
                                                    TreeHeader *hdr,
@@ -114,7 +116,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
         }
     }
     // wave reduce, block reduce through LDS, one partial per block (the
-    // single-block k_prep_final folds them: no contended atomics)
+    // last block folds them in prep_fold: no contended atomics)
     __shared__ unsigned long long s_key[7][kThreads / 64];
     __shared__ uint32_t s_bad[kThreads / 64];
 #pragma unroll
@@ -149,13 +151,28 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             const unsigned long long o = s_key[a][w];
             r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
-        part[(size_t)a * gridDim.x + blockIdx.x] = r;
+        __hip_atomic_store(part + (size_t)a * gridDim.x + blockIdx.x, r, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by prep_fold)
         uint32_t b = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
-        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
+        __hip_atomic_store(part + (size_t)7 * gridDim.x + blockIdx.x, (unsigned long long)b, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    // hand-off to the last block (prep_fold): sc1 stores waited for in every
+    // wave, a barrier, one agent-scope add; the last adder folds
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned long long *arrivals = part + 8ull * kPrepBlocks;
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(arrivals, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned long long)gridDim.x - 1ull;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(arrivals, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prep_fold(v, hdr, n, part, gridDim.x);
 }
 
 __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
@@ -176,12 +193,21 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
 }
 
 
-__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
-                                                         const float *__restrict__ lo,
-                                                         const float *__restrict__ hi,
-                                                         TreeHeader *hdr, uint32_t n,
-                                                         const unsigned long long *__restrict__ part,
-                                                         uint32_t nparts) {
+// Fold of k_prep's per-block partials into the header, run by the LAST block
+// of k_prep to finish (no launch of its own).  Hand-off without fences
+// (MI355X_MICROARCH.md, cross-workgroup table, row 1): every block stores its
+// partials with sc1 stores (relaxed agent-scope), waits for them
+// (s_waitcnt vmcnt(0)) in every wave, meets at a barrier, and one lane adds
+// to an arrival counter (agent scope); the block whose add returns
+// nblocks - 1 reads every partial with sc1 loads.  (A __threadfence() per
+// block -- an L2 write-back each -- made k_prep 0.147 ms, r04a; the fold as a
+// kernel of its own took 0.012 ms.)  The extreme triangles' boxes are
+// recomputed from the soup (axis_minmax, the values k_prep stored).
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t n,
+                          const unsigned long long *part, uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
     __shared__ unsigned long long s_red[8][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -189,7 +215,7 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
     for (int a = 0; a < 6; ++a) {
         unsigned long long r = a < 3 ? ~0ull : 0ull;
         for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) {
-            const unsigned long long o = part[(size_t)a * nparts + i];
+            const unsigned long long o = ld_sc1(part + (size_t)a * nparts + i);
             r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -200,13 +226,13 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
     }
     {   // the content hash: XOR of the blocks' partials
         unsigned long long hxy = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= part[(size_t)6 * nparts + i];
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= ld_sc1(part + (size_t)6 * nparts + i);
         for (int off = 32; off > 0; off >>= 1) hxy ^= __shfl_xor(hxy, off);
         if (lane == 0) s_red[6][wv] = hxy;
     }
     {   // non-finite flags of the blocks
         unsigned long long b = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= part[(size_t)7 * nparts + i];
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= ld_sc1(part + (size_t)7 * nparts + i);
         for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off);
         if (lane == 0) s_red[7][wv] = b;
     }
@@ -222,10 +248,10 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
         hdr->nonfinite = bad ? 1u : 0u;
         hdr->n_unique = 0;
         hdr->pad0 = 0;
+        hdr->n_tris = n;
     }
     const int a = threadIdx.x;
     if (a >= 3) return;
-    if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
     unsigned long long kmin = s_red[a][0], kmax = s_red[3 + a][0];
     for (uint32_t w = 1; w < kThreads / 64; ++w) {
         kmin = s_red[a][w] < kmin ? s_red[a][w] : kmin;
@@ -233,13 +259,14 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
     }
     hdr->lo_key[a] = kmin;
     hdr->hi_key[a] = kmax;
-    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
-    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
-    hdr->scene_lo[a] = lo[3ull * ilo + a];
-    float mx = hi[3ull * ihi + a];
-    float seed = v[a];                         // first vertex (App.cpp:103-106)
-    hdr->scene_hi[a] = (seed < mx) ? mx : seed;
-    hdr->n_tris = n;
+    const uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
+    const uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
+    float m, M, dummy;
+    axis_minmax(v[9ull * ilo + a], v[9ull * ilo + 3 + a], v[9ull * ilo + 6 + a], m, dummy);
+    axis_minmax(v[9ull * ihi + a], v[9ull * ihi + 3 + a], v[9ull * ihi + 6 + a], dummy, M);
+    hdr->scene_lo[a] = m;
+    const float seed = v[a];                   // first vertex (App.cpp:103-106)
+    hdr->scene_hi[a] = (seed < M) ? M : seed;
 }
 
 // ---------------------------------------------------------------------------
@@ -348,12 +375,20 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     uint32_t x[kScanItems];
     uint32_t sum = 0;
+    // 16-byte loads and stores when the whole run of 8 is in range and the
+    // arrays are 16-byte aligned (base is a multiple of 8 words)
+    const bool vec = base + kScanItems <= n && ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0u;
+    if (vec) {
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(in + base);
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(in + base + 4);
+        x[0] = q0.x; x[1] = q0.y; x[2] = q0.z; x[3] = q0.w;
+        x[4] = q1.x; x[5] = q1.y; x[6] = q1.z; x[7] = q1.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        const uint64_t i = base + k;
-        x[k] = (i < n) ? in[i] : 0u;
-        sum += x[k];
+        for (int k = 0; k < kScanItems; ++k) x[k] = (base + k < n) ? in[base + k] : 0u;
     }
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) sum += x[k];
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
     if (threadIdx.x < 64) {
@@ -365,11 +400,19 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
     }
     __syncthreads();
     uint32_t run = s_prefix + ex;
+    uint32_t o[kScanItems];
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
-        const uint64_t i = base + k;
-        if (i < n) out[i] = run;
+        o[k] = run;
         run += x[k];
+    }
+    if (vec) {
+        *reinterpret_cast<uint4 *>(out + base) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4 *>(out + base + 4) = make_uint4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k)
+            if (base + k < n) out[base + k] = o[k];
     }
 }
 
@@ -532,11 +575,20 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
     const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     uint32_t key[kScanItems + 1];   // key[0] = the code before this thread's first element
     key[0] = (base > 0 && base - 1 < n) ? keys[base - 1] : 0u;
+    static_assert(kScanItems == 8, "two 16-byte loads per thread");
+    if (base + kScanItems <= n) {   // whole: 16-byte loads (base is a multiple of 8 words)
+        const uint4 q0 = *reinterpret_cast<const uint4 *>(keys + base);
+        const uint4 q1 = *reinterpret_cast<const uint4 *>(keys + base + 4);
+        key[1] = q0.x; key[2] = q0.y; key[3] = q0.z; key[4] = q0.w;
+        key[5] = q1.x; key[6] = q1.y; key[7] = q1.z; key[8] = q1.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k) key[k + 1] = base + k < n ? keys[base + k] : 0u;
+    }
     uint32_t flags = 0, sum = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const uint64_t i = base + k;
-        key[k + 1] = i < n ? keys[i] : 0u;
         const bool f = i < n && (i == 0 || key[k + 1] != key[k]);
         flags |= (f ? 1u : 0u) << k;
         sum += f ? 1u : 0u;
@@ -553,6 +605,7 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
     }
     __syncthreads();
     uint32_t run = s_prefix + ex;   // runs started before element base
+    uint32_t lf[kScanItems];
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const uint64_t i = base + k;
@@ -564,9 +617,17 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
         }
         run += f ? 1u : 0u;
         const uint32_t leaf = run - 1u;
-        leaf_of[i] = leaf;
+        lf[k] = leaf;
         const uint32_t after = k + 1 < kScanItems ? key[k + 2] : nxt;
         if (i + 1 == n || after != key[k + 1]) run_end[leaf] = (uint32_t)(i + 1);
+    }
+    if (base + kScanItems <= n) {
+        *reinterpret_cast<uint4 *>(leaf_of + base) = make_uint4(lf[0], lf[1], lf[2], lf[3]);
+        *reinterpret_cast<uint4 *>(leaf_of + base + 4) = make_uint4(lf[4], lf[5], lf[6], lf[7]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k)
+            if (base + k < n) leaf_of[base + k] = lf[k];
     }
 }
 
@@ -641,11 +702,12 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
 // totalOrder, tkey).  A Karras node's subtree is the contiguous leaf range
 // [mn, mx] (k_karras, node_rng) with the left child [mn, split] and the right
 // [split + 1, mx], so each clip is one range query over the leaf boxes:
-//   k_seg_leaf  leaf boxes (CUDAKernels.cu:511-529) = level 0 of a segment
+//   k_seg_build leaf boxes (CUDAKernels.cu:511-529) = level 0 of a segment
 //               tree of the six box components (SoA), entry i of level L =
-//               leaves [i 2^L, (i+1) 2^L) (min for lo, max for hi);
-//   k_seg_up    10 levels per launch through LDS (2 launches at 1M leaves);
-//   k_fit       per node two O(log U) queries (no atomics, no hand-offs).
+//               leaves [i 2^L, (i+1) 2^L) (min for lo, max for hi), and
+//               levels 1..10 through LDS; up to 2^20 leaves its last block
+//               builds the rest (k_seg_up per 10 levels above that);
+//   k_fit       per node two O(log U) queries (no atomics).
 // totalOrder max/min is associative and commutative, so any grouping gives
 // the reference's result bit for bit.  (Before: boxes handed bottom-up through
 // device-scope atomics and arrival counters, three atomic round trips per
@@ -690,23 +752,15 @@ __device__ __forceinline__ void pack_tri(const float *__restrict__ p, float *__r
     for (int a = 0; a < 3; ++a) axis_minmax(q[a], q[3 + a], q[6 + a], lo[a], hi[a]);
 }
 
-// Leaf boxes, and the sorted triangle records of each leaf's run (the runs
-// partition the sorted triangles: read once with the
+// Leaf k's box (CUDAKernels.cu:511-529), and the sorted triangle records of
+// its run (the runs partition the sorted triangles: read once with the
 // vertices the boxes come from).
-__global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restrict__ hdr,
-                                                       const uint32_t *__restrict__ tri_idx,
-                                                       const float *__restrict__ v,
-                                                       float *__restrict__ tris_s,
-                                                       const int32_t *__restrict__ first,
-                                                       const uint32_t *__restrict__ cnt,
-                                                       float *__restrict__ seg, uint64_t cap) {
-    const uint32_t U = hdr->n_unique;
-    const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-    if (U < 2 || k >= U) return;
-    // leaf AABB (CUDAKernels.cu:511-529)
+__device__ __forceinline__ void leaf_box(const uint32_t *__restrict__ tri_idx, const float *__restrict__ v,
+                                         float *__restrict__ tris_s, const int32_t *__restrict__ first,
+                                         const uint32_t *__restrict__ cnt, uint32_t k, float blo[3],
+                                         float bhi[3]) {
     const int32_t f = first[k];
     const uint32_t c = cnt[k];
-    float blo[3], bhi[3];
     pack_tri(v + 9ull * tri_idx[f], tris_s + 9ull * f, blo, bhi);
     for (uint32_t i = 1; i < c; ++i) {
         float tlo[3], thi[3];
@@ -717,22 +771,15 @@ __global__ void __launch_bounds__(kThreads) k_seg_leaf(const TreeHeader *__restr
             bhi[a] = tmax(bhi[a], thi[a]);
         }
     }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        seg[a * cap + k] = blo[a];
-        seg[(3 + a) * cap + k] = bhi[a];
-    }
 }
 
-// Levels L0+1 .. L0+kSegSteps from level L0: block b owns level-L0 entries
-// [b kSegBlock, (b+1) kSegBlock).  Only entries of the U valid leaves are
-// combined (a partial last entry is never read by a query).
-__global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restrict__ hdr,
-                                                     float *__restrict__ seg, uint64_t cap, uint64_t nn,
-                                                     int L0) {
-    __shared__ float v[6][kSegBlock];
-    const uint32_t U = hdr->n_unique;
-    if (U < 2) return;
+// Levels L0+1 .. L0+kSegSteps of the segment tree from level-L0 entries
+// [base, base + kSegBlock) held in LDS (vl).  Only entries of the U valid
+// leaves are combined (a partial last entry is never read by a query).  The
+// last level's entries are stored sc1 when `hand_off` (the last-block
+// hand-off of k_seg_build).
+__device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__restrict__ seg, uint64_t cap,
+                                           uint64_t nn, uint32_t U, int L0, uint64_t base, bool hand_off) {
     const uint32_t tid = threadIdx.x;
     uint64_t off = seg_level_off(nn, L0), size = nn;
     uint64_t vsize = U;                             // valid entries of the level
@@ -740,12 +787,6 @@ __global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restric
         size = (size + 1) / 2;
         vsize = (vsize + 1) / 2;
     }
-    const uint64_t base = (uint64_t)blockIdx.x * kSegBlock;
-    for (uint32_t j = tid; j < kSegBlock; j += kThreads)
-        if (base + j < vsize)
-#pragma unroll
-            for (int c = 0; c < 6; ++c) v[c][j] = seg[c * cap + off + base + j];
-    __syncthreads();
     uint32_t cnt = kSegBlock;
     for (int s = 1; s <= kSegSteps; ++s) {
         if (size <= 1) break;                       // the top level is done (uniform)
@@ -763,24 +804,108 @@ __global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restric
                 const bool two = 2 * g + 1 < pvsize;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
-                    const float a = v[c][2 * j];
-                    r[nj][c] = two ? (c < 3 ? tmin(a, v[c][2 * j + 1]) : tmax(a, v[c][2 * j + 1])) : a;
+                    const float x = vl[c][2 * j];
+                    r[nj][c] = two ? (c < 3 ? tmin(x, vl[c][2 * j + 1]) : tmax(x, vl[c][2 * j + 1])) : x;
                 }
             }
         }
         __syncthreads();
         nj = 0;
+        const bool sc1 = hand_off && s == kSegSteps;
         for (uint32_t j = tid; j < cnt; j += kThreads, ++nj) {
             const uint64_t g = gb + j;
             if (g < vsize)
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
-                    v[c][j] = r[nj][c];
-                    seg[c * cap + off + g] = r[nj][c];
+                    vl[c][j] = r[nj][c];
+                    if (sc1)
+                        __hip_atomic_store(seg + c * cap + off + g, r[nj][c], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        seg[c * cap + off + g] = r[nj][c];
                 }
         }
         __syncthreads();
     }
+}
+
+// Leaf boxes (level 0, with the sorted triangle records of every run) and
+// levels 1..10 of the segment tree in one launch: block b owns leaves
+// [b kSegBlock, (b+1) kSegBlock).  With `top` (at most kSegBlock blocks,
+// nn <= 2^20) the last block to finish also builds the levels above 10 from
+// the blocks' level-10 entries -- stored sc1, waited for, a barrier, one
+// agent-scope add per block, read sc1 by the block whose add came last
+// (MI355X_MICROARCH.md, cross-workgroup table, row 1); larger trees take
+// k_seg_up launches for those levels.  (Round 3: k_seg_leaf + 2 x k_seg_up,
+// 0.035 + 0.018 + 0.012 ms at 1M, r04d.)
+__global__ void __launch_bounds__(kThreads) k_seg_build(const TreeHeader *__restrict__ hdr,
+                                                        const uint32_t *__restrict__ tri_idx,
+                                                        const float *__restrict__ v, float *__restrict__ tris_s,
+                                                        const int32_t *__restrict__ first,
+                                                        const uint32_t *__restrict__ cnt, float *__restrict__ seg,
+                                                        uint64_t cap, uint64_t nn, int top,
+                                                        unsigned long long *arrivals) {
+    __shared__ float vl[6][kSegBlock];
+    __shared__ uint32_t s_last;
+    const uint32_t U = hdr->n_unique;
+    if (U < 2) return;   // (uniform: no block takes part in the hand-off)
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * kSegBlock;
+    for (uint32_t j = tid; j < kSegBlock; j += kThreads) {
+        const uint64_t k = base + j;
+        if (k < U) {
+            float blo[3], bhi[3];
+            leaf_box(tri_idx, v, tris_s, first, cnt, (uint32_t)k, blo, bhi);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                vl[a][j] = blo[a];
+                vl[3 + a][j] = bhi[a];
+                seg[a * cap + k] = blo[a];
+                seg[(3 + a) * cap + k] = bhi[a];
+            }
+        }
+    }
+    __syncthreads();
+    seg_levels(vl, seg, cap, nn, U, 0, base, top != 0);
+    if (!top) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        s_last = __hip_atomic_fetch_add(arrivals, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned long long)gridDim.x - 1ull;
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) __hip_atomic_store(arrivals, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the level-10 entries of every block (sc1), then the levels above
+    const uint64_t off10 = seg_level_off(nn, kSegSteps);
+    uint64_t vs = U;
+    for (int l = 0; l < kSegSteps; ++l) vs = (vs + 1) / 2;
+    for (uint32_t j = tid; j < kSegBlock; j += kThreads)
+        if (j < vs)
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                vl[c][j] = __hip_atomic_load(seg + c * cap + off10 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    seg_levels(vl, seg, cap, nn, U, kSegSteps, 0, false);
+}
+
+// Levels L0+1 .. L0+kSegSteps from level L0 (trees over 2^20 leaves, levels
+// above 10): block b owns level-L0 entries [b kSegBlock, (b+1) kSegBlock).
+__global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restrict__ hdr,
+                                                     float *__restrict__ seg, uint64_t cap, uint64_t nn,
+                                                     int L0) {
+    __shared__ float vl[6][kSegBlock];
+    const uint32_t U = hdr->n_unique;
+    if (U < 2) return;
+    uint64_t off = seg_level_off(nn, L0), vsize = U;
+    for (int l = 0; l < L0; ++l) vsize = (vsize + 1) / 2;
+    const uint64_t base = (uint64_t)blockIdx.x * kSegBlock;
+    for (uint32_t j = threadIdx.x; j < kSegBlock; j += kThreads)
+        if (base + j < vsize)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) vl[c][j] = seg[c * cap + off + base + j];
+    __syncthreads();
+    seg_levels(vl, seg, cap, nn, U, L0, base, false);
 }
 
 // totalOrder max (HI) / min over leaves [a, b] of component c
@@ -881,8 +1006,8 @@ __global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__res
     const uint32_t U = hdr->n_unique;
     uint32_t p = blockIdx.x * kThreads + threadIdx.x;
     if (U < 2) {
-        // one leaf: no node, and k_seg_leaf did not run -- the sorted
-        // triangle records here (k_seg_leaf packs every leaf run otherwise)
+        // one leaf: no node, and k_seg_build did not run -- the sorted
+        // triangle records here (k_seg_build packs every leaf run otherwise)
         for (uint32_t i = p; i < n; i += gridDim.x * kThreads) {
             float lo[3], hi[3];
             pack_tri(v + 9ull * tri_idx[i], tris_s + 9ull * i, lo, hi);
@@ -986,7 +1111,9 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
         BIH_TRY(dalloc(&t.hist, hist_n, t));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks, t));
+        // + the arrival counts of k_prep and k_seg_build (zero between launches)
+        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks + 2, t));
+        BIH_TRY(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 2 * sizeof(unsigned long long), st));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
         // tag): stale data in fresh memory must not pass for a predecessor's
         // published prefix; afterwards every word carries an older call's
@@ -998,18 +1125,13 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     BIH_TRY(hipEventCreate(&e1));
     BIH_TRY(hipEventRecord(e0, st));
 
-    // header reset (no triangles; otherwise k_prep_final writes the header)
+    // header reset (no triangles; otherwise k_prep's last block writes the header)
     if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
                            t.tri_hi, t.hdr, t.prep_part);
-        // (folding the partials in k_prep's last block instead -- a device-scope
-        // fence per block before the arrival count -- made k_prep 0.147 ms
-        // against 0.016 + 0.012 for the two launches: r04a)
-        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
-                           t.hdr, n, t.prep_part, prep_blocks);
         hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
                            t.vals, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
@@ -1041,14 +1163,20 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr, t.first_idx,
                            t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
         const uint64_t cap = seg_capacity(nn);
-        // (also the sorted triangle records when U >= 2: every leaf run)
-        hipLaunchKernelGGL(k_seg_leaf, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.vals, t.v,
-                           t.tris_s, t.first_idx, t.dup_cnt, t.fit_seg, cap);
-        uint64_t lsize = nn;   // capacity of level L0 (>= its valid entries)
-        for (int L0 = 0; lsize > 1; L0 += kSegSteps) {
-            hipLaunchKernelGGL(k_seg_up, dim3((uint32_t)((lsize + kSegBlock - 1) / kSegBlock)), dim3(kThreads), 0,
-                               st, t.hdr, t.fit_seg, cap, nn, L0);
-            for (int s2 = 0; s2 < kSegSteps; ++s2) lsize = (lsize + 1) / 2;
+        // leaf boxes (and the sorted triangle records of every leaf run when U >= 2) + segment tree levels 0..10 (and, up to 2^20 leaves, the
+        // levels above by the last block); larger trees: k_seg_up per 10 levels
+        const uint64_t seg_blocks = (nn + kSegBlock - 1) / kSegBlock;
+        // (one block builds a whole tree of <= kSegBlock leaves by itself)
+        const int top = seg_blocks > 1 && seg_blocks <= kSegBlock ? 1 : 0;
+        hipLaunchKernelGGL(k_seg_build, dim3((uint32_t)seg_blocks), dim3(kThreads), 0, st, t.hdr, t.vals, t.v,
+                           t.tris_s, t.first_idx, t.dup_cnt, t.fit_seg, cap, nn, top, t.prep_part + 8ull * kPrepBlocks + 1);
+        if (!top && seg_blocks > 1) {
+            uint64_t lsize = seg_blocks;   // capacity of level 10 (>= its valid entries)
+            for (int L0 = kSegSteps; lsize > 1; L0 += kSegSteps) {
+                hipLaunchKernelGGL(k_seg_up, dim3((uint32_t)((lsize + kSegBlock - 1) / kSegBlock)), dim3(kThreads), 0,
+                                   st, t.hdr, t.fit_seg, cap, nn, L0);
+                for (int s2 = 0; s2 < kSegSteps; ++s2) lsize = (lsize + 1) / 2;
+            }
         }
         hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
                            t.axis, t.fit_seg, cap, nn, t.clip);
