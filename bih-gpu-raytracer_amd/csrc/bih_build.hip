@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 // Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
 // (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
-// by k_prep's last block (prep_fold).  The build is a deterministic function of the soup, so an
+// by k_prep_final.  The build is a deterministic function of the soup, so an
 // unchanged hash after a rebuild means an unchanged tree, and the per-camera
 // structures derived from it (bih_capi.cpp finish_build) stay valid.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -71,7 +71,7 @@ __device__ __forceinline__ void content_word(uint32_t w, uint32_t i, uint32_t &x
 }
 
 // Triangle AABB on one axis with std::minmax's rules (App.cpp:103-142):
-// leftmost min, rightmost max (k_prep; leaf_box recomputes it bit-equal).
+// leftmost min, rightmost max (k_prep; k_seg_leaf recomputes it bit-equal).
 __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float &m, float &M) {
     m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
     M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
@@ -84,8 +84,6 @@ __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float 
 // of the FIRST triangle attaining the maximum (or the seed vertex if it ties).
 // Ties only differ in the sign of zero; we reduce (value, index) keys.
 // ---------------------------------------------------------------------------
-__device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t n,
-                          const unsigned long long *part, uint32_t nparts);
 __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
                                                    float *__restrict__ lo, float *__restrict__ hi,
                                                    TreeHeader *hdr,
@@ -116,7 +114,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
         }
     }
     // wave reduce, block reduce through LDS, one partial per block (the
-    // last block folds them in prep_fold: no contended atomics)
+    // single-block k_prep_final folds them: no contended atomics)
     __shared__ unsigned long long s_key[7][kThreads / 64];
     __shared__ uint32_t s_bad[kThreads / 64];
 #pragma unroll
@@ -151,28 +149,13 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
             const unsigned long long o = s_key[a][w];
             r = (a == 6) ? (r ^ o) : (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
-        __hip_atomic_store(part + (size_t)a * gridDim.x + blockIdx.x, r, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        part[(size_t)a * gridDim.x + blockIdx.x] = r;
     }
-    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by prep_fold)
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
         uint32_t b = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
-        __hip_atomic_store(part + (size_t)7 * gridDim.x + blockIdx.x, (unsigned long long)b, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        part[(size_t)7 * gridDim.x + blockIdx.x] = b;
     }
-    // hand-off to the last block (prep_fold): sc1 stores waited for in every
-    // wave, a barrier, one agent-scope add; the last adder folds
-    __shared__ uint32_t s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned long long *arrivals = part + 8ull * kPrepBlocks;
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(arrivals, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned long long)gridDim.x - 1ull;
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) __hip_atomic_store(arrivals, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prep_fold(v, hdr, n, part, gridDim.x);
 }
 
 __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
@@ -193,21 +176,12 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
 }
 
 
-// Fold of k_prep's per-block partials into the header, run by the LAST block
-// of k_prep to finish (no launch of its own).  Hand-off without fences
-// (MI355X_MICROARCH.md, cross-workgroup table, row 1): every block stores its
-// partials with sc1 stores (relaxed agent-scope), waits for them
-// (s_waitcnt vmcnt(0)) in every wave, meets at a barrier, and one lane adds
-// to an arrival counter (agent scope); the block whose add returns
-// nblocks - 1 reads every partial with sc1 loads.  (A __threadfence() per
-// block -- an L2 write-back each -- made k_prep 0.147 ms, r04a; the fold as a
-// kernel of its own took 0.012 ms.)  The extreme triangles' boxes are
-// recomputed from the soup (axis_minmax, the values k_prep stored).
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t n,
-                          const unsigned long long *part, uint32_t nparts) {
+__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
+                                                         const float *__restrict__ lo,
+                                                         const float *__restrict__ hi,
+                                                         TreeHeader *hdr, uint32_t n,
+                                                         const unsigned long long *__restrict__ part,
+                                                         uint32_t nparts) {
     // fold the per-block (value, index) keys: min for lo, max for hi
     __shared__ unsigned long long s_red[8][kThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -215,7 +189,7 @@ __device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t
     for (int a = 0; a < 6; ++a) {
         unsigned long long r = a < 3 ? ~0ull : 0ull;
         for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) {
-            const unsigned long long o = ld_sc1(part + (size_t)a * nparts + i);
+            const unsigned long long o = part[(size_t)a * nparts + i];
             r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -226,13 +200,13 @@ __device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t
     }
     {   // the content hash: XOR of the blocks' partials
         unsigned long long hxy = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= ld_sc1(part + (size_t)6 * nparts + i);
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= part[(size_t)6 * nparts + i];
         for (int off = 32; off > 0; off >>= 1) hxy ^= __shfl_xor(hxy, off);
         if (lane == 0) s_red[6][wv] = hxy;
     }
     {   // non-finite flags of the blocks
         unsigned long long b = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= ld_sc1(part + (size_t)7 * nparts + i);
+        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= part[(size_t)7 * nparts + i];
         for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off);
         if (lane == 0) s_red[7][wv] = b;
     }
@@ -248,10 +222,10 @@ __device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t
         hdr->nonfinite = bad ? 1u : 0u;
         hdr->n_unique = 0;
         hdr->pad0 = 0;
-        hdr->n_tris = n;
     }
     const int a = threadIdx.x;
     if (a >= 3) return;
+    if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
     unsigned long long kmin = s_red[a][0], kmax = s_red[3 + a][0];
     for (uint32_t w = 1; w < kThreads / 64; ++w) {
         kmin = s_red[a][w] < kmin ? s_red[a][w] : kmin;
@@ -259,14 +233,13 @@ __device__ void prep_fold(const float *__restrict__ v, TreeHeader *hdr, uint32_t
     }
     hdr->lo_key[a] = kmin;
     hdr->hi_key[a] = kmax;
-    const uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
-    const uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
-    float m, M, dummy;
-    axis_minmax(v[9ull * ilo + a], v[9ull * ilo + 3 + a], v[9ull * ilo + 6 + a], m, dummy);
-    axis_minmax(v[9ull * ihi + a], v[9ull * ihi + 3 + a], v[9ull * ihi + 6 + a], dummy, M);
-    hdr->scene_lo[a] = m;
-    const float seed = v[a];                   // first vertex (App.cpp:103-106)
-    hdr->scene_hi[a] = (seed < M) ? M : seed;
+    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
+    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
+    hdr->scene_lo[a] = lo[3ull * ilo + a];
+    float mx = hi[3ull * ihi + a];
+    float seed = v[a];                         // first vertex (App.cpp:103-106)
+    hdr->scene_hi[a] = (seed < mx) ? mx : seed;
+    hdr->n_tris = n;
 }
 
 // ---------------------------------------------------------------------------
@@ -649,12 +622,27 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
     // leaf idx's triangle count (m_duplicatesCnts): k_runs left the run's end
     if (idx < (uint32_t)U) dup_cnt[idx] -= (uint32_t)first[idx];
     if (U == 1 && idx == 0) leaf_parent[0] = -1;   // no internal node (U >= 2: every leaf gets a parent below)
+    // the codes around the block's nodes, staged in LDS: the searches of
+    // most nodes (short leaf ranges) stay inside the window; farther probes
+    // read global memory
+    constexpr int kWin = 256, kWinN = kThreads + 2 * kWin;
+    __shared__ uint32_t s_mc[kWinN];
+    const int64_t w0 = (int64_t)blockIdx.x * kThreads - kWin;
+    for (int k = threadIdx.x; k < kWinN; k += kThreads) {
+        const int64_t g = w0 + k;
+        s_mc[k] = (g >= 0 && g < U) ? umc[g] : 0u;
+    }
+    __syncthreads();
+    auto mc = [&](int64_t i) -> uint32_t {
+        const int64_t o = i - w0;
+        return (o >= 0 && o < kWinN) ? s_mc[o] : umc[i];
+    };
     if (U < 2 || idx > (uint32_t)(U - 2)) return;
     if (idx == 0) parent[0] = -1;   // the root; every other node is written as a child below
-    uint32_t cur = umc[idx];
+    uint32_t cur = mc(idx);
     uint32_t pre0 = 0xFFFFFFFFu, pre1 = 0xFFFFFFFFu;
-    if (idx) pre0 = (uint32_t)clz32(cur ^ umc[idx - 1]);
-    if (idx < (uint32_t)(U - 1)) pre1 = (uint32_t)clz32(cur ^ umc[idx + 1]);
+    if (idx) pre0 = (uint32_t)clz32(cur ^ mc(idx - 1));
+    if (idx < (uint32_t)(U - 1)) pre1 = (uint32_t)clz32(cur ^ mc(idx + 1));
     int32_t diff = (int32_t)(pre1 - pre0);
     int d = (0 < diff) - (diff < 0);
     int lcp_min = (int32_t)(((d + 1) / 2) ? pre0 : pre1);   // pre[1 - (d+1)/2]
@@ -662,21 +650,21 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
     do {
         lmax *= 2;
         li = (int32_t)(idx + (uint32_t)(lmax * d));
-        lcp = (li < 0 || li > U - 1) ? -1 : clz32(cur ^ umc[li]);
+        lcp = (li < 0 || li > U - 1) ? -1 : clz32(cur ^ mc(li));
     } while (lcp > lcp_min);
     int l = 0;
     for (int t = lmax / 2; t >= 1; t /= 2) {
         int ti = (int32_t)(idx + (uint32_t)((l + t) * d));
-        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ umc[ti]);
+        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ mc(ti));
         if (lcp > lcp_min) l += t;
     }
     int other = (int32_t)(idx + (uint32_t)(l * d));
-    int lcp_ends = clz32(cur ^ umc[other]);
+    int lcp_ends = clz32(cur ^ mc(other));
     int s = 0, t = l;
     for (;;) {
         t = (int)ceilf((float)t / 2.0f);           // __float2int_ru(t / 2.0f)
         int ti = (int32_t)(idx + (uint32_t)((s + t) * d));
-        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ umc[ti]);
+        lcp = (ti < 0 || ti > U - 1) ? -1 : clz32(cur ^ mc(ti));
         if (lcp > lcp_ends) s += t;
         if (t == 1) break;
     }
@@ -691,7 +679,7 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
     is_leaf[2 * idx + 1] = l1;
     if (l0) leaf_parent[split] = (int32_t)idx; else parent[split] = (int32_t)idx;
     if (l1) leaf_parent[split + 1] = (int32_t)idx; else parent[split + 1] = (int32_t)idx;
-    axis_out[idx] = (clz32(umc[split] ^ umc[split + 1]) + 1) % 3;
+    axis_out[idx] = (clz32(mc(split) ^ mc(split + 1)) + 1) % 3;
 }
 
 // ---------------------------------------------------------------------------
@@ -778,8 +766,10 @@ __device__ __forceinline__ void leaf_box(const uint32_t *__restrict__ tri_idx, c
 // leaves are combined (a partial last entry is never read by a query).  The
 // last level's entries are stored sc1 when `hand_off` (the last-block
 // hand-off of k_seg_build).
+template <uint32_t NT>
 __device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__restrict__ seg, uint64_t cap,
                                            uint64_t nn, uint32_t U, int L0, uint64_t base, bool hand_off) {
+    static_assert(kSegBlock / 2 <= 4 * NT, "r[4]: at most 4 entries per thread per level");
     const uint32_t tid = threadIdx.x;
     uint64_t off = seg_level_off(nn, L0), size = nn;
     uint64_t vsize = U;                             // valid entries of the level
@@ -798,7 +788,7 @@ __device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__rest
         const uint64_t gb = base >> s;              // this block's first entry at level L0+s
         float r[4][6];
         uint32_t nj = 0;
-        for (uint32_t j = tid; j < cnt; j += kThreads, ++nj) {
+        for (uint32_t j = tid; j < cnt; j += NT, ++nj) {
             const uint64_t g = gb + j;
             if (g < vsize) {
                 const bool two = 2 * g + 1 < pvsize;
@@ -812,7 +802,7 @@ __device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__rest
         __syncthreads();
         nj = 0;
         const bool sc1 = hand_off && s == kSegSteps;
-        for (uint32_t j = tid; j < cnt; j += kThreads, ++nj) {
+        for (uint32_t j = tid; j < cnt; j += NT, ++nj) {
             const uint64_t g = gb + j;
             if (g < vsize)
 #pragma unroll
@@ -838,7 +828,8 @@ __device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__rest
 // (MI355X_MICROARCH.md, cross-workgroup table, row 1); larger trees take
 // k_seg_up launches for those levels.  (Round 3: k_seg_leaf + 2 x k_seg_up,
 // 0.035 + 0.018 + 0.012 ms at 1M, r04d.)
-__global__ void __launch_bounds__(kThreads) k_seg_build(const TreeHeader *__restrict__ hdr,
+constexpr uint32_t kSegThreads = 1024;   // k_seg_build: one leaf per thread
+__global__ void __launch_bounds__(kSegThreads) k_seg_build(const TreeHeader *__restrict__ hdr,
                                                         const uint32_t *__restrict__ tri_idx,
                                                         const float *__restrict__ v, float *__restrict__ tris_s,
                                                         const int32_t *__restrict__ first,
@@ -851,7 +842,7 @@ __global__ void __launch_bounds__(kThreads) k_seg_build(const TreeHeader *__rest
     if (U < 2) return;   // (uniform: no block takes part in the hand-off)
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kSegBlock;
-    for (uint32_t j = tid; j < kSegBlock; j += kThreads) {
+    for (uint32_t j = tid; j < kSegBlock; j += kSegThreads) {
         const uint64_t k = base + j;
         if (k < U) {
             float blo[3], bhi[3];
@@ -866,7 +857,7 @@ __global__ void __launch_bounds__(kThreads) k_seg_build(const TreeHeader *__rest
         }
     }
     __syncthreads();
-    seg_levels(vl, seg, cap, nn, U, 0, base, top != 0);
+    seg_levels<kSegThreads>(vl, seg, cap, nn, U, 0, base, top != 0);
     if (!top) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -880,13 +871,13 @@ __global__ void __launch_bounds__(kThreads) k_seg_build(const TreeHeader *__rest
     const uint64_t off10 = seg_level_off(nn, kSegSteps);
     uint64_t vs = U;
     for (int l = 0; l < kSegSteps; ++l) vs = (vs + 1) / 2;
-    for (uint32_t j = tid; j < kSegBlock; j += kThreads)
+    for (uint32_t j = tid; j < kSegBlock; j += kSegThreads)
         if (j < vs)
 #pragma unroll
             for (int c = 0; c < 6; ++c)
                 vl[c][j] = __hip_atomic_load(seg + c * cap + off10 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    seg_levels(vl, seg, cap, nn, U, kSegSteps, 0, false);
+    seg_levels<kSegThreads>(vl, seg, cap, nn, U, kSegSteps, 0, false);
 }
 
 // Levels L0+1 .. L0+kSegSteps from level L0 (trees over 2^20 leaves, levels
@@ -905,7 +896,7 @@ __global__ void __launch_bounds__(kThreads) k_seg_up(const TreeHeader *__restric
 #pragma unroll
             for (int c = 0; c < 6; ++c) vl[c][j] = seg[c * cap + off + base + j];
     __syncthreads();
-    seg_levels(vl, seg, cap, nn, U, L0, base, false);
+    seg_levels<kThreads>(vl, seg, cap, nn, U, L0, base, false);
 }
 
 // totalOrder max (HI) / min over leaves [a, b] of component c
@@ -1111,7 +1102,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
         BIH_TRY(dalloc(&t.hist, hist_n, t));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-        // + the arrival counts of k_prep and k_seg_build (zero between launches)
+        // + k_seg_build's arrival count (zero between launches)
         BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks + 2, t));
         BIH_TRY(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 2 * sizeof(unsigned long long), st));
         // look-back words (k_scan_onepass) start at tag 0 (never a call's
@@ -1125,13 +1116,19 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     BIH_TRY(hipEventCreate(&e1));
     BIH_TRY(hipEventRecord(e0, st));
 
-    // header reset (no triangles; otherwise k_prep's last block writes the header)
+    // header reset (no triangles; otherwise k_prep_final writes the header)
     if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
                            t.tri_hi, t.hdr, t.prep_part);
+        // (folding the partials in k_prep's last block instead -- with a
+        // device-scope fence per block: k_prep 0.147 ms, r04a; with an sc1
+        // store / agent-add / sc1 load hand-off: 0.032 ms, r04e -- against
+        // 0.016 + 0.012 for the two launches)
+        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
+                           t.hdr, n, t.prep_part, prep_blocks);
         hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
                            t.vals, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
@@ -1168,7 +1165,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         const uint64_t seg_blocks = (nn + kSegBlock - 1) / kSegBlock;
         // (one block builds a whole tree of <= kSegBlock leaves by itself)
         const int top = seg_blocks > 1 && seg_blocks <= kSegBlock ? 1 : 0;
-        hipLaunchKernelGGL(k_seg_build, dim3((uint32_t)seg_blocks), dim3(kThreads), 0, st, t.hdr, t.vals, t.v,
+        hipLaunchKernelGGL(k_seg_build, dim3((uint32_t)seg_blocks), dim3(kSegThreads), 0, st, t.hdr, t.vals, t.v,
                            t.tris_s, t.first_idx, t.dup_cnt, t.fit_seg, cap, nn, top, t.prep_part + 8ull * kPrepBlocks + 1);
         if (!top && seg_blocks > 1) {
             uint64_t lsize = seg_blocks;   // capacity of level 10 (>= its valid entries)

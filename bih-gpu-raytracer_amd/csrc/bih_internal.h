@@ -67,7 +67,7 @@ struct TreeHeader {
     uint32_t pad0;
     unsigned long long lo_key[3];   // argmin keys (App.cpp:133-137 tie rules)
     unsigned long long hi_key[3];   // argmax keys
-    unsigned long long content;     // hash of the input soup (k_prep, folded by its last block): the tree is a function of it
+    unsigned long long content;     // hash of the input soup (k_prep / k_prep_final): the tree is a function of it
 };
 
 // Render parameters, passed by value.

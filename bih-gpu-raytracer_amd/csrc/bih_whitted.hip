@@ -44,15 +44,8 @@ constexpr int kWLds = 8;                // stack slots per lane in LDS; deeper o
 constexpr uint32_t kWBlocksPerCU = 32;  // persistent grid of k_wh_trace
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
-constexpr uint32_t kWCounts = 128;      // counter words: [0..9] rays per queue, [16 + 8 d + x] rays of queue d
-                                        // taken from XCD x's part (k_wh_trace_dyn)
+constexpr uint32_t kWCounts = 32;       // counter words: [0..9] rays per queue, [16..25] rays taken (k_wh_trace_dyn)
 constexpr uint32_t kWFetch = 16;
-constexpr uint32_t kWParts = 8;         // queue parts: one per XCD (its L2)
-__device__ __forceinline__ uint32_t wh_xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & (kWParts - 1);
-}
 constexpr uint32_t kWSortBucketsGen = 4096;   // = kWSortBuckets (below): k_wh_gen zeroes the histogram
 constexpr uint32_t kWWorkWords = 18;    // work counters: {nodes, triangles} per bounce, u64 (k_wh_trace_dyn<true>)
 
@@ -481,12 +474,7 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
     stk.spill = spill + (uint64_t)blockIdx.x * kWT + lane;
     const WScene sc = load_wscene(a);
     const uint32_t n = counts[depth];
-    // the queue in kWParts contiguous parts, one per XCD: a wave takes rays
-    // from its own XCD's part (the rays are ordered by origin cell, so each
-    // XCD's L2 holds the nodes and triangles of its own cells), then from the
-    // others' once its part is drained
-    uint32_t part = wh_xcc_id(), parts_left = kWParts;
-    uint32_t *fetch = counts + kWFetch + kWParts * depth;   // rays of each part taken so far
+    uint32_t *fetch = counts + kWFetch + depth;   // rays of queue `depth` taken so far
     const float t_lo = depth ? kBounceTLo : 0.0f;
     const uint32_t *sid_in = reinterpret_cast<const uint32_t *>(qin.p) + 6 * qin.cap;
     WRay r;
@@ -496,21 +484,15 @@ __global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32
         const unsigned long long idle = __ballot(!has);
         if (more && (__popcll(idle) >= BIH_WH_REFILL || idle == ~0ull)) {
             const uint32_t k = (uint32_t)__popcll(idle);
-            // part p holds rays [n p / parts, n (p+1) / parts)
-            const uint32_t p0 = (uint32_t)(((uint64_t)n * part) / kWParts);
-            const uint32_t pn = (uint32_t)(((uint64_t)n * (part + 1u)) / kWParts) - p0;
             uint32_t first = 0;
-            if (lane == 0) first = atomicAdd(fetch + part, k);
+            if (lane == 0) first = atomicAdd(fetch, k);
             first = __builtin_amdgcn_readfirstlane(first);
-            if ((uint64_t)first + k >= pn) {               // u64: no wrap of first + k
-                part = (part + 1u) % kWParts;              // this part is drained: the next one
-                if (--parts_left == 0u) more = false;
-            }
+            if ((uint64_t)first + k >= n) more = false;   // u64: no wrap of first + k
             if (!has) {
                 const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const uint64_t i = (uint64_t)p0 + first + rk;
-                if ((uint64_t)first + rk < pn) {
+                const uint64_t i = (uint64_t)first + rk;
+                if (i < n) {
                     for (int c = 0; c < 3; ++c) {
                         r.o[c] = qin.p[c * qin.cap + i];
                         r.d[c] = qin.p[(3 + c) * qin.cap + i];
