@@ -7,11 +7,11 @@
 //   radix sort    stable LSD sort of (code, tri idx)    (Renderer.cpp:441-445)
 //   k_runs*       reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
 //   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710)
-//   k_fit         clip planes as range queries over a segment tree of the
+//   k_seg_build   leaf boxes + sorted {v0,e1,e2} triangles + segment tree
+//   k_fit         clip planes as range queries over the segment tree of the
 //                 leaf boxes instead of the leaf->root atomics of
 //                 FindClipPlanes (CUDAKernels.cu:497-549): same max/min, no
-//                 atomics
-//   k_pack        16-B render nodes + sorted {v0,e1,e2} triangles
+//                 atomics; and the 16-B render nodes
 // Everything is integer/byte work or exact f32 compares; all arithmetic is
 // compiled with -ffp-contract=off so it matches the strict-IEEE oracle.
 #include <hip/hip_runtime.h>
@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t lt_key(float f) {
 // ---------------------------------------------------------------------------
 // Hash of the input soup: two XOR-sums of murmur3 finalisers of (word, index)
 // (32-bit arithmetic), accumulated by k_prep as it reads the soup and folded
-// by k_prep_final.  The build is a deterministic function of the soup, so an
+// by k_morton's blocks (prep_fold).  The build is a deterministic function of the soup, so an
 // unchanged hash after a rebuild means an unchanged tree, and the per-camera
 // structures derived from it (bih_capi.cpp finish_build) stay valid.
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
         }
     }
     // wave reduce, block reduce through LDS, one partial per block (the
-    // single-block k_prep_final folds them: no contended atomics)
+    // blocks of k_morton fold them: no contended atomics)
     __shared__ unsigned long long s_key[7][kThreads / 64];
     __shared__ uint32_t s_bad[kThreads / 64];
 #pragma unroll
@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, 
         }
         part[(size_t)a * gridDim.x + blockIdx.x] = r;
     }
-    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by k_prep_final)
+    if (threadIdx.x == 7) {   // non-finite coordinates in this block (folded by prep_fold)
         uint32_t b = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) b |= s_bad[w];
         part[(size_t)7 * gridDim.x + blockIdx.x] = b;
@@ -176,19 +176,22 @@ __global__ void k_hdr_init(TreeHeader *hdr, uint32_t n) {
 }
 
 
-__global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict__ v,
-                                                         const float *__restrict__ lo,
-                                                         const float *__restrict__ hi,
-                                                         TreeHeader *hdr, uint32_t n,
-                                                         const unsigned long long *__restrict__ part,
-                                                         uint32_t nparts) {
-    // fold the per-block (value, index) keys: min for lo, max for hi
-    __shared__ unsigned long long s_red[8][kThreads / 64];
+// The fold of k_prep's per-block partials: the scene AABB with the
+// reference's tie rules, the content hash, the non-finite flag.  Every block
+// of k_morton folds them for itself (1024 threads: one partial per thread
+// and array) into slo / shi, and block 0 writes the header -- no launch of
+// its own (round 3's k_prep_final: one block, 0.012 ms).
+template <uint32_t NT>
+__device__ void prep_fold(const float *__restrict__ v, const float *__restrict__ lo, const float *__restrict__ hi,
+                          TreeHeader *hdr, uint32_t n, const unsigned long long *__restrict__ part,
+                          uint32_t nparts, float slo[3], float shi[3]) {
+    constexpr uint32_t NW = NT / 64;
+    __shared__ unsigned long long s_red[8][NW];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         unsigned long long r = a < 3 ? ~0ull : 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) {
+        for (uint32_t i = threadIdx.x; i < nparts; i += NT) {
             const unsigned long long o = part[(size_t)a * nparts + i];
             r = (a < 3) ? (o < r ? o : r) : (o > r ? o : r);
         }
@@ -198,23 +201,25 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
         }
         if (lane == 0) s_red[a][wv] = r;
     }
-    {   // the content hash: XOR of the blocks' partials
-        unsigned long long hxy = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) hxy ^= part[(size_t)6 * nparts + i];
-        for (int off = 32; off > 0; off >>= 1) hxy ^= __shfl_xor(hxy, off);
-        if (lane == 0) s_red[6][wv] = hxy;
-    }
-    {   // non-finite flags of the blocks
-        unsigned long long b = 0ull;
-        for (uint32_t i = threadIdx.x; i < nparts; i += kThreads) b |= part[(size_t)7 * nparts + i];
-        for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off);
-        if (lane == 0) s_red[7][wv] = b;
+    {   // the content hash: XOR of the blocks' partials; non-finite flags
+        unsigned long long hxy = 0ull, b = 0ull;
+        for (uint32_t i = threadIdx.x; i < nparts; i += NT) {
+            hxy ^= part[(size_t)6 * nparts + i];
+            b |= part[(size_t)7 * nparts + i];
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            hxy ^= __shfl_xor(hxy, off);
+            b |= __shfl_xor(b, off);
+        }
+        if (lane == 0) {
+            s_red[6][wv] = hxy;
+            s_red[7][wv] = b;
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        // the rest of the header (k_hdr_init's work when there are triangles)
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
         unsigned long long hxy = 0ull, bad = 0ull;
-        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+        for (uint32_t w = 0; w < NW; ++w) {
             hxy ^= s_red[6][w];
             bad |= s_red[7][w];
         }
@@ -222,24 +227,29 @@ __global__ void __launch_bounds__(kThreads) k_prep_final(const float *__restrict
         hdr->nonfinite = bad ? 1u : 0u;
         hdr->n_unique = 0;
         hdr->pad0 = 0;
+        hdr->n_tris = n;
     }
     const int a = threadIdx.x;
-    if (a >= 3) return;
-    if (n == 0) { hdr->scene_lo[a] = 0.f; hdr->scene_hi[a] = 0.f; return; }
-    unsigned long long kmin = s_red[a][0], kmax = s_red[3 + a][0];
-    for (uint32_t w = 1; w < kThreads / 64; ++w) {
-        kmin = s_red[a][w] < kmin ? s_red[a][w] : kmin;
-        kmax = s_red[3 + a][w] > kmax ? s_red[3 + a][w] : kmax;
+    if (a < 3) {
+        unsigned long long kmin = s_red[a][0], kmax = s_red[3 + a][0];
+        for (uint32_t w = 1; w < NW; ++w) {
+            kmin = s_red[a][w] < kmin ? s_red[a][w] : kmin;
+            kmax = s_red[3 + a][w] > kmax ? s_red[3 + a][w] : kmax;
+        }
+        const uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
+        const uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
+        const float mx = hi[3ull * ihi + a];
+        const float seed = v[a];                   // first vertex (App.cpp:103-106)
+        slo[a] = lo[3ull * ilo + a];
+        shi[a] = (seed < mx) ? mx : seed;
+        if (blockIdx.x == 0) {
+            hdr->lo_key[a] = kmin;
+            hdr->hi_key[a] = kmax;
+            hdr->scene_lo[a] = slo[a];
+            hdr->scene_hi[a] = shi[a];
+        }
     }
-    hdr->lo_key[a] = kmin;
-    hdr->hi_key[a] = kmax;
-    uint32_t ilo = 0xFFFFFFFFu - (uint32_t)(kmin & 0xFFFFFFFFull);
-    uint32_t ihi = 0xFFFFFFFFu - (uint32_t)(kmax & 0xFFFFFFFFull);
-    hdr->scene_lo[a] = lo[3ull * ilo + a];
-    float mx = hi[3ull * ihi + a];
-    float seed = v[a];                         // first vertex (App.cpp:103-106)
-    hdr->scene_hi[a] = (seed < mx) ? mx : seed;
-    hdr->n_tris = n;
+    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -255,13 +265,13 @@ __device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
 }
 
 __device__ __forceinline__ uint32_t morton_code(const float *__restrict__ lo, const float *__restrict__ hi,
-                                                const TreeHeader *__restrict__ hdr, uint32_t i) {
+                                                const float slo[3], const float shi[3], uint32_t i) {
     float q[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         float c = (lo[3ull * i + a] + hi[3ull * i + a]) / 2.0f;
-        float num = c - hdr->scene_lo[a];
-        float den = hdr->scene_hi[a] - hdr->scene_lo[a];
+        float num = c - slo[a];
+        float den = shi[a] - slo[a];
         float x = (num / den) * 1024.0f;
         q[a] = fminf(fmaxf(x, 0.0f), 1023.0f);
     }
@@ -280,21 +290,25 @@ constexpr int kRdPasses = 3;
 constexpr int kRsBlock = 1024;
 constexpr int kRsWaves = kRsBlock / 64;
 constexpr int kRsPer = kRsTile / kRsBlock;            // 4
-__global__ void __launch_bounds__(kRsBlock) k_morton(const float *__restrict__ lo,
+__global__ void __launch_bounds__(kRsBlock) k_morton(const float *__restrict__ v,
+                                                     const float *__restrict__ lo,
                                                      const float *__restrict__ hi,
-                                                     const TreeHeader *__restrict__ hdr, uint32_t n,
+                                                     TreeHeader *__restrict__ hdr, uint32_t n,
+                                                     const unsigned long long *__restrict__ part, uint32_t nparts,
                                                      uint32_t *__restrict__ keys,
                                                      uint32_t *__restrict__ vals,
                                                      uint32_t *__restrict__ hist, uint32_t nblocks) {
     __shared__ uint32_t h[kRdBins];
+    __shared__ float s_lo[3], s_hi[3];
     for (uint32_t k = threadIdx.x; k < kRdBins; k += kRsBlock) h[k] = 0u;
-    __syncthreads();
+    prep_fold<kRsBlock>(v, lo, hi, hdr, n, part, nparts, s_lo, s_hi);   // (ends with a barrier)
+    const float slo[3] = {s_lo[0], s_lo[1], s_lo[2]}, shi[3] = {s_hi[0], s_hi[1], s_hi[2]};
     const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
 #pragma unroll
     for (int r = 0; r < kRsPer; ++r) {
         const uint64_t i = base + (uint64_t)r * kRsBlock + threadIdx.x;
         if (i < n) {
-            const uint32_t key = morton_code(lo, hi, hdr, (uint32_t)i);
+            const uint32_t key = morton_code(lo, hi, slo, shi, (uint32_t)i);
             keys[i] = key;
             vals[i] = (uint32_t)i;
             atomicAdd(&h[key & (kRdBins - 1u)], 1u);
@@ -957,15 +971,33 @@ __device__ __forceinline__ float seg_query_pipe(const float *__restrict__ seg, u
     return res;
 }
 
+// The clip planes of node p and its 16-byte render record (k_pack_nodes'
+// layout, bih_internal.h) in one pass: the node's thread has every field.
+// A one-leaf tree has no node: the threads pack the sorted triangle records
+// instead (k_seg_build packs them for U >= 2).
 __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
                                                   const int2 *__restrict__ node_rng,
                                                   const int32_t *__restrict__ children,
                                                   const int32_t *__restrict__ axis,
                                                   const float *__restrict__ seg, uint64_t cap, uint64_t nn,
-                                                  float *__restrict__ clip) {
+                                                  float *__restrict__ clip,
+                                                  const uint8_t *__restrict__ is_leaf,
+                                                  const int32_t *__restrict__ first,
+                                                  const uint32_t *__restrict__ cnt, uint4 *__restrict__ nodes,
+                                                  const float *__restrict__ v, const uint32_t *__restrict__ tri_idx,
+                                                  uint32_t n, float *__restrict__ tris_s,
+                                                  TreeHeader *__restrict__ hdr_host) {
     const uint32_t U = hdr->n_unique;
     const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
-    if (U < 2 || p >= U - 1) return;
+    if (p == 0) *hdr_host = *hdr;   // the host reads it after the stream synchronises (build_tree_device)
+    if (U < 2) {
+        for (uint32_t i = p; i < n; i += gridDim.x * kThreads) {
+            float lo[3], hi[3];
+            pack_tri(v + 9ull * tri_idx[i], tris_s + 9ull * i, lo, hi);
+        }
+        return;
+    }
+    if (p >= U - 1) return;
     const int2 rg = node_rng[p];
     const uint32_t split = (uint32_t)children[2 * p];
     const int ax = axis[p];
@@ -976,50 +1008,23 @@ __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__
     const float lhi = seg_query<true>(seg + (3 + ax) * cap, nn, (uint32_t)rg.x, split);
     const float rlo = seg_query<false>(seg + ax * cap, nn, split + 1u, (uint32_t)rg.y);
 #endif
-    clip[2 * p] = tmax(-FLT_MAX, lhi);          // initial values GPUArrayManager.cpp:79-80
-    clip[2 * p + 1] = tmin(FLT_MAX, rlo);
-}
-
-// ---------------------------------------------------------------------------
-// k_pack_*: render layout (see bih_internal.h).
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_pack_nodes(const TreeHeader *__restrict__ hdr,
-                                                         const float *__restrict__ clip,
-                                                         const int32_t *__restrict__ axis,
-                                                         const int32_t *__restrict__ children,
-                                                         const uint8_t *__restrict__ is_leaf,
-                                                         const int32_t *__restrict__ first,
-                                                         const uint32_t *__restrict__ cnt,
-                                                         uint4 *__restrict__ nodes,
-                                                         const float *__restrict__ v,
-                                                         const uint32_t *__restrict__ tri_idx, uint32_t n,
-                                                         float *__restrict__ tris_s) {
-    const uint32_t U = hdr->n_unique;
-    uint32_t p = blockIdx.x * kThreads + threadIdx.x;
-    if (U < 2) {
-        // one leaf: no node, and k_seg_build did not run -- the sorted
-        // triangle records here (k_seg_build packs every leaf run otherwise)
-        for (uint32_t i = p; i < n; i += gridDim.x * kThreads) {
-            float lo[3], hi[3];
-            pack_tri(v + 9ull * tri_idx[i], tris_s + 9ull * i, lo, hi);
-        }
-        return;
-    }
-    if (p >= U - 1) return;
-    uint32_t split = (uint32_t)children[2 * p];
-    uint32_t lL = is_leaf[2 * p], lR = is_leaf[2 * p + 1];
-    uint32_t mid = (uint32_t)first[split + 1];
-    uint32_t cL = lL ? cnt[split] : 0u, cR = lR ? cnt[split + 1] : 0u;
-    uint32_t codeL = (cL >= 1 && cL <= 3) ? cL : 0u;
-    uint32_t codeR = (cR >= 1 && cR <= 3) ? cR : 0u;
+    const float c0 = tmax(-FLT_MAX, lhi);          // initial values GPUArrayManager.cpp:79-80
+    const float c1 = tmin(FLT_MAX, rlo);
+    clip[2 * p] = c0;
+    clip[2 * p + 1] = c1;
+    // the render record (k_pack_nodes until round 4)
+    const uint32_t lL = is_leaf[2 * p], lR = is_leaf[2 * p + 1];
+    const uint32_t mid = (uint32_t)first[split + 1];
+    const uint32_t cL = lL ? cnt[split] : 0u, cR = lR ? cnt[split + 1] : 0u;
+    const uint32_t codeL = (cL >= 1 && cL <= 3) ? cL : 0u;
+    const uint32_t codeR = (cR >= 1 && cR <= 3) ? cR : 0u;
     uint4 nd;
-    nd.x = __float_as_uint(clip[2 * p]);
-    nd.y = __float_as_uint(clip[2 * p + 1]);
-    nd.z = split | ((uint32_t)axis[p] << 27) | (lL << 29) | (lR << 30);
+    nd.x = __float_as_uint(c0);
+    nd.y = __float_as_uint(c1);
+    nd.z = split | ((uint32_t)ax << 27) | (lL << 29) | (lR << 30);
     nd.w = mid | (codeL << 27) | (codeR << 29);
     nodes[p] = nd;
 }
-
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kThreads - 1) / kThreads); }
 
@@ -1061,6 +1066,9 @@ void free_tree_device(DeviceTree &t) {
                     t.hist, t.partials, t.prep_part};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (t.hdr_host) (void)hipHostFree(t.hdr_host);
+    if (t.ev0) (void)hipEventDestroy(t.ev0);
+    if (t.ev1) (void)hipEventDestroy(t.ev1);
     if (t.owns_v && t.v) (void)hipFree(t.v);
     DeviceTree blank;
     blank.device = t.device;
@@ -1111,26 +1119,27 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         // (unique) tag
         BIH_TRY(hipMemsetAsync(t.partials, 0, (2 * (uint64_t)max_parts + 2) * sizeof(uint32_t), st));
     }
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    BIH_TRY(hipEventCreate(&e0));
-    BIH_TRY(hipEventCreate(&e1));
-    BIH_TRY(hipEventRecord(e0, st));
+    // timing events and the pinned copy of the header: once per tree
+    if (!t.ev0) {
+        BIH_TRY(hipEventCreate(&t.ev0));
+        BIH_TRY(hipEventCreate(&t.ev1));
+        BIH_TRY(hipHostMalloc((void **)&t.hdr_host, sizeof(TreeHeader), hipHostMallocDefault));
+    }
+    BIH_TRY(hipEventRecord(t.ev0, st));
 
-    // header reset (no triangles; otherwise k_prep_final writes the header)
+    // header reset (no triangles; otherwise k_morton's block 0 writes the header)
     if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
 
     if (n > 0) {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
                            t.tri_hi, t.hdr, t.prep_part);
-        // (folding the partials in k_prep's last block instead -- with a
-        // device-scope fence per block: k_prep 0.147 ms, r04a; with an sc1
-        // store / agent-add / sc1 load hand-off: 0.032 ms, r04e -- against
-        // 0.016 + 0.012 for the two launches)
-        hipLaunchKernelGGL(k_prep_final, dim3(1), dim3(kThreads), 0, st, t.v, t.tri_lo, t.tri_hi,
-                           t.hdr, n, t.prep_part, prep_blocks);
-        hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.tri_lo, t.tri_hi, t.hdr, n, t.keys,
-                           t.vals, t.hist, rs_blocks);
+        // (the fold of the partials: every k_morton block for itself; in
+        // k_prep's last block instead -- a device-scope fence per block: k_prep
+        // 0.147 ms, r04a; an sc1 store / agent-add / sc1 load hand-off: 0.032
+        // ms, r04e -- against 0.016 + 0.012 for k_prep + k_prep_final)
+        hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.v, t.tri_lo, t.tri_hi, t.hdr, n,
+                           t.prep_part, prep_blocks, t.keys, t.vals, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
         // counted the first digit); the sorted pairs end in keys2 / vals2,
         // which then become keys / vals
@@ -1176,20 +1185,19 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
             }
         }
         hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
-                           t.axis, t.fit_seg, cap, nn, t.clip);
-        hipLaunchKernelGGL(k_pack_nodes, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.clip,
-                           t.axis, t.children, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes, t.v, t.vals, n,
-                           t.tris_s);
+                           t.axis, t.fit_seg, cap, nn, t.clip, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes, t.v,
+                           t.vals, n, t.tris_s, t.hdr_host);
         BIH_TRY(hipGetLastError());
     }
-    BIH_TRY(hipEventRecord(e1, st));
-    TreeHeader h;
-    BIH_TRY(hipMemcpyAsync(&h, t.hdr, sizeof h, hipMemcpyDeviceToHost, st));
+    BIH_TRY(hipEventRecord(t.ev1, st));
+    // the header comes back through pinned host memory that k_fit's first
+    // thread writes (no copy-engine transfer after the last kernel); a tree
+    // without triangles takes the copy
+    if (n == 0) BIH_TRY(hipMemcpyAsync(t.hdr_host, t.hdr, sizeof(TreeHeader), hipMemcpyDeviceToHost, st));
     BIH_TRY(hipStreamSynchronize(st));
+    const TreeHeader h = *t.hdr_host;
     float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    (void)hipEventElapsedTime(&ms, t.ev0, t.ev1);
     if (ms_out) *ms_out = ms;
     t.u = h.n_unique;
     t.content = h.content;

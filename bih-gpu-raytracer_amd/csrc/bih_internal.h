@@ -67,7 +67,7 @@ struct TreeHeader {
     uint32_t pad0;
     unsigned long long lo_key[3];   // argmin keys (App.cpp:133-137 tie rules)
     unsigned long long hi_key[3];   // argmax keys
-    unsigned long long content;     // hash of the input soup (k_prep / k_prep_final): the tree is a function of it
+    unsigned long long content;     // hash of the input soup (k_prep, folded in k_morton): the tree is a function of it
 };
 
 // Render parameters, passed by value.
@@ -194,6 +194,8 @@ struct DeviceTree {
     uint32_t *hist = nullptr;                       // radix histograms
     uint32_t *partials = nullptr;
     unsigned long long *prep_part = nullptr;        // k_prep per-block AABB keys
+    TreeHeader *hdr_host = nullptr;                 // pinned host copy of hdr (k_fit writes it)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;        // build timing (build_ms)
 };
 
 // builder (bih_build.hip); returns hipError_t as int
