@@ -155,12 +155,6 @@ struct bih_tree {
     // it (and after the renders that read their set), not after each other
     hipEvent_t ev_tree = nullptr;
     bool tree_pending = false;
-    // A render's XORWOW advance (the next frame's input state) runs on this
-    // stream, forked from the render's stream after its waits, so the render
-    // kernel does not wait for it; the render's stream joins it before the
-    // slot's completion event (evd), and ev_rng follows it.
-    hipStream_t adv_stream = nullptr;
-    hipEvent_t ev_fork[kSlots] = {}, ev_adv[kSlots] = {};
     double build_ms = 0.0;
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
     // render state cache (Renderer::d_rand_state / CreateCUDABuffers)
@@ -214,14 +208,17 @@ hipError_t tree_malloc(bih_tree *tr, T **p, size_t bytes) {
     return e;
 }
 
+// Makes `dev` current for the call and restores the caller's device after
+// it; no hipSetDevice when it already is (the per-call host path).
 struct DeviceGuard {
     int prev = -1;
+    bool changed = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        (void)hipSetDevice(dev);
+        if (prev != dev) changed = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (changed && prev >= 0) (void)hipSetDevice(prev);
     }
 };
 
@@ -407,11 +404,6 @@ int create_tree(int device, void *stream, bih_tree **out) {
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_rng, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_tree, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&tr->adv_stream, hipStreamNonBlocking);
-    for (int k = 0; k < kSlots && e == hipSuccess; ++k) {
-        e = hipEventCreateWithFlags(&tr->ev_fork[k], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&tr->ev_adv[k], hipEventDisableTiming);
-    }
     for (CamSet &c : tr->cs) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c.ev_bins, hipEventDisableTiming);
         if (e == hipSuccess) e = hipHostMalloc((void **)&c.bins_host, 4 * sizeof(uint32_t), hipHostMallocDefault);
@@ -584,14 +576,6 @@ void bih_free(bih_tree *tr) {
     }
     if (tr->ev_rng) (void)hipEventDestroy(tr->ev_rng);
     if (tr->ev_tree) (void)hipEventDestroy(tr->ev_tree);
-    if (tr->adv_stream) {
-        (void)hipStreamSynchronize(tr->adv_stream);
-        (void)hipStreamDestroy(tr->adv_stream);
-    }
-    for (int k = 0; k < kSlots; ++k) {
-        if (tr->ev_fork[k]) (void)hipEventDestroy(tr->ev_fork[k]);
-        if (tr->ev_adv[k]) (void)hipEventDestroy(tr->ev_adv[k]);
-    }
     if (tr->owns_stream) (void)hipStreamDestroy(tr->stream);
     delete tr;
 }
@@ -1246,15 +1230,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
         a.rng_split = split;
     }
-    // the advance: in line when the render reads its split start states,
-    // else forked onto adv_stream below, once everything this render waits
-    // for and issues before its kernel is in the stream
-    const bool fork_adv = split == nullptr;
-    if (!fork_adv) {
-        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
-                                             2 * spp * a.fpi, a.nsplit));
-        if (rc) return rc;
-    }
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
+                                         2 * spp * a.fpi, a.nsplit));
+    if (rc) return rc;
     tr->next_frame = frame + nframes;
     if (use_bins) {
         a.bin_off = c.bins.off;
@@ -1297,24 +1275,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         if (le) return map_hip(le);
         c.fast_valid = true;
     }
-    // the next render (on any stream) orders after the advance, the
+    // the next render (on any stream) orders after the advance above, the
     // per-camera records, the shortcut boxes and the tile queue, which it
     // reads as they stand now
-    if (fork_adv) {
-        // fork: adv_stream follows everything issued on st so far (the slot
-        // and ring waits above, the camera's structures), runs the advance,
-        // and ev_rng follows it there; st goes on to the render kernel
-        e = hipEventRecord(tr->ev_fork[slot], st);
-        if (e == hipSuccess) e = hipStreamWaitEvent(tr->adv_stream, tr->ev_fork[slot], 0);
-        if (e != hipSuccess) return map_hip((int)e);
-        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes,
-                                             tr->adv_stream, nullptr, 2 * spp * a.fpi, 1));
-        if (rc) return rc;
-        e = hipEventRecord(tr->ev_adv[slot], tr->adv_stream);
-        if (e == hipSuccess) e = hipEventRecord(tr->ev_rng, tr->adv_stream);
-    } else {
-        e = hipEventRecord(tr->ev_rng, st);
-    }
+    e = hipEventRecord(tr->ev_rng, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
     memcpy(a.cam, cam, sizeof a.cam);
@@ -1357,11 +1321,6 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         if (e != hipSuccess) return map_hip((int)e);
     }
     tr->last_timed = tr->timing;
-    // (join: the slot's completion covers the forked advance too)
-    if (fork_adv) {
-        e = hipStreamWaitEvent(st, tr->ev_adv[slot], 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
