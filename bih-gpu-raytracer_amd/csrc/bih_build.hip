@@ -5,9 +5,9 @@
 //   k_morton      normalised centroid -> 30-bit Morton  (App.cpp:144-156,
 //                                                       Renderer.cpp:114-145)
 //   radix sort    stable LSD sort of (code, tri idx)    (Renderer.cpp:441-445)
-//   k_runs        reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472),
+//   k_runs        reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
+//   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710),
 //                 sorted {v0,e1,e2} triangles and their boxes
-//   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710)
 //   k_seg_build   leaf boxes + segment tree
 //   k_fit         clip planes as range queries over the segment tree of the
 //                 leaf boxes instead of the leaf->root atomics of
@@ -571,9 +571,7 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
                                                    unsigned long long *status, uint32_t tag,
                                                    uint32_t *__restrict__ umc, int32_t *__restrict__ first,
                                                    uint32_t *__restrict__ run_end, uint32_t *__restrict__ leaf_of,
-                                                   TreeHeader *hdr, const uint32_t *__restrict__ vals,
-                                                   const float *__restrict__ v, float *__restrict__ tris_s,
-                                                   float *__restrict__ slo, float *__restrict__ shi) {
+                                                   TreeHeader *hdr) {
     __shared__ uint32_t lds[4];
     __shared__ uint32_t s_prefix;
     const uint32_t tile = blockIdx.x;
@@ -599,21 +597,6 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
         sum += f ? 1u : 0u;
     }
     const uint32_t nxt = (base + kScanItems < n) ? keys[base + kScanItems] : 0u;
-    // the sorted triangle records {v0, e1, e2} and their boxes in sorted
-    // order (k_seg_build reads each leaf's boxes as one contiguous run): the
-    // gathers of the soup are issued here, so they overlap the look-back
-#pragma unroll 2
-    for (int k = 0; k < kScanItems; ++k) {
-        const uint64_t i = base + k;
-        if (i >= n) break;
-        float lo[3], hi[3];
-        pack_tri(v + 9ull * vals[i], tris_s + 9ull * i, lo, hi);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            slo[3 * i + a] = lo[a];
-            shi[3 * i + a] = hi[a];
-        }
-    }
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan(sum, lds, &tot);
     if (threadIdx.x < 64) {
@@ -663,9 +646,24 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
                                                      int32_t *__restrict__ axis_out,
                                                      int32_t *__restrict__ parent,
                                                      int32_t *__restrict__ leaf_parent,
-                                                     int2 *__restrict__ node_rng) {
+                                                     int2 *__restrict__ node_rng, uint32_t n,
+                                                     const uint32_t *__restrict__ vals,
+                                                     const float *__restrict__ v, float *__restrict__ tris_s,
+                                                     float *__restrict__ slo, float *__restrict__ shi) {
     const int U = (int)hdr->n_unique;
     uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
+    // sorted triangle idx: its record {v0, e1, e2} and its box, in sorted
+    // order (k_seg_build reads each leaf's boxes as one contiguous run); the
+    // gather of the soup overlaps this kernel's searches
+    if (idx < n) {
+        float lo[3], hi[3];
+        pack_tri(v + 9ull * vals[idx], tris_s + 9ull * idx, lo, hi);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            slo[3ull * idx + a] = lo[a];
+            shi[3ull * idx + a] = hi[a];
+        }
+    }
     // leaf idx's triangle count (m_duplicatesCnts): k_runs left the run's end
     if (idx < (uint32_t)U) dup_cnt[idx] -= (uint32_t)first[idx];
     if (U == 1 && idx == 0) leaf_parent[0] = -1;   // no internal node (U >= 2: every leaf gets a parent below)
@@ -774,7 +772,7 @@ __device__ __forceinline__ uint64_t seg_level_off(uint64_t nn, int L) {
 
 
 // Leaf k's box (CUDAKernels.cu:511-529): the boxes of its run of sorted
-// triangles, contiguous (k_runs wrote them in sorted order).
+// triangles, contiguous (k_karras wrote them in sorted order).
 __device__ __forceinline__ void leaf_box(const float *__restrict__ slo, const float *__restrict__ shi,
                                          const int32_t *__restrict__ first, const uint32_t *__restrict__ cnt,
                                          uint32_t k, float blo[3], float bhi[3]) {
@@ -1173,10 +1171,11 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
             const uint32_t nb = (n + kScanTile - 1) / kScanTile;
             hipLaunchKernelGGL(k_runs, dim3(nb), dim3(kThreads), 0, st, t.keys, n,
                                reinterpret_cast<unsigned long long *>(t.partials), next_scan_tag(), t.unique_mc,
-                               t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr, t.vals, t.v, t.tris_s, t.slo, t.shi);
+                               t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr);
         }
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr, t.first_idx,
-                           t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
+                           t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng, n, t.vals,
+                           t.v, t.tris_s, t.slo, t.shi);
         const uint64_t cap = seg_capacity(nn);
         // leaf boxes (and the sorted triangle records of every leaf run when U >= 2) + segment tree levels 0..10 (and, up to 2^20 leaves, the
         // levels above by the last block); larger trees: k_seg_up per 10 levels
