@@ -5,10 +5,9 @@
 //   k_morton      normalised centroid -> 30-bit Morton  (App.cpp:144-156,
 //                                                       Renderer.cpp:114-145)
 //   radix sort    stable LSD sort of (code, tri idx)    (Renderer.cpp:441-445)
-//   k_runs        reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
-//   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710),
-//                 sorted {v0,e1,e2} triangles and their boxes
-//   k_seg_build   leaf boxes + segment tree
+//   k_runs*       reduce_by_key + unique_by_key_copy    (Renderer.cpp:450-472)
+//   k_karras      Karras-2012 internal nodes            (CUDAKernels.cu:591-710)
+//   k_seg_build   leaf boxes + sorted {v0,e1,e2} triangles + segment tree
 //   k_fit         clip planes as range queries over the segment tree of the
 //                 leaf boxes instead of the leaf->root atomics of
 //                 FindClipPlanes (CUDAKernels.cu:497-549): same max/min, no
@@ -76,21 +75,6 @@ __device__ __forceinline__ void content_word(uint32_t w, uint32_t i, uint32_t &x
 __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float &m, float &M) {
     m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
     M = x0; if (!(x1 < M)) M = x1; if (!(x2 < M)) M = x2;
-}
-
-// Sorted triangle i as the render reads it: {v0, e1 = v1 - v0, e2 = v2 - v0}
-// (CUDAKernels.cu:18-19), from the input triangle p; returns its AABB (the
-// values k_prep wrote, axis_minmax).
-__device__ __forceinline__ void pack_tri(const float *__restrict__ p, float *__restrict__ o, float lo[3],
-                                         float hi[3]) {
-    float q[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) q[k] = p[k];
-    o[0] = q[0]; o[1] = q[1]; o[2] = q[2];
-    o[3] = q[3] - q[0]; o[4] = q[4] - q[1]; o[5] = q[5] - q[2];   // v0v1, CUDAKernels.cu:18
-    o[6] = q[6] - q[0]; o[7] = q[7] - q[1]; o[8] = q[8] - q[2];   // v0v2, :19
-#pragma unroll
-    for (int a = 0; a < 3; ++a) axis_minmax(q[a], q[3 + a], q[6 + a], lo[a], hi[a]);
 }
 
 // k_prep: lo/hi per triangle (std::minmax: leftmost min, rightmost max) and
@@ -646,24 +630,9 @@ __global__ void __launch_bounds__(kThreads) k_karras(const uint32_t *__restrict_
                                                      int32_t *__restrict__ axis_out,
                                                      int32_t *__restrict__ parent,
                                                      int32_t *__restrict__ leaf_parent,
-                                                     int2 *__restrict__ node_rng, uint32_t n,
-                                                     const uint32_t *__restrict__ vals,
-                                                     const float *__restrict__ v, float *__restrict__ tris_s,
-                                                     float *__restrict__ slo, float *__restrict__ shi) {
+                                                     int2 *__restrict__ node_rng) {
     const int U = (int)hdr->n_unique;
     uint32_t idx = blockIdx.x * kThreads + threadIdx.x;
-    // sorted triangle idx: its record {v0, e1, e2} and its box, in sorted
-    // order (k_seg_build reads each leaf's boxes as one contiguous run); the
-    // gather of the soup overlaps this kernel's searches
-    if (idx < n) {
-        float lo[3], hi[3];
-        pack_tri(v + 9ull * vals[idx], tris_s + 9ull * idx, lo, hi);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            slo[3ull * idx + a] = lo[a];
-            shi[3ull * idx + a] = hi[a];
-        }
-    }
     // leaf idx's triangle count (m_duplicatesCnts): k_runs left the run's end
     if (idx < (uint32_t)U) dup_cnt[idx] -= (uint32_t)first[idx];
     if (U == 1 && idx == 0) leaf_parent[0] = -1;   // no internal node (U >= 2: every leaf gets a parent below)
@@ -770,25 +739,40 @@ __device__ __forceinline__ uint64_t seg_level_off(uint64_t nn, int L) {
     return off;
 }
 
-
-// Leaf k's box (CUDAKernels.cu:511-529): the boxes of its run of sorted
-// triangles, contiguous (k_karras wrote them in sorted order).
-__device__ __forceinline__ void leaf_box(const float *__restrict__ slo, const float *__restrict__ shi,
-                                         const int32_t *__restrict__ first, const uint32_t *__restrict__ cnt,
-                                         uint32_t k, float blo[3], float bhi[3]) {
-    const uint64_t f = (uint64_t)first[k];
-    const uint32_t c = cnt[k];
+// Sorted triangle i as the render reads it: {v0, e1 = v1 - v0, e2 = v2 - v0}
+// (CUDAKernels.cu:18-19), from the input triangle p; returns its AABB (the
+// values k_prep wrote, axis_minmax).
+__device__ __forceinline__ void pack_tri(const float *__restrict__ p, float *__restrict__ o, float lo[3],
+                                         float hi[3]) {
+    float q[9];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        blo[a] = slo[3 * f + a];
-        bhi[a] = shi[3 * f + a];
-    }
-    for (uint32_t i = 1; i < c; ++i)
+    for (int k = 0; k < 9; ++k) q[k] = p[k];
+    o[0] = q[0]; o[1] = q[1]; o[2] = q[2];
+    o[3] = q[3] - q[0]; o[4] = q[4] - q[1]; o[5] = q[5] - q[2];   // v0v1, CUDAKernels.cu:18
+    o[6] = q[6] - q[0]; o[7] = q[7] - q[1]; o[8] = q[8] - q[2];   // v0v2, :19
+#pragma unroll
+    for (int a = 0; a < 3; ++a) axis_minmax(q[a], q[3 + a], q[6 + a], lo[a], hi[a]);
+}
+
+// Leaf k's box (CUDAKernels.cu:511-529), and the sorted triangle records of
+// its run (the runs partition the sorted triangles: read once with the
+// vertices the boxes come from).
+__device__ __forceinline__ void leaf_box(const uint32_t *__restrict__ tri_idx, const float *__restrict__ v,
+                                         float *__restrict__ tris_s, const int32_t *__restrict__ first,
+                                         const uint32_t *__restrict__ cnt, uint32_t k, float blo[3],
+                                         float bhi[3]) {
+    const int32_t f = first[k];
+    const uint32_t c = cnt[k];
+    pack_tri(v + 9ull * tri_idx[f], tris_s + 9ull * f, blo, bhi);
+    for (uint32_t i = 1; i < c; ++i) {
+        float tlo[3], thi[3];
+        pack_tri(v + 9ull * tri_idx[f + i], tris_s + 9ull * (f + i), tlo, thi);
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            blo[a] = tmin(blo[a], slo[3 * (f + i) + a]);
-            bhi[a] = tmax(bhi[a], shi[3 * (f + i) + a]);
+            blo[a] = tmin(blo[a], tlo[a]);
+            bhi[a] = tmax(bhi[a], thi[a]);
         }
+    }
 }
 
 // Levels L0+1 .. L0+kSegSteps of the segment tree from level-L0 entries
@@ -860,8 +844,8 @@ __device__ __forceinline__ void seg_levels(float (*vl)[kSegBlock], float *__rest
 // 0.035 + 0.018 + 0.012 ms at 1M, r04d.)
 constexpr uint32_t kSegThreads = 1024;   // k_seg_build: one leaf per thread
 __global__ void __launch_bounds__(kSegThreads) k_seg_build(const TreeHeader *__restrict__ hdr,
-                                                        const float *__restrict__ slo,
-                                                        const float *__restrict__ shi,
+                                                        const uint32_t *__restrict__ tri_idx,
+                                                        const float *__restrict__ v, float *__restrict__ tris_s,
                                                         const int32_t *__restrict__ first,
                                                         const uint32_t *__restrict__ cnt, float *__restrict__ seg,
                                                         uint64_t cap, uint64_t nn, int top,
@@ -876,7 +860,7 @@ __global__ void __launch_bounds__(kSegThreads) k_seg_build(const TreeHeader *__r
         const uint64_t k = base + j;
         if (k < U) {
             float blo[3], bhi[3];
-            leaf_box(slo, shi, first, cnt, (uint32_t)k, blo, bhi);
+            leaf_box(tri_idx, v, tris_s, first, cnt, (uint32_t)k, blo, bhi);
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 vl[a][j] = blo[a];
@@ -989,6 +973,8 @@ __device__ __forceinline__ float seg_query_pipe(const float *__restrict__ seg, u
 
 // The clip planes of node p and its 16-byte render record (k_pack_nodes'
 // layout, bih_internal.h) in one pass: the node's thread has every field.
+// A one-leaf tree has no node: the threads pack the sorted triangle records
+// instead (k_seg_build packs them for U >= 2).
 __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__ hdr,
                                                   const int2 *__restrict__ node_rng,
                                                   const int32_t *__restrict__ children,
@@ -998,11 +984,20 @@ __global__ void __launch_bounds__(kThreads) k_fit(const TreeHeader *__restrict__
                                                   const uint8_t *__restrict__ is_leaf,
                                                   const int32_t *__restrict__ first,
                                                   const uint32_t *__restrict__ cnt, uint4 *__restrict__ nodes,
+                                                  const float *__restrict__ v, const uint32_t *__restrict__ tri_idx,
+                                                  uint32_t n, float *__restrict__ tris_s,
                                                   TreeHeader *__restrict__ hdr_host) {
     const uint32_t U = hdr->n_unique;
     const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
     if (p == 0) *hdr_host = *hdr;   // the host reads it after the stream synchronises (build_tree_device)
-    if (U < 2 || p >= U - 1) return;
+    if (U < 2) {
+        for (uint32_t i = p; i < n; i += gridDim.x * kThreads) {
+            float lo[3], hi[3];
+            pack_tri(v + 9ull * tri_idx[i], tris_s + 9ull * i, lo, hi);
+        }
+        return;
+    }
+    if (p >= U - 1) return;
     const int2 rg = node_rng[p];
     const uint32_t split = (uint32_t)children[2 * p];
     const int ax = axis[p];
@@ -1068,7 +1063,7 @@ void free_tree_device(DeviceTree &t) {
     void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
                     t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,
                     t.children, t.parent, t.is_leaf, t.fit_rng, t.fit_seg, t.nodes, t.tris_s,
-                    t.hist, t.partials, t.prep_part, t.slo, t.shi};
+                    t.hist, t.partials, t.prep_part};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (t.hdr_host) (void)hipHostFree(t.hdr_host);
@@ -1113,8 +1108,6 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
         BIH_TRY(dalloc(&t.fit_seg, 6 * seg_capacity(nn), t));
         BIH_TRY(dalloc(&t.nodes, nn, t));
         BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
-        BIH_TRY(dalloc(&t.slo, 3 * nn, t));
-        BIH_TRY(dalloc(&t.shi, 3 * nn, t));
         BIH_TRY(dalloc(&t.hist, hist_n, t));
         BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
         // + k_seg_build's arrival count (zero between launches)
@@ -1174,16 +1167,15 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
                                t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr);
         }
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr, t.first_idx,
-                           t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng, n, t.vals,
-                           t.v, t.tris_s, t.slo, t.shi);
+                           t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
         const uint64_t cap = seg_capacity(nn);
         // leaf boxes (and the sorted triangle records of every leaf run when U >= 2) + segment tree levels 0..10 (and, up to 2^20 leaves, the
         // levels above by the last block); larger trees: k_seg_up per 10 levels
         const uint64_t seg_blocks = (nn + kSegBlock - 1) / kSegBlock;
         // (one block builds a whole tree of <= kSegBlock leaves by itself)
         const int top = seg_blocks > 1 && seg_blocks <= kSegBlock ? 1 : 0;
-        hipLaunchKernelGGL(k_seg_build, dim3((uint32_t)seg_blocks), dim3(kSegThreads), 0, st, t.hdr, t.slo, t.shi,
-                           t.first_idx, t.dup_cnt, t.fit_seg, cap, nn, top, t.prep_part + 8ull * kPrepBlocks + 1);
+        hipLaunchKernelGGL(k_seg_build, dim3((uint32_t)seg_blocks), dim3(kSegThreads), 0, st, t.hdr, t.vals, t.v,
+                           t.tris_s, t.first_idx, t.dup_cnt, t.fit_seg, cap, nn, top, t.prep_part + 8ull * kPrepBlocks + 1);
         if (!top && seg_blocks > 1) {
             uint64_t lsize = seg_blocks;   // capacity of level 10 (>= its valid entries)
             for (int L0 = kSegSteps; lsize > 1; L0 += kSegSteps) {
@@ -1193,8 +1185,8 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
             }
         }
         hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
-                           t.axis, t.fit_seg, cap, nn, t.clip, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes,
-                           t.hdr_host);
+                           t.axis, t.fit_seg, cap, nn, t.clip, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes, t.v,
+                           t.vals, n, t.tris_s, t.hdr_host);
         BIH_TRY(hipGetLastError());
     }
     BIH_TRY(hipEventRecord(t.ev1, st));

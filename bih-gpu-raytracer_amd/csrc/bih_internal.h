@@ -191,7 +191,6 @@ struct DeviceTree {
     float *fit_seg = nullptr;                       // [6][seg_capacity] leaf-box segment tree (k_fit)
     uint4 *nodes = nullptr;
     float *tris_s = nullptr;
-    float *slo = nullptr, *shi = nullptr;           // f32[3N] triangle boxes in sorted order (k_karras)
     uint32_t *hist = nullptr;                       // radix histograms
     uint32_t *partials = nullptr;
     unsigned long long *prep_part = nullptr;        // k_prep per-block AABB keys
