@@ -146,15 +146,22 @@ __global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, u
     uint32_t v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
-    for (uint32_t k = 0; k < steps; ++k) {
-        if (split && k && k % every == 0 && k / every < nsplit) {
-            uint32_t *o = split + (uint64_t)(k / every - 1) * 5 * P;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) o[(uint64_t)i * P + lp] = v[i];
+    // segments of `every` steps (no per-step division: the split test once
+    // per segment); split s is the state after s*every < steps steps
+    uint32_t k = 0;
+    for (uint32_t s = 1;; ++s) {
+        const bool store = split && s < nsplit && (uint64_t)s * every < steps;
+        const uint32_t end = store ? s * every : steps;
+#pragma unroll 8
+        for (; k < end; ++k) {
+            const uint32_t t = v[0] ^ (v[0] >> 2);
+            v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+            v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
         }
-        const uint32_t t = v[0] ^ (v[0] >> 2);
-        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+        if (!store) break;
+        uint32_t *o = split + (uint64_t)(s - 1) * 5 * P;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[(uint64_t)i * P + lp] = v[i];
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
@@ -1788,6 +1795,32 @@ __device__ __forceinline__ bool path_verify(const uint2 *__restrict__ path, uint
 }
 #endif
 
+// Ray::Ray (Ray.cu:3-10) + the scene-AABB slab test (CUDAKernels.cu:237-262):
+// the ray's inverse direction and [tMin, tMax]; true when the ray meets the box
+__device__ __forceinline__ bool scene_slab(const SceneU &sc, float dx, float dy, float dz, float &ix,
+                                           float &iy, float &iz, float &tMin, float &tMax) {
+    ix = 1.0f / dx;
+    iy = 1.0f / dy;
+    iz = 1.0f / dz;
+    const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+    tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
+    tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
+    const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
+    const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
+    bool in_box = !((tMin > tymax) || (tymin > tMax));
+    if (tymin > tMin) tMin = tymin;
+    if (tymax < tMax) tMax = tymax;
+    const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
+    const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
+    in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
+    if (tzmin > tMin) tMin = tzmin;
+    if (tzmax < tMax) tMax = tzmax;
+    return in_box;
+}
+#ifndef BIH_SLAB_AGAIN
+#define BIH_SLAB_AGAIN 0   // 1: 72 VGPRs, 7 waves, but 0.0420 vs 0.0413 ms per frame (A/B r04n)
+#endif
+
 // The candidate's verification plan (triangle_plan, bih_bins.hip): the
 // entry's leaf carries bit 31 when every decision on its root path is
 // proven; otherwise meta & 3 = 1-2 critical comparisons, each t_k against
@@ -2064,20 +2097,8 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 camera_dir(a, uf, vf, dx, dy, dz);
             }
             // Ray::Ray (Ray.cu:3-10) + scene-AABB slab test (CUDAKernels.cu:237-262)
-            const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-            const uint32_t sg = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
-            float tMin = (((sg & 1) ? sc.shi0 : sc.slo0) - sc.ox) * ix;
-            float tMax = (((sg & 1) ? sc.slo0 : sc.shi0) - sc.ox) * ix;
-            const float tymin = (((sg & 2) ? sc.shi1 : sc.slo1) - sc.oy) * iy;
-            const float tymax = (((sg & 2) ? sc.slo1 : sc.shi1) - sc.oy) * iy;
-            bool in_box = valid && !((tMin > tymax) || (tymin > tMax));
-            if (tymin > tMin) tMin = tymin;
-            if (tymax < tMax) tMax = tymax;
-            const float tzmin = (((sg & 4) ? sc.shi2 : sc.slo2) - sc.oz) * iz;
-            const float tzmax = (((sg & 4) ? sc.slo2 : sc.shi2) - sc.oz) * iz;
-            in_box = in_box && !((tMin > tzmax) || (tzmin > tMax));
-            if (tzmin > tMin) tMin = tzmin;
-            if (tzmax < tMax) tMax = tzmax;
+            float ix, iy, iz, tMin, tMax;
+            const bool in_box = valid && scene_slab(sc, dx, dy, dz, ix, iy, iz, tMin, tMax);
             const unsigned long long live = sc.U > 0 ? __ballot(in_box) : 0ull;
             unsigned long long hits = 0ull, undecided = 0ull;
             BIH_PH(2);
@@ -2089,6 +2110,15 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                                                                         cand, cmeta, cent, fc_ent, fc_mt, pf);
                 if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
                 BIH_PH(3);
+#if BIH_SLAB_AGAIN
+                // the slab test's values again for the verification, not kept
+                // live across the walk (the walk's register peak)
+                {
+                    float ex = dx, ey = dy, ez = dz;
+                    asm volatile("" : "+v"(ex), "+v"(ey), "+v"(ez));
+                    scene_slab(sc, ex, ey, ez, ix, iy, iz, tMin, tMax);
+                }
+#endif
                 const bool ok = ((found >> lane) & 1ull) &&
                                 ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
                 hits = __ballot(ok);

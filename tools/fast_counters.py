@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--tris", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--group", type=int, default=1, help="frames per call (bih_render_device_frames)")
     a = ap.parse_args()
     import torch
     import bihrt
@@ -24,9 +25,13 @@ def main():
     d = torch.from_numpy(tris).cuda()
     g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=s.cuda_stream)
     r = bihrt.Renderer(g, a.width, a.height)
-    out = torch.zeros(a.width * a.height, dtype=torch.int32, device="cuda")
+    P = a.width * a.height
+    out = torch.zeros(P * a.group, dtype=torch.int32, device="cuda")
     for f in range(a.frames):
-        r.render_device(out.data_ptr(), f, stream=s.cuda_stream)
+        if a.group > 1:
+            r.render_device_frames(out.data_ptr(), f * a.group, a.group, P, stream=s.cuda_stream)
+        else:
+            r.render_device(out.data_ptr(), f, stream=s.cuda_stream)
         r.sync(s.cuda_stream)
 
 
