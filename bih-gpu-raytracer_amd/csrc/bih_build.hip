@@ -1078,7 +1078,7 @@ void free_tree_device(DeviceTree &t) {
 // Allocates (first call) and runs the whole build on `stream`; synchronises
 // at the end to read U back (Renderer.cpp:459 also reads the reduce_by_key
 // end pointer on the host).
-int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
+int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync) {
     hipStream_t st = (hipStream_t)stream;
     const uint32_t n = t.n;
     const uint64_t nn = n ? n : 1;
@@ -1194,6 +1194,7 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out) {
     // thread writes (no copy-engine transfer after the last kernel); a tree
     // without triangles takes the copy
     if (n == 0) BIH_TRY(hipMemcpyAsync(t.hdr_host, t.hdr, sizeof(TreeHeader), hipMemcpyDeviceToHost, st));
+    if (!sync) return 0;
     BIH_TRY(hipStreamSynchronize(st));
     const TreeHeader h = *t.hdr_host;
     float ms = 0.f;

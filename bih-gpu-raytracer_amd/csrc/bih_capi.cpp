@@ -100,6 +100,7 @@ struct TreeParams {
     uint64_t bins_cap = 0;            // BIH_PARAM_BINS_CAP (0: no cap)
     uint32_t force_fallback = 0;      // BIH_PARAM_FORCE_FALLBACK
     uint32_t wh_counters = 0;         // BIH_PARAM_WHITTED_COUNTERS
+    uint32_t static_soup = 0;         // BIH_PARAM_STATIC_SOUP
 };
 static const TreeParams &env_params() {
     static const TreeParams p = [] {
@@ -155,7 +156,11 @@ struct bih_tree {
     // it (and after the renders that read their set), not after each other
     hipEvent_t ev_tree = nullptr;
     bool tree_pending = false;
-    double build_ms = 0.0;
+    mutable double build_ms = 0.0;
+    // an asynchronous rebuild's device time: read from its events on demand
+    // (bih_tree_get_info), not by the rebuild
+    mutable bool build_ms_pending = false;
+    bool owns_soup = false;          // bih_build: the soup is the tree's own copy (never changes)
     const float *host_v = nullptr;   // scene the tree was built from (identity check)
     // render state cache (Renderer::d_rand_state / CreateCUDABuffers)
     mutable std::mutex mu;
@@ -332,6 +337,7 @@ int wait_old_tree_readers(bih_tree *tr, hipStream_t st) {
 
 int finish_build(bih_tree *tr) {
     float ms = 0.f;
+    bool async = false;
     const bool had = tr->built;
     const uint64_t old_content = tr->t.content;
     const uint32_t old_n = tr->t.n, old_u = tr->t.u;
@@ -352,13 +358,24 @@ int finish_build(bih_tree *tr) {
         if (!b.owns_v) b.v = tr->t.v;   // the same soup (the owning copy is t's or b's)
         b.n = tr->t.n;
         b.device = tr->t.device;
-        e = bih::build_tree_device(b, tr->stream, &ms);
+        // a soup that cannot have changed since the last build (the tree's own
+        // copy, or BIH_PARAM_STATIC_SOUP) gives the same tree, header and
+        // content hash bit for bit: nothing to read back, so the host does not
+        // wait for the build -- it runs on the tree's stream behind the
+        // renders in flight, and the next render orders after it (ev_tree)
+        async = tr->owns_soup || tr->prm.static_soup;
+        if (async) {
+            b.u = tr->t.u;
+            b.content = tr->t.content;
+        }
+        e = bih::build_tree_device(b, tr->stream, &ms, !async);
         if (e == 0 || e == -1000) {
             std::swap(tr->t, tr->back);
             ++tr->gen;
         }
     }
     tr->build_ms = ms;
+    tr->build_ms_pending = async && e == 0;
     tr->built = e == 0;
     // the per-pixel RNG state does not depend on the geometry: a rebuild (the
     // reference rebuilds every frame) keeps the frame sequence going.  The
@@ -496,6 +513,7 @@ int bih_build(const bih_scene *scene, int device, bih_tree **out) {
     hipError_t e = tree_malloc(tr, &tr->t.v, bytes ? bytes : 16);
     if (e == hipSuccess) {
         tr->t.owns_v = true;
+        tr->owns_soup = true;
         tr->t.bytes += bytes;
         if (bytes) e = hipMemcpy(tr->t.v, scene->v, bytes, hipMemcpyHostToDevice);
     }
@@ -607,6 +625,13 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
                           (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
+    if (tr->build_ms_pending) {   // an asynchronous rebuild: its events, once it has run
+        float ms = 0.f;
+        if (hipEventSynchronize(tr->t.ev1) == hipSuccess && hipEventElapsedTime(&ms, tr->t.ev0, tr->t.ev1) == hipSuccess) {
+            tr->build_ms = ms;
+            tr->build_ms_pending = false;
+        }
+    }
     info->build_ms = tr->build_ms;
     info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
     return BIH_OK;
@@ -1415,6 +1440,10 @@ int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
     case BIH_PARAM_WHITTED_COUNTERS:
         if (value > 1) return BIH_ERR_INVALID;
         tr->prm.wh_counters = (uint32_t)value;
+        return BIH_OK;
+    case BIH_PARAM_STATIC_SOUP:
+        if (value > 1) return BIH_ERR_INVALID;
+        tr->prm.static_soup = (uint32_t)value;
         return BIH_OK;
     default:
         return BIH_ERR_INVALID;

@@ -199,7 +199,9 @@ struct DeviceTree {
 };
 
 // builder (bih_build.hip); returns hipError_t as int
-int build_tree_device(DeviceTree &t, void *stream, float *ms_out);
+// sync = false: returns once the kernels are enqueued (no header read back;
+// t.u / t.content keep their values, ms_out is not written)
+int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync = true);
 void free_tree_device(DeviceTree &t);
 
 // render (bih_render.hip)

@@ -40,7 +40,10 @@ using dev::xorwow_uniform;
 
 constexpr uint32_t kWT = 64;            // threads per block: one wave
 constexpr int kWStack = kStackDepth;    // Karras path length <= 30 (bih_internal.h)
-constexpr int kWLds = 8;                // stack slots per lane in LDS; deeper ones in HBM
+#ifndef BIH_WH_LDS
+#define BIH_WH_LDS 10   // (A/B r04r/s, ms per C4 frame: 6 958, 8 725, 10 683, 12 752, 16 877)
+#endif
+constexpr int kWLds = BIH_WH_LDS;       // stack slots per lane in LDS; deeper ones in HBM
 constexpr uint32_t kWBlocksPerCU = 32;  // persistent grid of k_wh_trace
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
@@ -351,9 +354,21 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
 #ifndef BIH_WH_STEPS
 #define BIH_WH_STEPS 4     // walk steps per lane between refill checks (A/B: 1 1.792 s, 2 1.777, 4 1.755 per 4K frame)
 #endif
+// BIH_WH_PREFETCH: a step requests the next node's record before it tests
+// the leaves it decided to visit, so the node load and the leaves' triangle
+// loads are in flight together (one memory round trip per step instead of
+// two); the record waits in the ray state for the next step.  The leaves are
+// still tested before the next node's decisions read the best hit: the same
+// decisions, the same hit.
+#ifndef BIH_WH_PREFETCH
+#define BIH_WH_PREFETCH 1
+#endif
 struct WRay {
     float o[3], d[3], ix, iy, iz, tMin, tMax, bt;
     uint32_t sg, cur, sp, bi, sid;
+#if BIH_WH_PREFETCH
+    uint4 nd;                  // the record of node cur (requested by the previous step)
+#endif
 };
 __device__ __forceinline__ bool wray_start(const WScene &s, WRay &r, float t_lo) {
     r.bt = FLT_MAX;
@@ -380,6 +395,9 @@ __device__ __forceinline__ bool wray_start(const WScene &s, WRay &r, float t_lo)
     if (t_lo > 0.0f && tMin < t_lo) tMin = t_lo;   // a bounce's walk starts at its origin (oracle)
     r.tMin = tMin;
     r.tMax = tMax;
+#if BIH_WH_PREFETCH
+    r.nd = s.nodes[0];
+#endif
     return true;
 }
 // one iteration of closest_walk's loop; true when the walk has ended.
@@ -403,11 +421,18 @@ __device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, 
         if (r.sp == 0) return true;
         --r.sp;
         stk.pop(r.sp, r.cur, r.tMin, r.tMax);
+#if BIH_WH_PREFETCH
+        r.nd = s.nodes[r.cur];
+#endif
         return false;
     }
     if (best < r.tMax) r.tMax = best;
     if (COUNT) ++cn;
+#if BIH_WH_PREFETCH
+    const uint4 nd = r.nd;
+#else
     const uint4 nd = s.nodes[r.cur];
+#endif
     const uint32_t ax = (nd.z >> 27) & 3u;
     const float org = pick3(ax, r.o[0], r.o[1], r.o[2]), inv = pick3(ax, r.ix, r.iy, r.iz);
     const uint32_t nr = (r.sg >> ax) & 1u;
@@ -424,25 +449,27 @@ __device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, 
     const uint32_t nb = nr ? mid : mid - cL, ne = nr ? mid + cR : mid;
     const uint32_t fb = nr ? mid - cL : mid, fe = nr ? mid : mid + cR;
     const uint32_t nearc = split + nr, farc = split + 1u - nr;
+    // the leaves this step visits, in the walk's order: [l0b, l0e) then [l1b, l1e)
+    uint32_t l0b = 0, l0e = 0, l1b = 0, l1e = 0;
     bool pop = false;
     if (!A && B) {
         pop = true;
     } else if (A && B) {
-        if (leafN) { leaf(nb, ne); pop = true; }
+        if (leafN) { l0b = nb; l0e = ne; pop = true; }
         else { r.cur = nearc; r.tMax = tn; }
     } else if (!A && !B) {
-        if (leafF) { leaf(fb, fe); pop = true; }
+        if (leafF) { l0b = fb; l0e = fe; pop = true; }
         else { r.cur = farc; r.tMin = tf; }
     } else {
         if (leafN && leafF) {
-            leaf(nb, ne);
-            leaf(fb, fe);
+            l0b = nb; l0e = ne;
+            l1b = fb; l1e = fe;
             pop = true;
         } else if (!leafN && leafF) {
-            leaf(fb, fe);
+            l0b = fb; l0e = fe;
             r.cur = nearc; r.tMax = tn;
         } else if (leafN && !leafF) {
-            leaf(nb, ne);
+            l0b = nb; l0e = ne;
             r.cur = farc; r.tMin = tf;
         } else {
             stk.push(r.sp, farc, tf, r.tMax);
@@ -450,15 +477,32 @@ __device__ __forceinline__ bool wray_step(const WScene &s, WRay &r, float t_lo, 
             r.cur = nearc; r.tMax = tn;
         }
     }
+    bool fin = false;
     if (pop) {
-        if (r.sp == 0) return true;
-        --r.sp;
-        stk.pop(r.sp, r.cur, r.tMin, r.tMax);
+        if (r.sp == 0) {
+            fin = true;
+        } else {
+            --r.sp;
+            stk.pop(r.sp, r.cur, r.tMin, r.tMax);
+        }
     }
-    return false;
+#if BIH_WH_PREFETCH
+    if (!fin) r.nd = s.nodes[r.cur];
+#endif
+    leaf(l0b, l0e);
+    leaf(l1b, l1e);
+    return fin;
 }
 template <bool COUNT>
-__global__ void __launch_bounds__(kWT) k_wh_trace_dyn(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
+#ifndef BIH_WH_WAVES
+#define BIH_WH_WAVES 0   // waves per SIMD forced on k_wh_trace_dyn (0: the compiler's choice)
+#endif
+#if BIH_WH_WAVES
+#define BIH_WH_OCC __attribute__((amdgpu_waves_per_eu(BIH_WH_WAVES, BIH_WH_WAVES)))
+#else
+#define BIH_WH_OCC
+#endif
+__global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
                                                       uint32_t *counts, uint8_t *hits, uint32_t *spill,
                                                       unsigned long long *work) {
     uint32_t cn = 0, ct = 0;   // COUNT: nodes entered, triangles tested by this lane

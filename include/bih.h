@@ -146,7 +146,10 @@ void bih_scene_free(bih_scene *scene);
 int bih_build(const bih_scene *scene, int device, bih_tree **out);
 int bih_build_device(const float *d_v, uint32_t n_tris, int device, void *stream,
                      bih_tree **out);
-/* Rebuild in place (per-frame rebuild as in Renderer::Render). */
+/* Rebuild in place (per-frame rebuild as in Renderer::Render).  Renders issued
+ * afterwards on any stream see the new tree.  When the soup cannot have
+ * changed (BIH_PARAM_STATIC_SOUP) the call does not wait for the device; else
+ * it returns after the build, with BIH_ERR_NONFINITE for a non-finite soup. */
 int bih_rebuild(bih_tree *tree);
 void bih_free(bih_tree *tree);
 
@@ -210,6 +213,13 @@ int bih_reserve(bih_tree *tree, uint32_t w, uint32_t h, uint32_t spp, const bih_
 #define BIH_PARAM_WHITTED_COUNTERS 5 /* 1: Whitted renders count the nodes and
                                         triangles each bounce's walks visit
                                         (bih_whitted_work; costs time)         */
+#define BIH_PARAM_STATIC_SOUP     6  /* 1: the caller does not change the device
+                                        soup of a bih_build_device tree between
+                                        builds, so bih_rebuild need not read the
+                                        new tree's header back: it returns once
+                                        the build is enqueued (renders order
+                                        after it on the device).  Implied for
+                                        bih_build trees (the tree owns its copy) */
 int bih_tree_set_param(bih_tree *tree, int param, uint64_t value);
 
 /* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)

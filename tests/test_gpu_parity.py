@@ -298,6 +298,36 @@ def test_rebuild_keeps_frame_sequence(gpu, bihrt_mod, oracle_mod):
     _tree_equal(g.arrays(), ot)
 
 
+def test_static_soup_rebuilds_do_not_wait(gpu, bihrt_mod, oracle_mod):
+    """BIH_PARAM_STATIC_SOUP: bih_rebuild returns without waiting for the
+    build, so rebuilds and renders on three streams overlap (the bench's
+    with_rebuild leg).  Every frame still equals the oracle's, the tree
+    exports the first build's arrays, and build_ms is the last build's device
+    time (read from its events)."""
+    import torch
+    tris = bihrt_mod.scenes.soup(50_000, seed=21)
+    d = torch.from_numpy(tris.copy()).cuda()
+    g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
+    g.set_param(bihrt_mod.PARAM_STATIC_SOUP, 1)
+    a = g.arrays()
+    w, h = 160, 90
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.zeros(h * w, dtype=torch.int32, device="cuda") for _ in range(6)]
+    for f in range(6):
+        g.rebuild()
+        r.render_device(outs[f].data_ptr(), f, stream=streams[f % 3].cuda_stream)
+    torch.cuda.synchronize()
+    assert g.info().build_ms > 0.0
+    ot = oracle_mod.OracleTree(tris)
+    for f in range(6):
+        ref, _ = ot.render(w, h, frame=f)
+        assert np.array_equal(outs[f].cpu().numpy().view(np.uint32).reshape(h, w), ref), f
+    b = g.arrays()
+    for k in TREE_KEYS:
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+
+
 def test_rebuild_of_changed_soup_rebuilds_camera_state(gpu, bihrt_mod, oracle_mod):
     """A rebuild keeps the per-camera structures (records, frustum bins, tile
     queues) only when the soup's content hash is unchanged: moving the
