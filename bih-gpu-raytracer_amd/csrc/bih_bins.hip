@@ -250,24 +250,43 @@ __device__ __forceinline__ double plane_lmin(double xmin, double xmax, double va
     const double r = 4.0 * 0x1p-24 * fabs(val);
     return plane_m((le ? val - xmax : xmin - val) - r, ramin, ramax);
 }
+// TAB: the per-axis values the walk picks by the node's axis (1 / min|X[a]|,
+// 1 / max|X[a]|, the corners' extent) come from a per-thread table in LDS
+// (tab[k * kThreads], k = 4 axis + field) -- one LDS read each instead of a
+// chain of selects over the three axes in registers.
+template <bool TAB>
 __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const TreeHeader *hdr,
                                   const float *o, const uint4 *node_prim, const int32_t *leaf_parent,
-                                  const int32_t *parent, float *vals) {
+                                  const int32_t *parent, float *vals, double *tab) {
     constexpr uint32_t kFull = 3u;
-    double amin[3], amax[3], xlo[3], xhi[3];
+#ifndef BIH_PLAN_LEAN
+#define BIH_PLAN_LEAN 0   // 1: the corners' extent per axis recomputed per level, not kept (12 VGPRs; slower)
+#endif
+    double amin[3], amax[3];
+#if !BIH_PLAN_LEAN
+    double xlo[3], xhi[3];
+#endif
     int sgn[3];
     bool finite_ok = true;   // no NaN corner coordinate: the one-value test is exact
     for (int ax = 0; ax < 3; ++ax) {
         const double lo = fmin(fmin(X[0][ax], X[1][ax]), X[2][ax]);
         const double hi = fmax(fmax(X[0][ax], X[1][ax]), X[2][ax]);
         finite_ok = finite_ok && X[0][ax] == X[0][ax] && X[1][ax] == X[1][ax] && X[2][ax] == X[2][ax];
+#if !BIH_PLAN_LEAN
         xlo[ax] = lo;
         xhi[ax] = hi;
+#endif
         const double mn = lo > 0.0 ? lo : (hi < 0.0 ? -hi : 0.0);
         const double mx = fmax(fabs(lo), fabs(hi));
         amin[ax] = mn > 0.0 ? 1.0 / mn : 0.0;   // reciprocals (plane_l)
         amax[ax] = mx > 0.0 ? 1.0 / mx : 0.0;
         sgn[ax] = lo > 0.0 ? 1 : (hi < 0.0 ? -1 : 0);
+        if (TAB) {
+            tab[(4 * ax + 0) * kThreads] = amin[ax];
+            tab[(4 * ax + 1) * kThreads] = amax[ax];
+            tab[(4 * ax + 2) * kThreads] = lo;
+            tab[(4 * ax + 3) * kThreads] = hi;
+        }
     }
     // slab faces: the smallest L over the faces that can be entries / exits
     PlanL slabE, slabX;
@@ -296,24 +315,45 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
     float lastEv = 0.0f, lastXv = 0.0f;
     uint32_t lastEa = 0, lastXa = 0;
     bool lastEslab = true, lastXslab = true;
-    uint32_t meta = 0, nc = 0, node = 0;
+    uint32_t meta = 0, nc = 0;
+    // the next level's record is requested before this level's f64 work
+    // (the walk is a chain of dependent loads)
+    uint4 rn = node_prim[0];
     for (int depth = 0;; ++depth) {
         if (depth == 64) return kFull;
-        const uint4 r = node_prim[node];
+        const uint4 r = rn;
         const uint32_t split = r.z >> 8, ax = r.z & 0xffu;
         if (ax > 2u) return kFull;
         const bool le = leaf <= split;             // left child: region X[a] <= clip0 - O
         const bool child_leaf = le ? ((r.w >> 26) & 1u) != 0u : (r.w >> 31) != 0u;
+        const uint32_t child = le ? split : split + 1u;
+        if (!child_leaf) rn = node_prim[child];
         const float val = __uint_as_float(le ? r.x : r.y);
         if (sgn[ax] == 0 || val == 0.0f || !(val == val)) return kFull;
         const bool is_exit = le == (sgn[ax] > 0);
-        const double lmin = plane_lmin(xlo[ax], xhi[ax], (double)val, le, amin[ax], amax[ax]);
+        double am, aM, lmin;
+        if (TAB) {
+            am = tab[(4 * ax + 0) * kThreads];
+            aM = tab[(4 * ax + 1) * kThreads];
+            lmin = plane_lmin(tab[(4 * ax + 2) * kThreads], tab[(4 * ax + 3) * kThreads], (double)val, le, am, aM);
+        } else {
+            am = amin[ax];
+            aM = amax[ax];
+#if BIH_PLAN_LEAN
+        const double c0 = ax == 0u ? X[0][0] : (ax == 1u ? X[0][1] : X[0][2]);
+        const double c1 = ax == 0u ? X[1][0] : (ax == 1u ? X[1][1] : X[1][2]);
+        const double c2 = ax == 0u ? X[2][0] : (ax == 1u ? X[2][1] : X[2][2]);
+        lmin = plane_lmin(fmin(fmin(c0, c1), c2), fmax(fmax(c0, c1), c2), (double)val, le, am, aM);
+#else
+        lmin = plane_lmin(xlo[ax], xhi[ax], (double)val, le, am, aM);
+#endif
+        }
         bool ok = finite_ok && lmin + (is_exit ? lastEmin : lastXmin) > 0.0;
         if (!ok) {
             // the three corners: this plane and the partner (the last plane
             // of the other kind: an entry plane has le = sgn < 0, an exit
             // plane le = sgn > 0)
-            const PlanL l = plane_l(X, ax, (double)val, le, amin[ax], amax[ax]);
+            const PlanL l = plane_l(X, ax, (double)val, le, am, aM);
             const bool qslab = is_exit ? lastEslab : lastXslab;
             const uint32_t qa = is_exit ? lastEa : lastXa;
             PlanL q;
@@ -322,7 +362,8 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
             } else {
                 const float qv = is_exit ? lastEv : lastXv;
                 const bool qle = is_exit ? sgn[qa] < 0 : sgn[qa] > 0;
-                q = plane_l(X, qa, (double)qv, qle, amin[qa], amax[qa]);
+                q = TAB ? plane_l(X, qa, (double)qv, qle, tab[(4 * qa + 0) * kThreads], tab[(4 * qa + 1) * kThreads])
+                        : plane_l(X, qa, (double)qv, qle, amin[qa], amax[qa]);
             }
             ok = true;
             for (int j = 0; j < 3; ++j) ok = ok && (l.L[j] + q.L[j] > 0.0);
@@ -345,12 +386,10 @@ __device__ uint32_t triangle_plan(const double (*X)[3], uint32_t leaf, const Tre
             lastEa = ax;
             lastEslab = false;
         }
-        const uint32_t child = le ? split : split + 1u;
         if (child_leaf) {
             if (child != leaf) return kFull;       // (a malformed tree: never)
             break;
         }
-        node = child;
     }
     return meta | nc;
 }
@@ -380,6 +419,14 @@ __device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint
     }
 }
 
+// BIH_FP_SPLIT: the verification plans (triangle_plan's f64 root-path walk,
+// a chain of dependent node loads) run in k_bin_plan, a kernel of their own
+// with fewer registers and so more waves to hide the chain's latency; k_bin_fp
+// leaves (a, b, cc, 1) of each triangle in front of the camera in its
+// record's plan slots (rec[12..15]; 0 = no plan).
+#ifndef BIH_FP_SPLIT
+#define BIH_FP_SPLIT 0   // (A/B pending: split 0.026 + 0.080 ms vs 0.0995 in one kernel, r04x)
+#endif
 // Footprint of alive triangle i = live[j]: bin rectangle brect[i] (bx0 |
 // bx1 << 16, by0 | by1 << 16; empty = bx0 > bx1) and its list entry
 // binrec[i]; the global list takes the rest.  leaf = the leaf of each sorted
@@ -455,7 +502,11 @@ __global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__r
             }
         };
         corners(a, b, cc);
-        if (front == 3) {
+#ifndef BIH_FP_EXP
+#define BIH_FP_EXP 0   // timing experiments only (wrong plans): 1 no plan walk, 2 no det refinement,
+                       // 4 no edge pre-test, 8 no root paths
+#endif
+        if (front == 3 && !(BIH_FP_EXP & 2)) {
             // the inflated triangle lies in front of the camera: the exact det
             // of an accepted ray has a geometric lower bound (det_lower_bound),
             // usually far above 1e-6 -- a much tighter inflation, a smaller
@@ -510,14 +561,19 @@ __global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__r
             rect = make_uint2((x0 / c.tw) | ((x1 / c.tw) << 16), (y0 / c.th) | ((y1 / c.th) << 16));
         }
         // the edge pre-test now (rr, a, b, cc end here), the plan after
-        edge_pretest(rr, a, b, cc, c, rec);
-#ifndef BIH_FP_EXP
-#define BIH_FP_EXP 0   // timing experiments only (wrong plans): 1 no plan walk, no paths
-#endif
-#if BIH_FP_EXP & 1
+        if (!(BIH_FP_EXP & 4)) edge_pretest(rr, a, b, cc, c, rec);
+#if BIH_FP_SPLIT
+        // the plan is k_bin_plan's: it recomputes the corners from (a, b, cc)
+        if (side == 1) {
+            plan_vals[0] = a;
+            plan_vals[1] = b;
+            plan_vals[2] = cc;
+            plan_vals[3] = 1.0f;
+        }
+#elif BIH_FP_EXP & 1
         plan = 1u;
 #else
-        if (side == 1) plan = triangle_plan(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, plan_vals);
+        if (side == 1) plan = triangle_plan<false>(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, plan_vals, nullptr);
 #endif
         brect[i] = rect;
     } else {
@@ -537,11 +593,70 @@ __global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__r
 #define BIH_FAST_COUNTERS 0
 #endif
     // counter builds check every plan against the root-path check: all paths
-    if (plan == 3u || BIH_FAST_COUNTERS) write_path(node_prim, leaf, path);
+    if (!BIH_FP_SPLIT && (plan == 3u || BIH_FAST_COUNTERS) && !(BIH_FP_EXP & 8)) write_path(node_prim, leaf, path);
     for (int k = 0; k < 4; ++k) rec[12 + k] = plan_vals[k];
     float4 *o = reinterpret_cast<float4 *>(binrec + 16ull * i);
     for (int k = 0; k < 4; ++k) o[k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
     if (side == 0) glist[atomicAdd(gcount, 1u)] = i;   // every packet tests it
+}
+
+// The verification plan of alive triangle i = live[j] (k_bin_fp's, split
+// off: BIH_FP_SPLIT): the inflated triangle's corners again from the record
+// and k_bin_fp's (a, b, cc) -- the same f64 expressions, the same corners --
+// then triangle_plan, the entry's leaf word and plan, and the root path of a
+// full-check leaf.
+#ifndef BIH_PLAN_TAB
+#define BIH_PLAN_TAB 1     // triangle_plan<true>: per-axis values from an LDS table
+#endif
+#ifndef BIH_PLAN_WAVES
+#define BIH_PLAN_WAVES 0   // waves per SIMD forced on k_bin_plan (0: the compiler's choice)
+#endif
+#if BIH_PLAN_WAVES
+#define BIH_PLAN_OCC __attribute__((amdgpu_waves_per_eu(BIH_PLAN_WAVES, BIH_PLAN_WAVES)))
+#else
+#define BIH_PLAN_OCC
+#endif
+__global__ void __launch_bounds__(kThreads) BIH_PLAN_OCC k_bin_plan(const float *__restrict__ prim, BinCamera c,
+                                                       const TreeHeader *__restrict__ hdr,
+                                                       const uint4 *__restrict__ node_prim,
+                                                       const uint32_t *__restrict__ tri_leaf,
+                                                       const int32_t *__restrict__ leaf_parent,
+                                                       const int32_t *__restrict__ parent,
+                                                       uint2 *__restrict__ path, float *__restrict__ binrec,
+                                                       const uint32_t *__restrict__ live,
+                                                       const uint32_t *__restrict__ live_count) {
+#if BIH_PLAN_TAB
+    __shared__ double s_tab[12 * kThreads];
+#endif
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= *live_count) return;
+    const uint32_t i = live[j];
+    float *rec = binrec + 16ull * i;
+    const float4 abc = *reinterpret_cast<const float4 *>(rec + 12);
+    const uint32_t leaf = tri_leaf[i];
+    uint32_t plan = 3u;
+    float vals[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (abc.w != 0.0f) {
+        const float *r = prim + 16ull * i;
+        float rr[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) rr[k] = r[k];
+        const double cu[3] = {-(double)abc.x, 1.0 + (double)abc.y + (double)abc.z, -(double)abc.x};
+        const double cv[3] = {-(double)abc.y, -(double)abc.y, 1.0 + (double)abc.x + (double)abc.z};
+        double cx[3][3];
+        for (int q = 0; q < 3; ++q)
+            for (int ax = 0; ax < 3; ++ax)
+                cx[q][ax] = (cu[q] * (double)rr[ax] + cv[q] * (double)rr[3 + ax]) - (double)rr[6 + ax];
+#if BIH_PLAN_TAB
+        plan = triangle_plan<true>(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, vals, s_tab + threadIdx.x);
+#else
+        plan = triangle_plan<false>(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, vals, nullptr);
+#endif
+    }
+    rec[10] = __uint_as_float(leaf | (plan == 0u ? 0x80000000u : 0u));
+    rec[11] = __uint_as_float(plan);
+    *reinterpret_cast<float4 *>(rec + 12) = make_float4(vals[0], vals[1], vals[2], vals[3]);
+    if (plan == 3u || BIH_FAST_COUNTERS) write_path(node_prim, leaf, path);
 }
 
 // Tile (bx, by) against a triangle's edge pre-test (k0..k8 = 3 x {K0', Ku,
@@ -1151,6 +1266,9 @@ int launch_bin_footprints(const float *tris, uint32_t n, const uint4 *nodes, uin
         hipLaunchKernelGGL(k_bin_fp, g, dim3(kThreads), 0, st, prim, n, c, hdr, node_prim, tri_leaf, leaf_parent,
                            parent, b.path, b.brect, b.binrec, b.gcount,
                            b.glist, b.live, b.gcount + 3);
+        if (BIH_FP_SPLIT)
+            hipLaunchKernelGGL(k_bin_plan, g, dim3(kThreads), 0, st, prim, c, hdr, node_prim, tri_leaf, leaf_parent,
+                               parent, b.path, b.binrec, b.live, b.gcount + 3);
         hipLaunchKernelGGL(k_bin_count, g, dim3(kThreads), 0, st, b.brect, b.live, b.gcount + 3, b.bins_x,
                            reinterpret_cast<const float4 *>(b.binrec), c.w, c.h, c.tw, c.th, b.cnt, b.cntq,
                            reinterpret_cast<unsigned long long *>(b.blkcnt),

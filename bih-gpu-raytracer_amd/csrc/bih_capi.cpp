@@ -598,9 +598,24 @@ void bih_free(bih_tree *tr) {
     delete tr;
 }
 
+// An asynchronous rebuild (BIH_PARAM_STATIC_SOUP) may still be running: the
+// host-side readers of the tree (info, export) wait for it first, and take
+// its device time from its events.
+static int wait_async_build(const bih_tree *tr) {
+    if (!tr->build_ms_pending) return BIH_OK;
+    float ms = 0.f;
+    hipError_t e = hipEventSynchronize(tr->t.ev1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, tr->t.ev0, tr->t.ev1);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->build_ms = ms;
+    tr->build_ms_pending = false;
+    return BIH_OK;
+}
+
 int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     if (!tr || !info) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
+    if (int rc = wait_async_build(tr)) return rc;
     bih::TreeHeader h;
     if (tr->t.hdr) {
         hipError_t e = hipMemcpy(&h, tr->t.hdr, sizeof h, hipMemcpyDeviceToHost);
@@ -625,13 +640,6 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
                           (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
-    if (tr->build_ms_pending) {   // an asynchronous rebuild: its events, once it has run
-        float ms = 0.f;
-        if (hipEventSynchronize(tr->t.ev1) == hipSuccess && hipEventElapsedTime(&ms, tr->t.ev0, tr->t.ev1) == hipSuccess) {
-            tr->build_ms = ms;
-            tr->build_ms_pending = false;
-        }
-    }
     info->build_ms = tr->build_ms;
     info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
     return BIH_OK;
@@ -666,6 +674,7 @@ int bih_tree_export(const bih_tree *tr, int which, void *dst, size_t *bytes) {
     *bytes = need;
     if (need == 0) return BIH_OK;
     DeviceGuard g(tr->t.device);
+    if (int rc = wait_async_build(tr)) return rc;
     hipError_t e = hipMemcpy(dst, src, need, hipMemcpyDeviceToHost);
     return map_hip((int)e);
 }
@@ -1132,10 +1141,15 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     const int slot = tr->slot;
     int rc = BIH_OK;
     hipError_t e = hipSuccess;
-    if (tr->tree_pending) {
-        e = hipStreamWaitEvent(st, tr->ev_tree, 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
+    // the last (re)build: waited for right before the first work of this
+    // call that reads the tree, so that the XORWOW advance (which does not)
+    // runs beside a rebuild still in flight
+    bool tree_waited = !tr->tree_pending;
+    auto wait_tree = [&]() -> hipError_t {
+        if (tree_waited) return hipSuccess;
+        tree_waited = true;
+        return hipStreamWaitEvent(st, tr->ev_tree, 0);
+    };
     // primary-ray records follow the camera (the origin; the miss-proof boxes
     // also the direction bounds)
     const uint32_t n_int = tr->t.u > 0 ? tr->t.u - 1 : 0;
@@ -1174,6 +1188,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             if (want_bins) {
                 need_prim = true;
             } else {
+                e = wait_tree();
+                if (e != hipSuccess) return map_hip((int)e);
                 int le = bih::launch_prim(tr->t.tris_s, tr->t.n, tr->t.nodes, tr->t.first_idx,
                                           tr->t.dup_cnt, tr->t.leaf_parent, tr->t.parent, n_int,
                                           cam->origin, dmax, c.prim, st);
@@ -1194,6 +1210,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             if (rc) return rc;
             float dmax[3];
             (void)bih_camera_ray_bound(cam, dmax);
+            e = wait_tree();
+            if (e != hipSuccess) return map_hip((int)e);
             rc = build_bins(tr, c, cam, dmax, w, h, spp, need_prim, st);
             if (rc) {
                 if (need_prim) c.prim_valid = false;
@@ -1259,6 +1277,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
                                          2 * spp * a.fpi, a.nsplit));
     if (rc) return rc;
     tr->next_frame = frame + nframes;
+    e = wait_tree();
+    if (e != hipSuccess) return map_hip((int)e);
     if (use_bins) {
         a.bin_off = c.bins.off;
         a.bin_list = c.bin_list;

@@ -15,6 +15,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--in-flight", type=int, default=3)
+    ap.add_argument("--static", type=int, default=1, help="BIH_PARAM_STATIC_SOUP (asynchronous rebuilds)")
+    ap.add_argument("--render", type=int, default=1, help="0: rebuilds only")
     a = ap.parse_args()
     import torch
     import bihrt
@@ -23,6 +25,7 @@ def main():
     tris = bihrt.scenes.soup(1_000_000, seed=1)
     d = torch.from_numpy(tris).cuda()
     g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=streams[0].cuda_stream)
+    g.set_param(bihrt.PARAM_STATIC_SOUP, a.static)
     r = bihrt.Renderer(g, W, H)
     outs = [torch.zeros(W * H, dtype=torch.int32, device="cuda") for _ in streams]
 
@@ -33,7 +36,8 @@ def main():
             t0 = time.perf_counter()
             g.rebuild()
             t1 = time.perf_counter()
-            r.render_device(outs[j].data_ptr(), k, stream=streams[j].cuda_stream)
+            if a.render:
+                r.render_device(outs[j].data_ptr(), k, stream=streams[j].cuda_stream)
             t2 = time.perf_counter()
             tb += t1 - t0
             tr += t2 - t1
