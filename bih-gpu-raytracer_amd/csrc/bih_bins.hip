@@ -425,7 +425,10 @@ __device__ void write_path(const uint4 *__restrict__ node_prim, uint32_t k, uint
 // leaves (a, b, cc, 1) of each triangle in front of the camera in its
 // record's plan slots (rec[12..15]; 0 = no plan).
 #ifndef BIH_FP_SPLIT
-#define BIH_FP_SPLIT 0   // (A/B pending: split 0.026 + 0.080 ms vs 0.0995 in one kernel, r04x)
+#define BIH_FP_SPLIT 0   // 1: slower (0.027 + 0.073 ms with the LDS table vs 0.0965 in one kernel, r04y)
+#endif
+#ifndef BIH_FP_TAB
+#define BIH_FP_TAB 1      // k_bin_fp's plan walk with triangle_plan<true> (LDS per-axis table): 0.0865 vs 0.0963 ms (r04z)
 #endif
 // Footprint of alive triangle i = live[j]: bin rectangle brect[i] (bx0 |
 // bx1 << 16, by0 | by1 << 16; empty = bx0 > bx1) and its list entry
@@ -451,6 +454,9 @@ __global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__r
                                                      uint32_t *__restrict__ glist,
                                                      const uint32_t *__restrict__ live,
                                                      const uint32_t *__restrict__ live_count) {
+#if BIH_FP_TAB
+    __shared__ double s_tab[12 * kThreads];
+#endif
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= *live_count) return;
     const uint32_t i = live[j];   // k_cam_tris
@@ -573,7 +579,12 @@ __global__ void __launch_bounds__(kThreads) BIH_FP_OCC k_bin_fp(const float *__r
 #elif BIH_FP_EXP & 1
         plan = 1u;
 #else
+#if BIH_FP_TAB
+        if (side == 1) plan = triangle_plan<true>(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, plan_vals,
+                                                  s_tab + threadIdx.x);
+#else
         if (side == 1) plan = triangle_plan<false>(cx, leaf, hdr, c.o, node_prim, leaf_parent, parent, plan_vals, nullptr);
+#endif
 #endif
         brect[i] = rect;
     } else {
