@@ -352,8 +352,10 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
 #define BIH_WH_REFILL 16   // idle lanes of a wave that trigger a refill
 #endif
 #ifndef BIH_WH_STEPS
-#define BIH_WH_STEPS 32    // walk steps per lane between refill checks (A/B r03: 1 1.792 s, 2 1.777, 4 1.755 per 4K frame;
-                           // r04y-za after the one-round-trip step: 2 0.698, 4 0.680, 8 0.669-0.671, 16 0.660, 32 0.653)
+#define BIH_WH_STEPS 256   // walk steps per lane between refill checks (A/B r03: 1 1.792 s, 2 1.777, 4 1.755 per 4K frame;
+                           // r04y-zg after the one-round-trip step: 2 0.698, 4 0.680, 8 0.669, 16 0.660, 32 0.653,
+                           // 64 0.645, 128 0.639, 256 0.635, 512 0.636, 1024 0.647: a refill stalls the whole wave
+                           // on the new rays' loads, so fewer, larger refills pay until idle lanes wait too long)
 #endif
 // BIH_WH_PREFETCH: a step requests the next node's record before it tests
 // the leaves it decided to visit, so the node load and the leaves' triangle
