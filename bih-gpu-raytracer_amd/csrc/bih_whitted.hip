@@ -363,6 +363,9 @@ __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t d
 // two); the record waits in the ray state for the next step.  The leaves are
 // still tested before the next node's decisions read the best hit: the same
 // decisions, the same hit.
+#ifndef BIH_WH_MAXDIAG
+#define BIH_WH_MAXDIAG 0   // diagnostic build: bih_whitted_work's triangles = the longest walk per bounce
+#endif
 #ifndef BIH_WH_PREFETCH
 #define BIH_WH_PREFETCH 1
 #endif
@@ -509,6 +512,9 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
                                                       uint32_t *counts, uint8_t *hits, uint32_t *spill,
                                                       unsigned long long *work) {
     uint32_t cn = 0, ct = 0;   // COUNT: nodes entered, triangles tested by this lane
+#if BIH_WH_MAXDIAG
+    uint32_t cn_ray0 = 0, cmax = 0;   // (diagnostic build: the longest walk, in nodes, reported as 'tris')
+#endif
     __shared__ uint32_t s_node[kWLds * kWT];
     __shared__ float s_min[kWLds * kWT];
     __shared__ float s_max[kWLds * kWT];
@@ -546,6 +552,9 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
                     }
                     r.sid = sid_in[i];
                     has = wray_start(sc, r, t_lo);   // a ray that misses the scene box ends here: no hit
+#if BIH_WH_MAXDIAG
+                    cn_ray0 = cn;
+#endif
                 }
             }
         }
@@ -556,6 +565,9 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
         bool fin = false;
         if (has)
             for (int k = 0; k < BIH_WH_STEPS && !fin; ++k) fin = wray_step<COUNT>(sc, r, t_lo, stk, cn, ct);
+#if BIH_WH_MAXDIAG
+        if (fin && cn - cn_ray0 > cmax) cmax = cn - cn_ray0;
+#endif
         const bool hit = fin && r.bi != kNoHit;
         if (hit) hits[r.sid] = (uint8_t)(depth + 1);
         // the mirror ray (oracle whitted_path), then compaction into qout
@@ -598,10 +610,23 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
             n64 += __shfl_xor(n64, off, 64);
             t64 += __shfl_xor(t64, off, 64);
         }
+#if BIH_WH_MAXDIAG
+        unsigned long long m64 = cmax;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(m64, off, 64);
+            m64 = o > m64 ? o : m64;
+        }
+        if (lane == 0) {
+            atomicAdd(work + 2 * depth, n64);
+            atomicMax(work + 2 * depth + 1, m64);
+        }
+#else
         if (lane == 0) {
             atomicAdd(work + 2 * depth, n64);
             atomicAdd(work + 2 * depth + 1, t64);
         }
+#endif
     }
 }
 
