@@ -49,7 +49,11 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr float kBounceTLo = 1e-4f;     // t_lo of secondary rays (oracle: 1e-4f)
 constexpr uint32_t kWCounts = 32;       // counter words: [0..9] rays per queue, [16..25] rays taken (k_wh_trace_dyn)
 constexpr uint32_t kWFetch = 16;
-constexpr uint32_t kWSortBucketsGen = 4096;   // = kWSortBuckets (below): k_wh_gen zeroes the histogram
+#ifndef BIH_WH_SORT_BITS
+#define BIH_WH_SORT_BITS 5   // origin cells per axis 2^bits (3: LDS-aggregated counts; more: global atomics;
+                             // A/B r04zo per 4K frame: 3 0.636 s, 4 0.644, 5 0.620, 6 0.623)
+#endif
+constexpr uint32_t kWSortBucketsGen = 8u << (3 * BIH_WH_SORT_BITS);   // = kWSortBuckets (below): k_wh_gen zeroes the histogram
 constexpr uint32_t kWWorkWords = 18;    // work counters: {nodes, triangles} per bounce, u64 (k_wh_trace_dyn<true>)
 
 struct WScene {
@@ -639,8 +643,9 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
 // k_wh_sort_scan, k_wh_sort_scatter); the order within a bucket is arbitrary.
 // No result depends on the queue order (each ray carries its sample id and
 // its walk is its own), so the pixels and hit counts are unchanged.
-constexpr uint32_t kWSortBits = 3;                              // cells per axis: 8
-constexpr uint32_t kWSortBuckets = 8u << (3 * kWSortBits);      // x 8 octants = 4096
+constexpr uint32_t kWSortBits = BIH_WH_SORT_BITS;              // cells per axis: 2^bits
+constexpr uint32_t kWSortBuckets = 8u << (3 * kWSortBits);      // x 8 octants (3 bits: 4096)
+constexpr bool kWSortLds = kWSortBits == 3;                     // counts aggregated in LDS per block
 constexpr uint32_t kWSortChunk = 4096;                          // rays per sort block (16 per thread)
 __device__ __forceinline__ uint32_t wh_cell(float o, float lo, float hi) {
     const float q = (o - lo) / (hi - lo) * (float)(1u << kWSortBits);
@@ -663,11 +668,34 @@ __device__ __forceinline__ uint32_t wh_sort_key(const WScene &s, const WQueue &q
 template <bool SCATTER>
 __global__ void __launch_bounds__(256) k_wh_sort_pass(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
                                                       const uint32_t *counts, uint32_t *hist) {
-    __shared__ uint32_t s_cnt[kWSortBuckets];
-    __shared__ uint32_t s_base[SCATTER ? kWSortBuckets : 1];
+    __shared__ uint32_t s_cnt[kWSortLds ? kWSortBuckets : 1];
+    __shared__ uint32_t s_base[(SCATTER && kWSortLds) ? kWSortBuckets : 1];
     const uint32_t n = counts[depth];
     const uint64_t c0 = (uint64_t)blockIdx.x * kWSortChunk;
     if (c0 >= n) return;
+    if (!kWSortLds) {
+        // finer keys: one global atomic per ray (count, then the ray's slot)
+        const WScene sc = load_wscene(a);
+        const uint32_t *sid_in = reinterpret_cast<const uint32_t *>(qin.p) + 6 * qin.cap;
+        uint32_t *cur = hist + kWSortBuckets;
+        for (uint32_t r = 0; r < kWSortChunk / 256; ++r) {
+            const uint64_t i = c0 + r * 256 + threadIdx.x;
+            if (i >= n) continue;
+            const uint32_t key = wh_sort_key(sc, qin, i);
+            if (!SCATTER) {
+                atomicAdd(hist + key, 1u);
+            } else {
+                const uint64_t j = atomicAdd(cur + key, 1u);
+                float o[3], d[3];
+                for (int c = 0; c < 3; ++c) {
+                    o[c] = qin.p[c * qin.cap + i];
+                    d[c] = qin.p[(3 + c) * qin.cap + i];
+                }
+                qout.put(j, o, d, sid_in[i]);
+            }
+        }
+        return;
+    }
     for (uint32_t k = threadIdx.x; k < kWSortBuckets; k += 256) s_cnt[k] = 0u;
     __syncthreads();
     const WScene sc = load_wscene(a);
@@ -702,13 +730,14 @@ __global__ void __launch_bounds__(256) k_wh_sort_pass(const RenderArgs a, uint32
     }
 }
 // Bucket starts: cursors = exclusive scan of the histogram; the histogram is
-// zeroed for the next bounce's count (one block of 1024 threads, 4 buckets each).
+// zeroed for the next bounce's count (one block of 1024 threads, kPer buckets each).
+constexpr uint32_t kWSortPer = kWSortBuckets / 1024;
 __global__ void __launch_bounds__(1024) k_wh_sort_scan(uint32_t *hist) {
     __shared__ uint32_t s_w[16];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint32_t v[4], sum = 0;
-    for (int k = 0; k < 4; ++k) {
-        v[k] = hist[4 * t + k];
+    uint32_t v[kWSortPer], sum = 0;
+    for (uint32_t k = 0; k < kWSortPer; ++k) {
+        v[k] = hist[kWSortPer * t + k];
         sum += v[k];
     }
     uint32_t inc = sum;
@@ -720,13 +749,13 @@ __global__ void __launch_bounds__(1024) k_wh_sort_scan(uint32_t *hist) {
     __syncthreads();
     uint32_t run = inc - sum;
     for (uint32_t k = 0; k < w; ++k) run += s_w[k];
-    for (int k = 0; k < 4; ++k) {
-        hist[kWSortBuckets + 4 * t + k] = run;
-        hist[4 * t + k] = 0u;
+    for (uint32_t k = 0; k < kWSortPer; ++k) {
+        hist[kWSortBuckets + kWSortPer * t + k] = run;
+        hist[kWSortPer * t + k] = 0u;
         run += v[k];
     }
 }
-static_assert(kWSortBuckets == 4 * 1024, "k_wh_sort_scan: 1024 threads x 4 buckets");
+static_assert(kWSortBuckets % 1024 == 0, "k_wh_sort_scan: 1024 threads x kWSortPer buckets");
 static_assert(kWSortBuckets == kWSortBucketsGen, "k_wh_gen zeroes every bucket");
 
 // shade of a sample with h hits (oracle whitted_shade), f32
