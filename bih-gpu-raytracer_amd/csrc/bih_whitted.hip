@@ -53,7 +53,10 @@ constexpr uint32_t kWFetch = 16;
 #define BIH_WH_SORT_BITS 5   // origin cells per axis 2^bits (3: LDS-aggregated counts; more: global atomics;
                              // A/B r04zo per 4K frame: 3 0.636 s, 4 0.644, 5 0.620, 6 0.623)
 #endif
-constexpr uint32_t kWSortBucketsGen = 8u << (3 * BIH_WH_SORT_BITS);   // = kWSortBuckets (below): k_wh_gen zeroes the histogram
+#ifndef BIH_WH_SORT_DIR
+#define BIH_WH_SORT_DIR 0    // 1: the direction's dominant axis joins the key (x 4 buckets; r04zp: 0.617 vs 0.621 s, noise)
+#endif
+constexpr uint32_t kWSortBucketsGen = (8u << (3 * BIH_WH_SORT_BITS)) << (BIH_WH_SORT_DIR ? 2 : 0);   // = kWSortBuckets
 constexpr uint32_t kWWorkWords = 18;    // work counters: {nodes, triangles} per bounce, u64 (k_wh_trace_dyn<true>)
 
 struct WScene {
@@ -644,8 +647,8 @@ __global__ void __launch_bounds__(kWT) BIH_WH_OCC k_wh_trace_dyn(const RenderArg
 // No result depends on the queue order (each ray carries its sample id and
 // its walk is its own), so the pixels and hit counts are unchanged.
 constexpr uint32_t kWSortBits = BIH_WH_SORT_BITS;              // cells per axis: 2^bits
-constexpr uint32_t kWSortBuckets = 8u << (3 * kWSortBits);      // x 8 octants (3 bits: 4096)
-constexpr bool kWSortLds = kWSortBits == 3;                     // counts aggregated in LDS per block
+constexpr uint32_t kWSortBuckets = (8u << (3 * kWSortBits)) << (BIH_WH_SORT_DIR ? 2 : 0);   // x 8 octants (3 bits: 4096)
+constexpr bool kWSortLds = kWSortBuckets == 4096;               // counts aggregated in LDS per block
 constexpr uint32_t kWSortChunk = 4096;                          // rays per sort block (16 per thread)
 __device__ __forceinline__ uint32_t wh_cell(float o, float lo, float hi) {
     const float q = (o - lo) / (hi - lo) * (float)(1u << kWSortBits);
@@ -658,9 +661,15 @@ __device__ __forceinline__ uint32_t wh_sort_key(const WScene &s, const WQueue &q
         const uint32_t v = wh_cell(q.p[c * q.cap + i], s.slo[c], s.shi[c]);
         for (uint32_t b = 0; b < kWSortBits; ++b) cell |= ((v >> b) & 1u) << (3 * b + (2 - c));
     }
-    const uint32_t oct = (q.p[3 * q.cap + i] < 0.0f ? 1u : 0u) | (q.p[4 * q.cap + i] < 0.0f ? 2u : 0u) |
-                         (q.p[5 * q.cap + i] < 0.0f ? 4u : 0u);
+    const float dx = q.p[3 * q.cap + i], dy = q.p[4 * q.cap + i], dz = q.p[5 * q.cap + i];
+    const uint32_t oct = (dx < 0.0f ? 1u : 0u) | (dy < 0.0f ? 2u : 0u) | (dz < 0.0f ? 4u : 0u);
+#if BIH_WH_SORT_DIR
+    const float ax = fabsf(dx), ay = fabsf(dy), az = fabsf(dz);
+    const uint32_t dom = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+    return (((cell << 3) | oct) << 2) | dom;
+#else
     return (cell << 3) | oct;
+#endif
 }
 // Per-block bucket counts of queue q's rays [blockIdx.x * chunk, +chunk) into
 // LDS; SCATTER = false adds them to the global histogram, true reserves each
