@@ -59,6 +59,7 @@ def test_errors_without_device(bihrt_mod):
     assert L.bih_render_device(None, None, 1, 1, 1, 0, 0, None, 0, None, None, None) == -1
     assert L.bih_reserve(None, 1920, 1080, 4, None, 16) == -1
     assert L.bih_tree_set_param(None, bihrt_mod.PARAM_ITEM_TILES, 1) == -1
+    assert L.bih_tree_set_param(None, bihrt_mod.PARAM_STATIC_SOUP, 1) == -1
     # the tree-info struct carries the allocation counter (ABI 2)
     assert bihrt_mod._lib.TreeInfo.device_allocs.offset + 8 == C.sizeof(bihrt_mod._lib.TreeInfo)
 

@@ -308,6 +308,8 @@ def test_static_soup_rebuilds_do_not_wait(gpu, bihrt_mod, oracle_mod):
     tris = bihrt_mod.scenes.soup(50_000, seed=21)
     d = torch.from_numpy(tris.copy()).cuda()
     g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
+    with pytest.raises(bihrt_mod.BihError):
+        g.set_param(bihrt_mod.PARAM_STATIC_SOUP, 2)
     g.set_param(bihrt_mod.PARAM_STATIC_SOUP, 1)
     a = g.arrays()
     w, h = 160, 90
