@@ -204,11 +204,12 @@ class Workload:
                     (lambda base, k: C.tiling.frame_of_step(base, k, C.rank, C.world, g)), C.world)
         return C.tiling.band_rows(self.H, a.band, C.rank, C.world), (lambda base, k: base + k), 1
 
-    def step(self, mode, rows, c, frame, traverse, ev=None, rebuild=False, nf=None, m=1):
-        """One render call (call index c): frames frame .. frame+m-1."""
+    def step(self, mode, rows, c, frame, traverse, ev=None, rebuild=False, nf=None, m=1, first=0):
+        """One render call (call index c): frames frame .. frame+m-1, on
+        stream first + c % nf."""
         C = self.C
         nf = nf or C.F
-        j = c % nf
+        j = first + c % nf
         s = C.streams[j]
         o = self.outs[j].data_ptr()
         strong = mode == "strong" and C.world > 1
@@ -241,7 +242,7 @@ class Workload:
                 # call c's gather runs on stream j while call c+1 renders on j+1
                 self.gathers[(j, m)](self.outs[j], self.frame_img[j])
 
-    def timed(self, mode, traverse, base, rebuild=False, nf=None, g=None, rows=None, steps=None):
+    def timed(self, mode, traverse, base, rebuild=False, nf=None, g=None, rows=None, steps=None, first=0):
         """Times exactly `steps` frames per rank (args.steps), in calls of g
         frames (the last call takes the rest).  Untimed first: args.warmup
         frames in calls of g, then one call of every timed call size the
@@ -258,7 +259,7 @@ class Workload:
         warm += [m for m in sorted(set(calls)) if m not in warm]
         k = c = 0
         for m in warm:
-            self.step(mode, rows, c, frame_of(base, k), traverse, rebuild=rebuild, nf=nf, m=m)
+            self.step(mode, rows, c, frame_of(base, k), traverse, rebuild=rebuild, nf=nf, m=m, first=first)
             k, c = k + m, c + 1
         C.sync_all()
         allocs0 = self.arrays.info().device_allocs
@@ -269,7 +270,7 @@ class Workload:
         t0 = time.perf_counter()
         for i, m in enumerate(calls):
             self.step(mode, rows, c, frame_of(base, k), traverse, evs[i] if evs else None, rebuild=rebuild,
-                      nf=nf, m=m)
+                      nf=nf, m=m, first=first)
             k, c = k + m, c + 1
         C.sync_all()
         el = C.max_over_ranks(time.perf_counter() - t0)
@@ -515,10 +516,16 @@ def main():
     # Renderer.cpp:415-503): time rebuild + render per step as well
     rebuild_leg = None
     if not args.no_rebuild_leg:
-        el3, _, fps3 = wl.timed(mode, trav, 2000, rebuild=True, g=1)
+        # the renders on the other streams than the tree's (streams[0], where
+        # the rebuilds go), so that a rebuild never queues behind a render
+        # (BIH_REBUILD_STREAMS=all: every stream, as the other legs)
+        sep = C.F > 1 and os.environ.get("BIH_REBUILD_STREAMS", "") != "all"
+        el3, _, fps3 = wl.timed(mode, trav, 2000, rebuild=True, g=1, nf=C.F - 1 if sep else None,
+                                first=1 if sep else 0)
         rebuild_leg = {"value": fps3 * rays_per_frame * args.steps / el3, "unit": "rays/s",
                        "ms_per_step": 1e3 * el3 / args.steps,
                        "build_ms": arrays.info().build_ms,
+                       "render_streams": (C.F - 1) if sep else C.F,
                        "note": "step = bih_rebuild + render"
                                + (" + gather" if mode == "strong" and world > 1 else "")}
 

@@ -1144,6 +1144,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // the last (re)build: waited for right before the first work of this
     // call that reads the tree, so that the XORWOW advance (which does not)
     // runs beside a rebuild still in flight
+    // a build that has completed needs no wait (no barrier packet on `st`)
+    if (tr->tree_pending && hipEventQuery(tr->ev_tree) == hipSuccess) tr->tree_pending = false;
     bool tree_waited = !tr->tree_pending;
     auto wait_tree = [&]() -> hipError_t {
         if (tree_waited) return hipSuccess;
@@ -1500,6 +1502,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
         hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
+    if (tr->tree_pending && hipEventQuery(tr->ev_tree) == hipSuccess) tr->tree_pending = false;
     if (tr->tree_pending) {   // the last (re)build (a rebuild does not order ev_rng)
         hipError_t e = hipStreamWaitEvent(st, tr->ev_tree, 0);
         if (e != hipSuccess) return map_hip((int)e);
