@@ -1359,6 +1359,11 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     a.ray_stats = d_ray_stats;
     a.work = tr->work + (size_t)slot * bih::kWorkWords;
     a.spill = tr->spill + (size_t)slot * tr->spill_per_slot;
+    // another render still running: a multi-frame launch takes fewer
+    // resident blocks so that the two overlap (bih_render.hip,
+    // bins_grid_blocks); alone, it takes every slot
+    for (int k = 0; k < kSlots && nframes > 1 && !a.shared_grid; ++k)
+        if (k != slot && tr->used[k] && hipEventQuery(tr->evd[k]) == hipErrorNotReady) a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);

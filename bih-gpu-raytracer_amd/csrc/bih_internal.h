@@ -119,6 +119,7 @@ struct RenderArgs {
     // in one launch (bih_render_device_frames); frame j's pixels at
     // out + j * out_stride, its XORWOW draws 2*spp*j past rng_in's
     uint32_t nframes = 1;
+    uint32_t shared_grid = 0;   // 1: another render is in flight: a multi-frame k_render_bins leaves it room
     uint64_t out_stride = 0;
     // k_render_bins: frames per queue item (an item covers its tile in
     // frames [s*fpi, min((s+1)*fpi, nframes)) of the launch, s = 0 ..

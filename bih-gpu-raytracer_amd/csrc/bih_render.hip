@@ -3049,10 +3049,11 @@ int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks
 // calls in flight then overlap -- the next call's advance and first waves
 // run in the free slots while this one drains (1080p headline, blocks per CU
 // of 16-frame launches: 6 (all) 0.0420 ms per frame, 5 0.0419, 4 0.0399, 3
-// 0.0397, 2 0.0400; r04zk/zl).  An isolated 16-frame launch is slower with
-// fewer waves (4: 0.0494 ms per frame against 0.0454 with all 6): the
-// pipelined frame loop, not the lone launch, is what this trades for.
-// One-frame launches keep every slot (4 per CU: 0.087 -> 0.093 ms alone).
+// 0.0397, 2 0.0400; r04zk/zl).  Only while another render is in flight
+// (RenderArgs::shared_grid, from the other slots' events): a lone 16-frame
+// launch is slower with fewer waves (4: 0.0494 ms per frame against 0.0454
+// with all 6), so it takes every slot.  One-frame launches keep every slot
+// (4 per CU: 0.087 -> 0.093 ms alone).
 #ifndef BIH_BINS_MULTI_PER_CU
 #define BIH_BINS_MULTI_PER_CU 4
 #endif
@@ -3106,7 +3107,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev
         // frustum bins: the list-walk kernel, then the exact walk for what it
         // left undecided (the fallback grid stays within the spill area)
         const uint32_t fb = grid < 64u ? grid : 64u;
-        const uint32_t gb = bins_grid_blocks(dev, a.nframes);
+        const uint32_t gb = bins_grid_blocks(dev, a.shared_grid ? a.nframes : 1u);
         if (BIH_FAST_COUNTERS || BIH_PHASES) {
             const hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
             if (e != hipSuccess) return (int)e;
