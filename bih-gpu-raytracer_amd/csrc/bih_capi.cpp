@@ -32,6 +32,11 @@
 #endif
 constexpr int kSlots = BIH_RENDER_SLOTS;
 constexpr int kRngBufs = kSlots + 1;
+#ifndef BIH_SHARE_ONE_FRAME
+#define BIH_SHARE_ONE_FRAME 1
+#endif
+// one-frame renders also take the shared grid while another render is in flight
+constexpr bool kShareOneFrame = BIH_SHARE_ONE_FRAME != 0;
 constexpr size_t kEntryBytes = 16 * bih::kBinEntryF4;   // frustum-bin list entry
 
 // Per-camera structures (bih_render.hip / bih_bins.hip): primary-ray records,
@@ -132,6 +137,7 @@ struct bih_tree {
     bih::DeviceTree back;
     uint32_t gen = 0;
     uint32_t slot_gen[kSlots] = {};
+    hipStream_t slot_stream[kSlots] = {};   // the stream render slot k was issued on
     TreeParams prm = env_params();
     uint64_t allocs = 0;             // hipMalloc calls of the render side (+ t.allocs: the builder's)
     hipStream_t stream = nullptr;
@@ -1362,8 +1368,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // another render still running: a multi-frame launch takes fewer
     // resident blocks so that the two overlap (bih_render.hip,
     // bins_grid_blocks); alone, it takes every slot
-    for (int k = 0; k < kSlots && nframes > 1 && !a.shared_grid; ++k)
-        if (k != slot && tr->used[k] && hipEventQuery(tr->evd[k]) == hipErrorNotReady) a.shared_grid = 1;
+    // (a render queued on this same stream cannot overlap this one)
+    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid; ++k)
+        if (k != slot && tr->used[k] && tr->slot_stream[k] != st && hipEventQuery(tr->evd[k]) == hipErrorNotReady)
+            a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
@@ -1377,6 +1385,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
     tr->slot_gen[slot] = tr->gen;
+    tr->slot_stream[slot] = st;
     tr->slot_cs[slot] = ci;
     tr->cs_cur = ci;
     tr->last_slot = slot;
@@ -1569,6 +1578,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
     tr->slot_gen[slot] = tr->gen;
+    tr->slot_stream[slot] = st;
     tr->slot_cs[slot] = -1;            // reads no camera set
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;

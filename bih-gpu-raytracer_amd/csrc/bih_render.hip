@@ -3107,7 +3107,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev
         // frustum bins: the list-walk kernel, then the exact walk for what it
         // left undecided (the fallback grid stays within the spill area)
         const uint32_t fb = grid < 64u ? grid : 64u;
-        const uint32_t gb = bins_grid_blocks(dev, a.shared_grid ? a.nframes : 1u);
+        const uint32_t gb = bins_grid_blocks(dev, a.shared_grid ? 2u : 1u);
         if (BIH_FAST_COUNTERS || BIH_PHASES) {
             const hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
             if (e != hipSuccess) return (int)e;
