@@ -109,19 +109,64 @@ def parse():
     return ap.parse_args()
 
 
+def visible_gpu_count():
+    """GPUs this process may use, counted WITHOUT any HIP call (the launcher
+    must not initialise the runtime before it starts the ranks): the KFD
+    topology nodes that have SIMDs (/sys/class/kfd/kfd/topology/nodes/*/
+    properties, simd_count > 0; CPU nodes have none), else amdsmi's processor
+    handles, limited by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES.  None when neither source is readable.
+    BIH_KFD_TOPOLOGY overrides the topology directory (tests)."""
+    root = os.environ.get("BIH_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology/nodes")
+    n = None
+    try:
+        names = os.listdir(root)
+    except OSError:
+        names = None
+    if names is not None:
+        n = 0
+        for d in names:
+            try:
+                with open(os.path.join(root, d, "properties")) as f:
+                    kv = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(kv.get("simd_count", "0")) > 0:
+                n += 1
+    if n is None:
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            try:
+                n = len(amdsmi.amdsmi_get_processor_handles())
+            finally:
+                amdsmi.amdsmi_shut_down()
+        except Exception:
+            return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a launcher: start the N ranks as child
     processes (torch.distributed.run on 127.0.0.1, one process per GPU) before
     this process makes any GPU call; rank 0's JSON line goes to our stdout.
-    Non-zero exit if fewer than N devices are visible or a rank fails."""
+    Exit 2 if the devices cannot be counted without HIP or fewer than N are
+    visible (N ranks sharing one GPU over gloo, BIH_BENCH_SHARE_GPU=1, need
+    one); otherwise the child's exit status."""
     import socket
     import subprocess
-    if not args.stub and os.environ.get("BIH_BENCH_SHARE_GPU") != "1":
-        import torch
-        n = torch.cuda.device_count()      # counts devices without initialising them
-        if n < args.gpus:
-            print(f"bench.py: --gpus {args.gpus} but {n} devices are visible", file=sys.stderr)
-            return 2
+    n = visible_gpu_count()
+    need = 1 if os.environ.get("BIH_BENCH_SHARE_GPU") == "1" else args.gpus
+    if n is None:
+        print("bench.py: cannot count the GPUs without HIP (no KFD topology, no amdsmi)", file=sys.stderr)
+        return 2
+    if n < need:
+        print(f"bench.py: --gpus {args.gpus} but {n} devices are visible", file=sys.stderr)
+        return 2
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -306,6 +351,12 @@ def main():
         return
     import numpy as np
     import torch
+
+    # a rank of an N > 1 run needs its own device (counted, not initialised)
+    if world > 1 and os.environ.get("BIH_BENCH_SHARE_GPU") != "1" and torch.cuda.device_count() <= local:
+        print(f"bench.py: rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} devices are visible",
+              file=sys.stderr)
+        sys.exit(3)
 
     # PMC traffic passes run as child processes before this one initialises
     # the GPU (rocprofv3 must start the program itself)

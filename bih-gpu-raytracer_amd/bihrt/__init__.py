@@ -20,7 +20,7 @@ import numpy as np
 
 from . import scenes  # noqa: F401
 from ._lib import (PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_ITEM_TILES, PARAM_PAIR_CAP, PARAM_STATIC_SOUP,
-                   PARAM_WHITTED_COUNTERS,
+                   PARAM_TEST_ALLOC_FAIL, PARAM_WHITTED_COUNTERS,
                    TRAVERSE_ANYHIT,
                    TRAVERSE_REFERENCE, BihError, Camera, Framebuffer, Rows, Scene, TreeInfo, check, load)
 from . import _lib
@@ -277,4 +277,4 @@ def write_ppm(path: str, img: np.ndarray):
 __all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
            "camera_ray_bound", "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
            "TRAVERSE_REFERENCE", "PARAM_ITEM_TILES", "PARAM_PAIR_CAP", "PARAM_BINS_CAP", "PARAM_FORCE_FALLBACK",
-           "PARAM_WHITTED_COUNTERS", "PARAM_STATIC_SOUP"]
+           "PARAM_WHITTED_COUNTERS", "PARAM_STATIC_SOUP", "PARAM_TEST_ALLOC_FAIL"]

@@ -24,6 +24,7 @@ ERRORS = {
 TRAVERSE_ANYHIT, TRAVERSE_REFERENCE = 0, 1
 PARAM_ITEM_TILES, PARAM_PAIR_CAP, PARAM_BINS_CAP, PARAM_FORCE_FALLBACK, PARAM_WHITTED_COUNTERS = 1, 2, 3, 4, 5   # bih_tree_set_param
 PARAM_STATIC_SOUP = 6
+PARAM_TEST_ALLOC_FAIL = 7   # tests: the next allocating build fails at its k-th allocation
 (ARR_MORTON_SORTED, ARR_TRI_INDEX, ARR_UNIQUE_MC, ARR_DUP_COUNT, ARR_FIRST_IDX, ARR_LEAF_PARENT,
  ARR_CLIP, ARR_AXIS, ARR_CHILDREN, ARR_IS_LEAF, ARR_PARENT, ARR_TRI_LO, ARR_TRI_HI) = range(13)
 

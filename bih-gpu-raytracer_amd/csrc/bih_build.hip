@@ -1040,9 +1040,15 @@ template <class T>
 static hipError_t dalloc(T **p, size_t count, DeviceTree &t) {
     size_t b = count * sizeof(T);
     if (b == 0) b = 16;
+    if (t.fail_alloc && --t.fail_alloc == 0) return hipErrorOutOfMemory;   // tests
+    const hipError_t e = hipMalloc((void **)p, b);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
     t.bytes += b;
     ++t.allocs;
-    return hipMalloc((void **)p, b);
+    return e;
 }
 
 // exclusive scan for the other translation units (frustum bins)
@@ -1059,13 +1065,25 @@ uint32_t next_scan_tag() {
 
 size_t scan_partials_words(uint32_t n) { return 2 * (size_t)((n + kScanTile - 1) / kScanTile) + 2; }
 
+// The build's device buffers (not the soup, the events or the pinned
+// header), freed and cleared: a tree whose allocation failed part-way holds
+// none of them, so its next build allocates them all again.
+static void free_build_buffers(DeviceTree &t) {
+    void **ptrs[] = {(void **)&t.hdr, (void **)&t.tri_lo, (void **)&t.tri_hi, (void **)&t.keys,
+                     (void **)&t.vals, (void **)&t.keys2, (void **)&t.vals2, (void **)&t.scan_tmp,
+                     (void **)&t.flags, (void **)&t.unique_mc, (void **)&t.dup_cnt, (void **)&t.first_idx,
+                     (void **)&t.leaf_parent, (void **)&t.clip, (void **)&t.axis, (void **)&t.children,
+                     (void **)&t.parent, (void **)&t.is_leaf, (void **)&t.fit_rng, (void **)&t.fit_seg,
+                     (void **)&t.nodes, (void **)&t.tris_s, (void **)&t.hist, (void **)&t.partials,
+                     (void **)&t.prep_part};
+    for (void **p : ptrs) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+}
+
 void free_tree_device(DeviceTree &t) {
-    void *ptrs[] = {t.hdr, t.tri_lo, t.tri_hi, t.keys, t.vals, t.keys2, t.vals2, t.scan_tmp,
-                    t.flags, t.unique_mc, t.dup_cnt, t.first_idx, t.leaf_parent, t.clip, t.axis,
-                    t.children, t.parent, t.is_leaf, t.fit_rng, t.fit_seg, t.nodes, t.tris_s,
-                    t.hist, t.partials, t.prep_part};
-    for (void *p : ptrs)
-        if (p) (void)hipFree(p);
+    free_build_buffers(t);
     if (t.hdr_host) (void)hipHostFree(t.hdr_host);
     if (t.ev0) (void)hipEventDestroy(t.ev0);
     if (t.ev1) (void)hipEventDestroy(t.ev1);
@@ -1074,6 +1092,47 @@ void free_tree_device(DeviceTree &t) {
     blank.device = t.device;
     t = blank;
 }
+
+#define BIH_TRY_E(x)                                \
+    do {                                            \
+        hipError_t e__ = (x);                       \
+        if (e__ != hipSuccess) return e__;          \
+    } while (0)
+static hipError_t alloc_build_buffers(DeviceTree &t, uint64_t nn, uint64_t hist_n, uint32_t max_parts,
+                                      hipStream_t st) {
+    BIH_TRY_E(dalloc(&t.hdr, 1, t));
+    BIH_TRY_E(dalloc(&t.tri_lo, 3 * nn, t));
+    BIH_TRY_E(dalloc(&t.tri_hi, 3 * nn, t));
+    BIH_TRY_E(dalloc(&t.keys, nn, t));
+    BIH_TRY_E(dalloc(&t.vals, nn, t));
+    BIH_TRY_E(dalloc(&t.keys2, nn, t));
+    BIH_TRY_E(dalloc(&t.vals2, nn, t));
+    BIH_TRY_E(dalloc(&t.scan_tmp, nn + 1, t));
+    BIH_TRY_E(dalloc(&t.unique_mc, nn, t));
+    BIH_TRY_E(dalloc(&t.dup_cnt, nn, t));
+    BIH_TRY_E(dalloc(&t.first_idx, nn, t));
+    BIH_TRY_E(dalloc(&t.leaf_parent, nn, t));
+    BIH_TRY_E(dalloc(&t.clip, 2 * nn, t));
+    BIH_TRY_E(dalloc(&t.axis, nn, t));
+    BIH_TRY_E(dalloc(&t.children, 2 * nn, t));
+    BIH_TRY_E(dalloc(&t.parent, nn, t));
+    BIH_TRY_E(dalloc(&t.is_leaf, 2 * nn, t));
+    BIH_TRY_E(dalloc(&t.fit_rng, nn, t));
+    BIH_TRY_E(dalloc(&t.fit_seg, 6 * seg_capacity(nn), t));
+    BIH_TRY_E(dalloc(&t.nodes, nn, t));
+    BIH_TRY_E(dalloc(&t.tris_s, 9 * nn, t));
+    BIH_TRY_E(dalloc(&t.hist, hist_n, t));
+    BIH_TRY_E(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
+    // + k_seg_build's arrival count (zero between launches)
+    BIH_TRY_E(dalloc(&t.prep_part, 8ull * kPrepBlocks + 2, t));
+    BIH_TRY_E(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 2 * sizeof(unsigned long long), st));
+    // look-back words (k_scan_onepass) start at tag 0 (never a call's tag):
+    // stale data in fresh memory must not pass for a predecessor's published
+    // prefix; afterwards every word carries an older call's (unique) tag
+    BIH_TRY_E(hipMemsetAsync(t.partials, 0, (2 * (uint64_t)max_parts + 2) * sizeof(uint32_t), st));
+    return hipSuccess;
+}
+#undef BIH_TRY_E
 
 // Allocates (first call) and runs the whole build on `stream`; synchronises
 // at the end to read U back (Renderer.cpp:459 also reads the reduce_by_key
@@ -1087,37 +1146,19 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync) {
     const uint32_t max_parts =
         (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
     if (!t.hdr) {
-        BIH_TRY(dalloc(&t.hdr, 1, t));
-        BIH_TRY(dalloc(&t.tri_lo, 3 * nn, t));
-        BIH_TRY(dalloc(&t.tri_hi, 3 * nn, t));
-        BIH_TRY(dalloc(&t.keys, nn, t));
-        BIH_TRY(dalloc(&t.vals, nn, t));
-        BIH_TRY(dalloc(&t.keys2, nn, t));
-        BIH_TRY(dalloc(&t.vals2, nn, t));
-        BIH_TRY(dalloc(&t.scan_tmp, nn + 1, t));
-        BIH_TRY(dalloc(&t.unique_mc, nn, t));
-        BIH_TRY(dalloc(&t.dup_cnt, nn, t));
-        BIH_TRY(dalloc(&t.first_idx, nn, t));
-        BIH_TRY(dalloc(&t.leaf_parent, nn, t));
-        BIH_TRY(dalloc(&t.clip, 2 * nn, t));
-        BIH_TRY(dalloc(&t.axis, nn, t));
-        BIH_TRY(dalloc(&t.children, 2 * nn, t));
-        BIH_TRY(dalloc(&t.parent, nn, t));
-        BIH_TRY(dalloc(&t.is_leaf, 2 * nn, t));
-        BIH_TRY(dalloc(&t.fit_rng, nn, t));
-        BIH_TRY(dalloc(&t.fit_seg, 6 * seg_capacity(nn), t));
-        BIH_TRY(dalloc(&t.nodes, nn, t));
-        BIH_TRY(dalloc(&t.tris_s, 9 * nn, t));
-        BIH_TRY(dalloc(&t.hist, hist_n, t));
-        BIH_TRY(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-        // + k_seg_build's arrival count (zero between launches)
-        BIH_TRY(dalloc(&t.prep_part, 8ull * kPrepBlocks + 2, t));
-        BIH_TRY(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 2 * sizeof(unsigned long long), st));
-        // look-back words (k_scan_onepass) start at tag 0 (never a call's
-        // tag): stale data in fresh memory must not pass for a predecessor's
-        // published prefix; afterwards every word carries an older call's
-        // (unique) tag
-        BIH_TRY(hipMemsetAsync(t.partials, 0, (2 * (uint64_t)max_parts + 2) * sizeof(uint32_t), st));
+        // all or nothing: a failure part-way frees what was allocated, so
+        // that the tree never holds a header without its buffers (the next
+        // build of it allocates them again)
+        const size_t bytes0 = t.bytes;
+        const hipError_t e = alloc_build_buffers(t, nn, hist_n, max_parts, st);
+        t.fail_alloc = 0;
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);   // the memsets, if any were issued
+            (void)hipGetLastError();          // not sticky for the next build
+            free_build_buffers(t);
+            t.bytes = bytes0;
+            return (int)e;
+        }
     }
     // timing events and the pinned copy of the header: once per tree
     if (!t.ev0) {

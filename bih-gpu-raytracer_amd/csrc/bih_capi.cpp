@@ -106,6 +106,7 @@ struct TreeParams {
     uint32_t force_fallback = 0;      // BIH_PARAM_FORCE_FALLBACK
     uint32_t wh_counters = 0;         // BIH_PARAM_WHITTED_COUNTERS
     uint32_t static_soup = 0;         // BIH_PARAM_STATIC_SOUP
+    uint32_t test_alloc_fail = 0;     // BIH_PARAM_TEST_ALLOC_FAIL (one-shot)
 };
 static const TreeParams &env_params() {
     static const TreeParams p = [] {
@@ -348,11 +349,19 @@ int finish_build(bih_tree *tr) {
     const uint64_t old_content = tr->t.content;
     const uint32_t old_n = tr->t.n, old_u = tr->t.u;
     int e = 0;
+    // tests: the next build that allocates its buffers fails part-way
+    auto arm_fail = [&](bih::DeviceTree &d) {
+        if (tr->prm.test_alloc_fail && !d.hdr) {
+            d.fail_alloc = tr->prm.test_alloc_fail;
+            tr->prm.test_alloc_fail = 0;
+        }
+    };
     if (!had) {
         // first build (or after a failed one): in place, after every render
         // launched through this tree (it may run on another stream)
         int rc = wait_renders(tr, tr->stream);
         if (rc) return rc;
+        arm_fail(tr->t);
         e = bih::build_tree_device(tr->t, tr->stream, &ms);
     } else {
         // rebuild into `back` (allocated by its first build): only the
@@ -374,6 +383,7 @@ int finish_build(bih_tree *tr) {
             b.u = tr->t.u;
             b.content = tr->t.content;
         }
+        arm_fail(b);
         e = bih::build_tree_device(b, tr->stream, &ms, !async);
         if (e == 0 || e == -1000) {
             std::swap(tr->t, tr->back);
@@ -621,6 +631,8 @@ static int wait_async_build(const bih_tree *tr) {
 int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     if (!tr || !info) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
+    // a rebuild swaps t and back under the same lock: never read a half-swapped tree
+    std::lock_guard<std::mutex> lk(tr->mu);
     if (int rc = wait_async_build(tr)) return rc;
     bih::TreeHeader h;
     if (tr->t.hdr) {
@@ -653,6 +665,7 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
 
 int bih_tree_export(const bih_tree *tr, int which, void *dst, size_t *bytes) {
     if (!tr || !bytes) return BIH_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(tr->mu);   // (as bih_tree_get_info)
     const uint64_t N = tr->t.n, U = tr->t.u, M = U > 0 ? U - 1 : 0;
     const void *src = nullptr;
     size_t need = 0;
@@ -1444,9 +1457,16 @@ int bih_reserve(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_ro
     const uint32_t ntiles = ((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
     for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles);
     if (!rc) rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, (size_t)ntiles * max_frames, 8);
-    uint32_t fpi = 1, nsplit = 1;
-    item_split(tr, w, rows.nrows, spp, max_frames, &fpi, &nsplit);
-    if (!rc && nsplit > 1) rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(nsplit - 1) * 5 * P, 1);
+    // split start states: item_split's split count does not grow steadily
+    // with the frame count (3 frames may split 3 ways, 4 frames 2 ways), so
+    // the largest over every call of 1 .. max_frames frames
+    uint32_t most = 1;
+    for (uint32_t nf = 1; nf <= max_frames; ++nf) {
+        uint32_t fpi = 1, nsplit = 1;
+        item_split(tr, w, rows.nrows, spp, nf, &fpi, &nsplit);
+        most = std::max(most, nsplit);
+    }
+    if (!rc && most > 1) rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(most - 1) * 5 * P, 1);
     if (rc) return rc;
     return map_hip((int)hipStreamSynchronize(tr->stream));
 }
@@ -1480,6 +1500,10 @@ int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
     case BIH_PARAM_STATIC_SOUP:
         if (value > 1) return BIH_ERR_INVALID;
         tr->prm.static_soup = (uint32_t)value;
+        return BIH_OK;
+    case BIH_PARAM_TEST_ALLOC_FAIL:
+        if (value > 64) return BIH_ERR_INVALID;
+        tr->prm.test_alloc_fail = (uint32_t)value;
         return BIH_OK;
     default:
         return BIH_ERR_INVALID;
@@ -1521,6 +1545,10 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
         hipError_t e = hipStreamWaitEvent(st, tr->ev_tree, 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
+    // bih_whitted_work describes the last Whitted launch issued: none until
+    // this one is (a failure below, or a reallocated wh_mem, leaves nothing
+    // to read)
+    tr->wh_last_slot = -1;
     rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
     if (rc) return rc;
     RngGuard rng_guard{tr};
@@ -1639,6 +1667,11 @@ int bih_sync(const bih_tree *tr, void *stream) {
     if (!tr) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
+#if BIH_BINS_TIMELINE
+    if (const char *path = getenv("BIH_TIMELINE_OUT")) {
+        if (hipStreamSynchronize(st) == hipSuccess) (void)bih::bins_timeline_dump(path);
+    }
+#endif
 #if BIH_WAVE_TIMELINE
     if (tr->spill && tr->last_slot >= 0 && hipStreamSynchronize(st) == hipSuccess) {
         // per-wave records of k_render_packet_asm at each wave's spill base

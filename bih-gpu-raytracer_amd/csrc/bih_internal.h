@@ -197,6 +197,8 @@ struct DeviceTree {
     unsigned long long *prep_part = nullptr;        // k_prep per-block AABB keys
     TreeHeader *hdr_host = nullptr;                 // pinned host copy of hdr (k_fit writes it)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;        // build timing (build_ms)
+    uint32_t fail_alloc = 0;                        // tests (BIH_PARAM_TEST_ALLOC_FAIL): the k-th
+                                                    // buffer allocation of the next build fails
 };
 
 // builder (bih_build.hip); returns hipError_t as int
@@ -207,6 +209,7 @@ void free_tree_device(DeviceTree &t);
 
 // render (bih_render.hip)
 int upload_rng_tables(int device);
+long bins_timeline_dump(const char *path);         // diagnostic builds (BIH_BINS_TIMELINE)
 const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host() on the device
 // config C4 (bih_whitted.hip): device bytes of the ray queues for `rays`
 // samples, and the frame's launches (k_wh_gen, 9 x k_wh_trace, k_wh_shade);

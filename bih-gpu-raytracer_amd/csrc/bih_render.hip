@@ -34,6 +34,8 @@
 #include <string.h>
 
 #include <mutex>
+#include <stdio.h>
+#include <vector>
 
 #include "bih_internal.h"
 #include "bih_bound.h"
@@ -1870,6 +1872,26 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 // the slot from a band head.  One device-wide atomic per batch instead of
 // one per item: a single head word saturates near 90 dequeues per us.
 // ---------------------------------------------------------------------------
+#ifndef BIH_BINS_TIMELINE
+#define BIH_BINS_TIMELINE 0   // diagnostic builds: per-item records of k_render_bins (bins_timeline_dump)
+#endif
+#if BIH_BINS_TIMELINE
+// {wave | xcc << 24 | kind << 28, start, duration, list length} per queue
+// item (s_memrealtime, 100 MHz); kind 0 live item, 1 background item, 2
+// wave start, 3 wave exit
+constexpr uint32_t kTlCap = 1u << 20;
+__device__ uint32_t g_tl_count;
+__device__ uint4 g_tl_rec[kTlCap];
+__device__ __forceinline__ void tl_rec(uint32_t lane, uint32_t kind, uint64_t t0, uint64_t t1, uint32_t len) {
+    if (lane == 0) {
+        const uint32_t k = atomicAdd(&g_tl_count, 1u);
+        if (k < kTlCap)
+            g_tl_rec[k] = make_uint4((blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) | (xcc_id() << 24) |
+                                         (kind << 28),
+                                     (uint32_t)t0, (uint32_t)(t1 - t0), len);
+    }
+}
+#endif
 #ifndef BIH_BINS_WAVES_PER_EU
 #define BIH_BINS_WAVES_PER_EU 0   // 0: the compiler's choice (97 VGPRs, 4 waves: 0.048 vs 0.050 ms/frame forced to 5)
 #endif
@@ -2014,9 +2036,16 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             it = g;
         }
 #else
+#if BIH_BINS_TIMELINE
+    const uint64_t tl_w0 = __builtin_amdgcn_s_memrealtime();
+    tl_rec(lane, 2u, tl_w0, tl_w0, 0u);
+#endif
     while (q.next(lane, it)) {
 #endif
         BIH_PH(0);
+#if BIH_BINS_TIMELINE
+        const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const uint4 hb = q.hb;
         // multi-frame launch: an item covers its tile in frames [f0, nf)
         const uint32_t fs = a.nsplit > 1 ? it / hb.w : 0u;
@@ -2045,6 +2074,9 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 }
             }
             BIH_PH(1);
+#if BIH_BINS_TIMELINE
+            tl_rec(lane, 1u, tl_t0, __builtin_amdgcn_s_memrealtime(), 0u);
+#endif
             continue;
         }
         if (a.dbg & 2u) continue;
@@ -2169,7 +2201,17 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             }
             BIH_PH(5);
         }
+#if BIH_BINS_TIMELINE
+        tl_rec(lane, 0u, tl_t0, __builtin_amdgcn_s_memrealtime(),
+               ((const uint32_t *)a.bin_off)[bin + 1] - ((const uint32_t *)a.bin_off)[bin]);
+#endif
     }
+#if BIH_BINS_TIMELINE
+    {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        tl_rec(lane, 3u, t, t, 0u);
+    }
+#endif
 #if BIH_PHASES
     if (lane == 0)
         for (int k = 0; k < 6; ++k)
@@ -3094,6 +3136,32 @@ static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t bloc
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render_fallback<L>, dim3(fb_blocks), dim3(kThreads), 0, st, a);
     return hipGetLastError();
+}
+
+// Diagnostic builds (BIH_BINS_TIMELINE): appends the per-item records of the
+// k_render_bins launches since the last dump to `path` (raw uint4s) and
+// resets the count.  Returns the number of records, or -1.
+long bins_timeline_dump(const char *path) {
+#if BIH_BINS_TIMELINE
+    uint32_t n = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_tl_count), sizeof n) != hipSuccess) return -1;
+    if (n > kTlCap) n = kTlCap;
+    std::vector<uint4> h(n);
+    if (n && hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_tl_rec), n * sizeof(uint4)) != hipSuccess) return -1;
+    const uint32_t zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl_count), &zero, sizeof zero) != hipSuccess) return -1;
+    if (FILE *f = fopen(path, "ab")) {
+        const uint32_t hdr[4] = {0x544C4942u, n, 0u, 0u};   // "BILT", count: one block per dump
+        fwrite(hdr, sizeof hdr, 1, f);
+        if (n) fwrite(h.data(), sizeof(uint4), n, f);
+        fclose(f);
+    }
+    return (long)n;
+#else
+    (void)path;
+    return -1;
+#endif
 }
 
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev_k0, void *ev_k1) {

@@ -220,6 +220,11 @@ int bih_reserve(bih_tree *tree, uint32_t w, uint32_t h, uint32_t spp, const bih_
                                         the build is enqueued (renders order
                                         after it on the device).  Implied for
                                         bih_build trees (the tree owns its copy) */
+#define BIH_PARAM_TEST_ALLOC_FAIL 7  /* tests, one-shot: the next build that
+                                        allocates its buffers fails at its k-th
+                                        allocation (1..64; BIH_ERR_OOM); the tree
+                                        frees what it had allocated and stays
+                                        usable (0 = off)                       */
 int bih_tree_set_param(bih_tree *tree, int param, uint64_t value);
 
 /* Config C4 (BASELINE.json configs[3]): 8 bounces of mirror (Whitted)

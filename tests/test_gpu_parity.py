@@ -574,9 +574,14 @@ def test_10m_4k_shortcut_equals_exact_walk(gpu, bihrt_mod, oracle_mod):
         a = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_ANYHIT)
         b = _device_render(bihrt_mod, g, w, h, 4, frame, bihrt_mod.TRAVERSE_REFERENCE)
         assert np.array_equal(a, b), (frame, int((a != b).sum()))
-        # 6 rows spread over the frame against the oracle
-        ref, _ = ot.render(w, h, frame=frame, rows=(137, 6, 353), mode=oracle_mod.MODE_GPU_ANYHIT)
-        assert np.array_equal(a[[137 + 353 * k for k in range(6)]], ref), frame
+        # against the oracle: frame 0 every 16th row (135 rows, 2.1 M rays),
+        # frame 5 six rows spread over the frame
+        if frame == 0:
+            ref, _ = ot.render(w, h, frame=frame, rows=(0, 135, 16), mode=oracle_mod.MODE_GPU_ANYHIT)
+            assert np.array_equal(a[0::16], ref), (frame, int((a[0::16] != ref).sum()))
+        else:
+            ref, _ = ot.render(w, h, frame=frame, rows=(137, 6, 353), mode=oracle_mod.MODE_GPU_ANYHIT)
+            assert np.array_equal(a[[137 + 353 * k for k in range(6)]], ref), frame
     assert set(np.unique(a).tolist()) <= {0x281414, 0x1e4e4e, 0x148989, 0x0ac4c4, 0x00ffff}
 
 
@@ -740,8 +745,9 @@ def soup1m(bihrt_mod, oracle_mod):
 def test_headline_call_shape_equals_oracle(layout, gpu, bihrt_mod, oracle_mod, soup1m):
     """The bench's own call: bih_render_device_frames with 16 frames on the 1M
     soup at 1920x1080 (one k_render_bins launch; per-lane XORWOW state kept in
-    LDS across the frames of an item).  Frames 0, 7 and 15 equal the oracle on
-    every 16th row; the state then carries into the next call (cudaRender's
+    LDS across the frames of an item).  Frames 0 and 15 equal the oracle on
+    every row, frame 7 on every 16th row; the state then
+    carries into the next call (frames 16 and 31, every 16th row) (cudaRender's
     persistent curandState, CUDAKernels.cu:411-419; the frame loop of
     App.cpp:174-186).  `bands_rank3_of8`: rank 3's interleaved 8-row bands of
     an 8-GPU split (few tiles: the item's frames are split, start states from
@@ -763,10 +769,21 @@ def test_headline_call_shape_equals_oracle(layout, gpu, bihrt_mod, oracle_mod, s
     r.sync()
     fr = buf.cpu().numpy().view(np.uint32).reshape(2 * G, rows.nrows, w)
     assert g.bins_stats().usable
-    pick = np.arange(0, ys.size, 16)                   # every 16th local row
+    # frames 0 and 15 (the first and last of the call): every row against the
+    # oracle (full frame: 8.3 M rays each, ~2 s of the oracle on the box's
+    # 16 host threads); frames 7, 16 and 31: every 16th local row
     for f in (0, 7, 15, 16, 31):
-        ref = np.stack([ot.render(w, h, frame=f, rows=(int(y), 1, 1), mode=oracle_mod.MODE_GPU_ANYHIT,
-                                  threads=0)[0][0] for y in ys[pick]])
+        pick = np.arange(ys.size) if f in (0, 15) else np.arange(0, ys.size, 16)
+        if layout.startswith("bands"):
+            ref = np.concatenate([ot.render(w, h, frame=f, rows=(int(y0), 8, 1), mode=oracle_mod.MODE_GPU_ANYHIT,
+                                            threads=0)[0] for y0 in ys[pick][::8]]) if f in (0, 15) else \
+                np.stack([ot.render(w, h, frame=f, rows=(int(y), 1, 1), mode=oracle_mod.MODE_GPU_ANYHIT,
+                                    threads=0)[0][0] for y in ys[pick]])
+        elif f in (0, 15):
+            ref, _ = ot.render(w, h, frame=f, mode=oracle_mod.MODE_GPU_ANYHIT, threads=0)
+        else:
+            ref, _ = ot.render(w, h, frame=f, rows=(0, len(pick), 16), mode=oracle_mod.MODE_GPU_ANYHIT, threads=0)
+        assert ref.shape == fr[f][pick].shape, (ref.shape, fr[f][pick].shape)
         assert np.array_equal(fr[f][pick], ref), (layout, f, int((fr[f][pick] != ref).sum()))
     assert not np.array_equal(fr[0], fr[15])           # the jitter moves between frames
 
@@ -801,3 +818,53 @@ def test_steady_frame_loop_allocates_nothing(gpu, bihrt_mod):
     r2.render_device_frames(outs[1].data_ptr(), 5, 16, h * w)
     r2.sync()
     assert g2.info().device_allocs > b0
+
+
+def test_reserved_share_calls_of_every_length_allocate_nothing(gpu, bihrt_mod):
+    """A rank's share of an 8-way band split has few tiles, so a call's items
+    are split over its frames, and the split count is not monotone in the
+    frame count (item_split).  bih_reserve(max_frames=16) sizes the split
+    start states for every call length 1..16: no allocation in the loop."""
+    import torch
+    from bihrt.tiling import band_rows
+    tris = bihrt_mod.scenes.soup(100_000, seed=5)
+    w, h, G = 1920, 1080, 16
+    rows = band_rows(h, 8, 3, 8)
+    g = bihrt_mod.GPUArrayManager(tris)
+    g.reserve(w, h, 4, rows, G)
+    r = bihrt_mod.Renderer(g, w, h)
+    out = torch.zeros(G * rows.nrows * w, dtype=torch.int32, device="cuda")
+    r.render_device_frames(out.data_ptr(), 0, 2, rows.nrows * w, rows=rows)   # camera structures
+    r.sync()
+    a0 = g.info().device_allocs
+    f = 2
+    for m in [3, 5, 7, 1, 9, 11, 13, 16, 6, 2]:
+        r.render_device_frames(out.data_ptr(), f, m, rows.nrows * w, rows=rows)
+        f += m
+    r.sync()
+    assert g.info().device_allocs == a0
+
+
+def test_failed_back_tree_allocation_leaves_tree_usable(gpu, bihrt_mod, oracle_mod):
+    """The first bih_rebuild allocates the second tree buffer; when that
+    allocation fails part-way (BIH_PARAM_TEST_ALLOC_FAIL) the rebuild reports
+    BIH_ERR_OOM, the partial buffers are freed, and the following rebuilds
+    (the first in place, the next into a freshly allocated buffer) and renders
+    are exact (a half-allocated buffer would be read through null pointers)."""
+    tris = bihrt_mod.scenes.soup(20_000, seed=9)
+    w, h = 128, 96
+    ot = oracle_mod.OracleTree(tris)
+    for k in (1, 5, 24):   # fail at the header, in the middle, at the last buffer
+        g = bihrt_mod.GPUArrayManager(tris)
+        r = bihrt_mod.Renderer(g, w, h)
+        g.set_param(bihrt_mod.PARAM_TEST_ALLOC_FAIL, k)
+        with pytest.raises(bihrt_mod.BihError) as ei:
+            g.rebuild()
+        assert ei.value.code == -4, ei.value          # BIH_ERR_OOM
+        g.rebuild()
+        g.rebuild()
+        for f in range(2):
+            img = r.render(f)
+            ref, _ = ot.render(w, h, frame=f)
+            assert np.array_equal(img, ref), (k, f)
+        g.close()

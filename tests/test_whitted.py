@@ -233,6 +233,8 @@ def test_whitted_4k_properties(gpu, bihrt_mod, oracle_mod):
                 lut[key] = pixel_of(list(key))
             assert img[y, x] == lut[key]
     ot = oracle_mod.OracleTree(tris)
-    ref, _, dep = ot.render_whitted(w, h, rows=(1003, 2, 211), depths=True)
-    assert np.array_equal(img[[1003, 1214]], ref)
-    assert np.array_equal(hs[[1003, 1214]].reshape(-1), dep)
+    # every 64th row (34 rows, 0.52 M primary samples and their bounces)
+    # against the oracle, pixels and per-sample hit counts
+    ref, _, dep = ot.render_whitted(w, h, rows=(0, 34, 64), depths=True)
+    assert np.array_equal(img[0::64], ref), int((img[0::64] != ref).sum())
+    assert np.array_equal(hs[0::64].reshape(-1), dep)

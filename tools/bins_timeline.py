@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Analyses the per-item records of k_render_bins written by a
+BIH_BINS_TIMELINE=1 build (bih_sync appends one block per synchronised call
+to $BIH_TIMELINE_OUT; tools/call_breakdown.py --sync 1 makes one block per
+launch).  Per launch: span (first wave start -> last wave exit), items, item
+durations, when the queue ran dry (last item start) and the tail after it,
+wave-slot utilisation (item time / (waves x span)) and its profile over the
+span in tenths.  Times: s_memrealtime, 100 MHz (10 ns).
+usage: tools/bins_timeline.py FILE [--skip N] [--show K]"""
+import argparse
+import struct
+
+import numpy as np
+
+
+def blocks(path):
+    data = open(path, "rb").read()
+    off = 0
+    while off + 16 <= len(data):
+        magic, n, _, _ = struct.unpack_from("<4I", data, off)
+        off += 16
+        if magic != 0x544C4942:
+            raise SystemExit("bad block header")
+        rec = np.frombuffer(data, dtype=np.uint32, count=4 * n, offset=off).reshape(n, 4).astype(np.int64)
+        off += 16 * n
+        yield rec
+
+
+def analyse(rec):
+    wave = rec[:, 0] & 0xFFFFFF
+    xcc = (rec[:, 0] >> 24) & 15
+    kind = rec[:, 0] >> 28
+    t = rec[:, 1].copy()
+    t = (t - t[0] + (1 << 31)) % (1 << 32) - (1 << 31)    # unwrap relative to the first record
+    t -= t.min()
+    dur = rec[:, 2]
+    ln = rec[:, 3]
+    starts, exits = t[kind == 2], t[kind == 3]
+    span = (exits.max() - starts.min()) / 100.0          # us
+    items = kind <= 1
+    live, bg = kind == 0, kind == 1
+    it_s, it_e = t[items] / 100.0, (t[items] + dur[items]) / 100.0
+    nwaves = int((kind == 2).sum())
+    last_start = it_s.max()
+    busy = dur[items].sum() / 100.0
+    prof = []
+    edges = np.linspace(0, span, 11)
+    for a, b in zip(edges[:-1], edges[1:]):
+        ov = np.clip(np.minimum(it_e, b) - np.maximum(it_s, a), 0, None).sum()
+        prof.append(ov / (nwaves * (b - a)))
+    d_live = dur[live] / 100.0
+    q = lambda v, f: float(np.quantile(v, f)) if v.size else 0.0
+    out = {
+        "span_us": span, "waves": nwaves, "items_live": int(live.sum()), "items_bg": int(bg.sum()),
+        "utilisation": busy / (nwaves * span),
+        "queue_dry_us": float(last_start), "tail_us": span - float(last_start),
+        "wave_exit_q10_q50_q90_us": [q(exits / 100.0, 0.1), q(exits / 100.0, 0.5), q(exits / 100.0, 0.9)],
+        "live_item_us_mean_p50_p90_p99_max": [float(d_live.mean()) if d_live.size else 0.0, q(d_live, .5),
+                                             q(d_live, .9), q(d_live, .99), float(d_live.max()) if d_live.size else 0.0],
+        "bg_item_us_mean": float((dur[bg] / 100.0).mean()) if bg.any() else 0.0,
+        "profile_tenths": [round(x, 3) for x in prof],
+        "xcd_exit_us": [round(float(exits[xcc[kind == 3] == x].max() / 100.0), 1) if (xcc[kind == 3] == x).any()
+                        else None for x in range(8)],
+    }
+    # the longest live items: start, duration, list length
+    if live.any():
+        idx = np.argsort(-dur[live])[:5]
+        ls, ld, ll = t[live][idx] / 100.0, dur[live][idx] / 100.0, ln[live][idx]
+        out["longest_live"] = [(round(float(a), 1), round(float(b), 1), int(c)) for a, b, c in zip(ls, ld, ll)]
+        # items that end in the last 10 % of the span
+        late = (it_e > 0.9 * span) & (kind[items] == 0)
+        out["live_items_ending_in_last_tenth"] = int(late.sum())
+        # list length vs duration (mean per list-length class)
+        cls = np.floor(np.log2(np.maximum(ln[live], 1))).astype(int)
+        out["us_by_log2_list_len"] = {int(c): (int((cls == c).sum()), round(float(d_live[cls == c].mean()), 2))
+                                      for c in np.unique(cls)}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("file")
+    ap.add_argument("--skip", type=int, default=2, help="blocks to skip (warm-up)")
+    ap.add_argument("--show", type=int, default=3)
+    a = ap.parse_args()
+    res = [analyse(r) for r in blocks(a.file)][a.skip:]
+    for r in res[:a.show]:
+        print("---")
+        for k, v in r.items():
+            print(f"  {k}: {v}")
+    if res:
+        keys = ["span_us", "utilisation", "queue_dry_us", "tail_us"]
+        print("mean over %d launches:" % len(res), {k: round(float(np.mean([r[k] for r in res])), 3) for k in keys})
+        print("mean profile:", [round(float(x), 3) for x in np.mean([r["profile_tenths"] for r in res], 0)])
+
+
+if __name__ == "__main__":
+    main()
