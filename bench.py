@@ -48,8 +48,10 @@ def parse():
                          "environment) N > 1 starts the N ranks itself (torch.distributed.run, before this "
                          "process touches the GPU) and relays rank 0's line; under a launcher it must equal "
                          "WORLD_SIZE.  Default: WORLD_SIZE, else 1")
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    # the defaults are the driver's command (--gpus 1 --steps 20 --warmup 5);
+    # --steps 500 --warmup 50 gives the steady state of a long frame loop
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tris", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
