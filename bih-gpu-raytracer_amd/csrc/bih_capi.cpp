@@ -159,6 +159,7 @@ struct bih_tree {
     // records.
     hipEvent_t ev_rng = nullptr;
     bool rng_pending = false;
+    bool rng_after_render = false;   // ev_rng follows the last render (it wrote the next state itself)
     // after the last (re)build of the tree: the per-camera builds order after
     // it (and after the renders that read their set), not after each other
     hipEvent_t ev_tree = nullptr;
@@ -208,6 +209,8 @@ struct bih_tree {
     size_t wh_rays = 0;              // queue capacity (rays)
     uint64_t wh_last_rays = 0;       // rays of the last Whitted render (its buffer layout)
     int wh_last_slot = -1;           // its slot (evd), when it ran with work counters
+    unsigned long long *wh_mask = nullptr;   // primary samples' hit masks per tile (bounce 0 through the bins)
+    size_t wh_mask_cap = 0;                  // tiles
 };
 
 namespace {
@@ -413,7 +416,10 @@ int finish_build(bih_tree *tr) {
     hipError_t he = hipEventRecord(tr->ev_tree, tr->stream);
     if (he == hipSuccess && !had) he = hipEventRecord(tr->ev_rng, tr->stream);
     if (he != hipSuccess) return map_hip((int)he);
-    if (!had) tr->rng_pending = true;
+    if (!had) {
+        tr->rng_pending = true;
+        tr->rng_after_render = false;
+    }
     tr->tree_pending = true;
     return BIH_OK;
 }
@@ -602,6 +608,7 @@ void bih_free(bih_tree *tr) {
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
     if (tr->rsplit) (void)hipFree(tr->rsplit);
     if (tr->wh_mem) (void)hipFree(tr->wh_mem);
+    if (tr->wh_mask) (void)hipFree(tr->wh_mask);
     for (int k = 0; k < kSlots; ++k) {
         if (tr->ev0[k]) (void)hipEventDestroy(tr->ev0[k]);
         if (tr->evd[k]) (void)hipEventDestroy(tr->evd[k]);
@@ -657,7 +664,8 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
-                          (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4;
+                          (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4 +
+                         (tr->wh_mem ? bih::whitted_bytes(tr->wh_rays) : 0) + tr->wh_mask_cap * 8;
     info->build_ms = tr->build_ms;
     info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
     return BIH_OK;
@@ -815,6 +823,17 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
     }
     tr->next_frame = frame + 1;
     return BIH_OK;
+}
+
+// The XORWOW advance inside k_render_bins (RenderArgs::rng_out) with
+// BIH_FUSED_ADVANCE=1 (experimental, A/B); default: the k_rng_advance launch
+// ahead of every render.
+static bool fused_advance_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("BIH_FUSED_ADVANCE");
+        return e && strcmp(e, "1") == 0;
+    }();
+    return on;
 }
 
 // Frustum bins are on unless BIH_BINS=0 (A-B); they never change a pixel.
@@ -1108,10 +1127,14 @@ static void item_split(const bih_tree *tr, uint32_t w, uint32_t nrows, uint32_t 
 // kRenderPerFrame, before any RNG work, when this render does not go
 // through the bins (the caller then renders the frames one by one).
 constexpr int kRenderPerFrame = 1;
+// hit_mask (config C4's primary rays, one frame): also write each tile's
+// 64-bit mask of the samples that hit (RenderArgs::hit_mask), and leave the
+// XORWOW ring at this frame's state for the Whitted render that follows
+// (kRenderPerFrame, before any work, when the bins do not cover the render).
 static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
                               uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
                               uint32_t *d_out, uint32_t *d_ray_stats, void *stream, uint32_t nframes,
-                              uint64_t out_stride) {
+                              uint64_t out_stride, unsigned long long *hit_mask = nullptr) {
     if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0 || traverse > 1) return BIH_ERR_INVALID;
     bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
     if (rows.nrows == 0) return BIH_OK;
@@ -1260,7 +1283,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         // a packet's rows are one bin row when tiles and bands align
         use_bins = rows.row0 % th == 0 && rows.band_h % th == 0;
     }
-    if (nframes > 1 && !use_bins) return kRenderPerFrame;
+    if ((nframes > 1 || hit_mask) && !use_bins) return kRenderPerFrame;
     // the frame's per-pixel XORWOW state (InitRandGPU / the state earlier
     // frames left), and the state cudaRender leaves behind for the frame
     // after this launch's last (CUDAKernels.cu:419)
@@ -1294,10 +1317,26 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
         a.rng_split = split;
     }
-    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
-                                         2 * spp * a.fpi, a.nsplit));
-    if (rc) return rc;
-    tr->next_frame = frame + nframes;
+    // nsplit == 1 through the bins: the render writes the next call's state
+    // itself (RenderArgs::rng_out), so no k_rng_advance launch sits ahead of
+    // it; the next render then orders after this one (ev_rng below).  Split
+    // launches read stored split states, which the advance kernel makes.
+    const bool fused = use_bins && a.nsplit == 1 && fused_advance_enabled() && !hit_mask;
+    if (hit_mask) {
+        // the ring stays at this frame: the Whitted render of the same frame
+        // draws the same jitter and advances it
+        a.hit_mask = hit_mask;
+        tr->next_frame = frame;
+    } else if (fused) {
+        a.rng_out = rng_buf(tr, nxt);
+        const uint32_t steps = 2 * spp * nframes;
+        a.adv_ppl = steps >= 256 ? 1u : steps >= 128 ? 2u : steps >= 64 ? 4u : 8u;
+    } else {
+        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
+                                             2 * spp * a.fpi, a.nsplit));
+        if (rc) return rc;
+    }
+    if (!hit_mask) tr->next_frame = frame + nframes;
     e = wait_tree();
     if (e != hipSuccess) return map_hip((int)e);
     if (use_bins) {
@@ -1343,10 +1382,13 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     }
     // the next render (on any stream) orders after the advance above, the
     // per-camera records, the shortcut boxes and the tile queue, which it
-    // reads as they stand now
-    e = hipEventRecord(tr->ev_rng, st);
-    if (e != hipSuccess) return map_hip((int)e);
-    tr->rng_pending = true;
+    // reads as they stand now (a render that writes the next state itself:
+    // after the render, below)
+    if (!fused) {
+        e = hipEventRecord(tr->ev_rng, st);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->rng_pending = true;
+    }
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;
@@ -1382,13 +1424,22 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // resident blocks so that the two overlap (bih_render.hip,
     // bins_grid_blocks); alone, it takes every slot
     // (a render queued on this same stream cannot overlap this one)
-    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid; ++k)
+    // (not behind a render that wrote this render's input state: this one
+    // starts after it ends)
+    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid && !tr->rng_after_render; ++k)
         if (k != slot && tr->used[k] && tr->slot_stream[k] != st && hipEventQuery(tr->evd[k]) == hipErrorNotReady)
             a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
     if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
+    if (fused) {
+        // the next render reads the state this one wrote
+        e = hipEventRecord(tr->ev_rng, st);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->rng_pending = true;
+    }
+    tr->rng_after_render = fused;
     if (tr->timing) {
         e = hipEventRecord(tr->ev2[slot], st);
         if (e != hipSuccess) return map_hip((int)e);
@@ -1403,7 +1454,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     tr->cs_cur = ci;
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
-    tr->rng_cur = nxt;                 // frame+1's state
+    if (!hit_mask) tr->rng_cur = nxt;  // frame+1's state
     rng_guard.armed = false;
     return BIH_OK;
 }
@@ -1530,6 +1581,41 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     // count by at most one 64-ray fetch per wave of its grid (<= 2^20 lanes)
     if ((uint64_t)h * w * spp > 0xFFFFFFFFull - (1ull << 20)) return BIH_ERR_TOO_LARGE;
     DeviceGuard g(tr->t.device);
+    // Bounce 0 through the frustum bins: the any-hit render of the same
+    // frame (the primary render's kernels) leaves per tile the mask of its
+    // samples that hit; only those enter the closest-hit walk of bounce 0 (a
+    // proven miss has no closest hit: same visit set, same test).  Its pixels
+    // go to d_out, which the Whitted shade overwrites.  BIH_WH_BINS=0: every
+    // primary sample is walked (A/B).
+    unsigned long long *mask = nullptr;
+    uint32_t mask_tiles_x = 0;
+    static const bool wh_bins = [] {
+        const char *e = getenv("BIH_WH_BINS");
+        return !(e && e[0] == '0');
+    }();
+    if (wh_bins && bins_enabled() && spp <= 64 && (spp & (spp - 1)) == 0 && tr->t.u > 1) {
+        uint32_t tw = 0, th = 0;
+        tile_shape(spp, &tw, &th);
+        mask_tiles_x = (w + tw - 1) / tw;
+        const size_t ntiles = (size_t)mask_tiles_x * ((rows.nrows + th - 1) / th);
+        {
+            std::lock_guard<std::mutex> lk(tr->mu);
+            if (tr->wh_mask_cap < ntiles) {
+                int rc = drain_renders(tr);
+                if (rc) return rc;
+                if (tr->wh_mask) (void)hipFree(tr->wh_mask);
+                tr->wh_mask = nullptr;
+                tr->wh_mask_cap = 0;
+                hipError_t e = tree_malloc(tr, &tr->wh_mask, ntiles * 8);
+                if (e != hipSuccess) return map_hip((int)e);
+                tr->wh_mask_cap = ntiles;
+            }
+        }
+        const int mrc = render_device_impl(tr, cam, w, h, spp, frame, seed, &rows, BIH_TRAVERSE_ANYHIT, d_out,
+                                           nullptr, stream, 1, 0, tr->wh_mask);
+        if (mrc == BIH_OK) mask = tr->wh_mask;
+        else if (mrc != kRenderPerFrame) return mrc;
+    }
     std::lock_guard<std::mutex> lk(tr->mu);
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     // the queues are shared by every Whitted render of this tree: order after
@@ -1570,6 +1656,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     hipError_t e = hipEventRecord(tr->ev_rng, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
+    tr->rng_after_render = false;
     bih::RenderArgs a;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
@@ -1593,7 +1680,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     const int slot = tr->slot;
     const bool count = tr->prm.wh_counters != 0;
     rc = bih::launch_whitted(a, tr->wh_mem, rays, d_hits, st, tr->timing ? tr->ev0[slot] : nullptr,
-                             tr->timing ? tr->ev1[slot] : nullptr, count);
+                             tr->timing ? tr->ev1[slot] : nullptr, count, mask, mask_tiles_x);
     if (rc) return map_hip(rc);
     tr->wh_last_rays = rays;
     tr->wh_last_slot = count ? slot : -1;

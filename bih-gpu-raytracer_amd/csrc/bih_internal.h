@@ -128,6 +128,18 @@ struct RenderArgs {
     uint32_t fpi = 1;
     uint32_t nsplit = 1;
     const uint32_t *rng_split = nullptr;    // split s >= 1's start states at (s-1) * 5 planes (k_rng_advance)
+    // k_render_bins with nsplit == 1: the XORWOW state after the launch's
+    // frames (the next call's rng_in) written by the render itself -- live
+    // items store the state their frame loop ends with, and advance items
+    // (after each band's background items, adv_ppl pixels per lane) step the
+    // background pixels' states -- instead of a k_rng_advance launch ahead
+    // of the render.  null: the advance kernel ran.
+    uint32_t *rng_out = nullptr;
+    uint32_t adv_ppl = 1;
+    // one-frame k_render_bins (config C4's primary rays): per local tile the
+    // 64-bit mask of its samples that hit (lane = pixel * spp + sample), 0 for
+    // background tiles; k_render_fallback writes the undecided packets'
+    unsigned long long *hit_mask = nullptr;
 };
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
@@ -217,7 +229,7 @@ const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host()
 // per sample.
 size_t whitted_bytes(uint64_t rays);
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
-                   void *ev_k1, bool count);
+                   void *ev_k1, bool count, const unsigned long long *hit_mask = nullptr, uint32_t tiles_x = 0);
 int whitted_work(const void *mem, uint64_t rays, uint32_t ray_counts[9], unsigned long long work[18], void *stream);
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);

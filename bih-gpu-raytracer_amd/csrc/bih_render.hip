@@ -1877,18 +1877,20 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 #endif
 #if BIH_BINS_TIMELINE
 // {wave | xcc << 24 | kind << 28, start, duration, list length} per queue
-// item (s_memrealtime, 100 MHz); kind 0 live item, 1 background item, 2
-// wave start, 3 wave exit
-constexpr uint32_t kTlCap = 1u << 20;
-__device__ uint32_t g_tl_count;
-__device__ uint4 g_tl_rec[kTlCap];
+// item (s_memrealtime, 100 MHz); kind 0 live item, 1 background or advance
+// item (length 1), 2 wave start, 3 wave exit.  Each wave appends to its own
+// run of kTlPerWave records (no shared counter: a single atomic word would
+// serialise the items, ~90 per us); g_tl_n[wave] counts them.
+constexpr uint32_t kTlWaves = 1u << 14, kTlPerWave = 62;
+__device__ uint32_t g_tl_n[kTlWaves];
+__device__ uint4 g_tl_rec[kTlWaves * kTlPerWave];
 __device__ __forceinline__ void tl_rec(uint32_t lane, uint32_t kind, uint64_t t0, uint64_t t1, uint32_t len) {
-    if (lane == 0) {
-        const uint32_t k = atomicAdd(&g_tl_count, 1u);
-        if (k < kTlCap)
-            g_tl_rec[k] = make_uint4((blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) | (xcc_id() << 24) |
-                                         (kind << 28),
-                                     (uint32_t)t0, (uint32_t)(t1 - t0), len);
+    const uint32_t wv = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (lane == 0 && wv < kTlWaves) {
+        const uint32_t k = g_tl_n[wv]++;
+        if (k < kTlPerWave)
+            g_tl_rec[wv * kTlPerWave + k] = make_uint4(wv | (xcc_id() << 24) | (kind << 28), (uint32_t)t0,
+                                                       (uint32_t)(t1 - t0), len);
     }
 }
 #endif
@@ -1924,6 +1926,10 @@ struct BinQueue {
     unsigned long long pending;        // a position claimed ahead (claim()), lane 0
     bool has_pending;
     uint32_t nf;                       // frames per launch: a band holds hb.w * nf items
+    uint32_t adv_tpi;                  // background tiles per advance item (0: none), after them
+    __device__ __forceinline__ uint32_t items(const uint4 &h) const {
+        return h.w * nf + (adv_tpi ? (h.z + adv_tpi - 1u) / adv_tpi : 0u);
+    }
 
     // Claims the slot position next() will use, so that its round trip
     // overlaps the current item's loads (BIH_QUEUE_AHEAD).
@@ -1949,7 +1955,7 @@ struct BinQueue {
             if (hi != 0 && lo < kBinBatch) {
                 const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch;
                 hb = hdr[b];
-                if (start + lo < hb.w * nf) {
+                if (start + lo < items(hb)) {
                     item = start + lo;
                     band = b;
                     return true;
@@ -1962,7 +1968,7 @@ struct BinQueue {
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    if (c < h.w * nf) {
+                    if (c < items(h)) {
                         if (lane == 0)
                             atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
                         hb = h;
@@ -2006,6 +2012,8 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.left = 8;
     q.has_pending = false;
     q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
+    constexpr uint32_t PT = 64u >> LOG2SPP;   // pixels per tile
+    q.adv_tpi = a.rng_out ? (64u * a.adv_ppl) / PT : 0u;
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
     // timing experiment: items dealt round-robin over the waves (no atomics)
@@ -2052,11 +2060,63 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         it -= fs * hb.w;
         const uint32_t f0 = fs * a.fpi;
         const uint32_t nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
+        if (q.adv_tpi && it >= hb.w) {
+            // advance item: the XORWOW state of background pixels (no
+            // triangle can be hit there, so the render never draws their
+            // jitter) stepped over the launch's 2*SPP*nframes draws into
+            // rng_out, adv_ppl pixels per lane, loads issued together
+            const uint64_t P = (uint64_t)a.nrows * a.w;
+            const uint32_t k0 = (it - hb.w) * q.adv_tpi;
+            const uint32_t steps = 2u * SPP * a.nframes;
+            // two pixels per pass (both loads in flight; the walk's registers
+            // are dead here, but all eight at once took 148 VGPRs)
+#pragma unroll 1
+            for (uint32_t i = 0; i < a.adv_ppl; i += 2) {
+                uint32_t v[2][5];
+                uint64_t lpx[2];
+                bool ok[2];
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t p = (i + h) * 64u + lane, k = k0 + p / PT;
+                    ok[h] = false;
+                    lpx[h] = 0;
+                    if (i + h < a.adv_ppl && k < hb.z) {
+                        const uint32_t t = a.bin_queue[hb.x + hb.y + k];
+                        uint32_t x, lr, ss;
+                        ray_coords<LOG2SPP>((uint64_t)t * 64 + (p % PT) * SPP, tiles_x, x, lr, ss);
+                        ok[h] = x < a.w && lr < a.nrows;
+                        lpx[h] = (uint64_t)lr * a.w + x;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) v[h][j] = ok[h] ? a.rng_in[(uint64_t)j * P + lpx[h]] : 0u;
+                }
+#pragma unroll 4
+                for (uint32_t k = 0; k < steps; ++k) {
+#pragma unroll
+                    for (uint32_t h = 0; h < 2; ++h) {
+                        const uint32_t t = v[h][0] ^ (v[h][0] >> 2);
+                        v[h][0] = v[h][1]; v[h][1] = v[h][2]; v[h][2] = v[h][3]; v[h][3] = v[h][4];
+                        v[h][4] = (v[h][4] ^ (v[h][4] << 4)) ^ (t ^ (t << 1));
+                    }
+                }
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h)
+                    if (ok[h]) {
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) a.rng_out[(uint64_t)j * P + lpx[h]] = v[h][j];
+                    }
+            }
+#if BIH_BINS_TIMELINE
+            tl_rec(lane, 1u, tl_t0, __builtin_amdgcn_s_memrealtime(), 1u);
+#endif
+            continue;
+        }
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
             const uint32_t k = (it - hb.y) * 64u + lane;
             if (k < hb.z && !(a.dbg & 1u)) {
                 const uint32_t t = a.bin_queue[hb.x + hb.y + k];
+                if (a.hit_mask) a.hit_mask[t] = 0ull;      // (one-frame launches)
                 const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
                 const uint32_t x0 = tx * TW;
                 for (uint32_t fj = f0; fj < nf; ++fj) {
@@ -2120,7 +2180,9 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                     if (k == 2u * s + 1u) xv = x;
                 }
                 const float ru = dev::xorwow_to_uniform(xu), rv = dev::xorwow_to_uniform(xv);
-                if (fj + 1u < nf) {
+                // (after the launch's last frame too when the render writes
+                // the next call's state: stored once the item is done)
+                if (fj + 1u < nf || a.rng_out) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
                 }
@@ -2199,7 +2261,15 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
                 fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
             }
+            if (a.hit_mask && lane == 0) a.hit_mask[tile] = hits;
             BIH_PH(5);
+        }
+        if (a.rng_out && valid && s == 0u) {
+            // the pixel's state after the launch's frames: the next call's
+            // input (cudaRender's write-back, CUDAKernels.cu:419)
+            const uint64_t P = (uint64_t)a.nrows * a.w;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = s_rs[i][tid];
         }
 #if BIH_BINS_TIMELINE
         tl_rec(lane, 0u, tl_t0, __builtin_amdgcn_s_memrealtime(),
@@ -2270,6 +2340,7 @@ __global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a
             const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
             fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
         }
+        if (a.hit_mask && lane == 0) a.hit_mask[tile] = hits;
     }
 }
 
@@ -3143,21 +3214,27 @@ static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t bloc
 // resets the count.  Returns the number of records, or -1.
 long bins_timeline_dump(const char *path) {
 #if BIH_BINS_TIMELINE
-    uint32_t n = 0;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_tl_count), sizeof n) != hipSuccess) return -1;
-    if (n > kTlCap) n = kTlCap;
-    std::vector<uint4> h(n);
-    if (n && hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_tl_rec), n * sizeof(uint4)) != hipSuccess) return -1;
-    const uint32_t zero = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl_count), &zero, sizeof zero) != hipSuccess) return -1;
+    std::vector<uint32_t> cnt(kTlWaves);
+    std::vector<uint4> rec((size_t)kTlWaves * kTlPerWave);
+    if (hipMemcpyFromSymbol(cnt.data(), HIP_SYMBOL(g_tl_n), kTlWaves * 4) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(rec.data(), HIP_SYMBOL(g_tl_rec), rec.size() * sizeof(uint4)) != hipSuccess) return -1;
+    std::vector<uint32_t> zero(kTlWaves, 0u);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl_n), zero.data(), kTlWaves * 4) != hipSuccess) return -1;
+    std::vector<uint4> out;
+    uint32_t lost = 0;
+    for (uint32_t w = 0; w < kTlWaves; ++w) {
+        const uint32_t n = cnt[w] < kTlPerWave ? cnt[w] : kTlPerWave;
+        lost += cnt[w] - n;
+        for (uint32_t k = 0; k < n; ++k) out.push_back(rec[(size_t)w * kTlPerWave + k]);
+    }
     if (FILE *f = fopen(path, "ab")) {
-        const uint32_t hdr[4] = {0x544C4942u, n, 0u, 0u};   // "BILT", count: one block per dump
+        const uint32_t hdr[4] = {0x544C4942u, (uint32_t)out.size(), lost, 0u};   // "BILT", count, dropped
         fwrite(hdr, sizeof hdr, 1, f);
-        if (n) fwrite(h.data(), sizeof(uint4), n, f);
+        if (!out.empty()) fwrite(out.data(), sizeof(uint4), out.size(), f);
         fclose(f);
     }
-    return (long)n;
+    return (long)out.size();
 #else
     (void)path;
     return -1;

@@ -247,21 +247,47 @@ struct WQueue {
     }
 };
 
-// counts[0..9]: rays in queue d (d = bounce depth)
+// counts[0..9]: rays in queue d (d = bounce depth).  With hit_mask (the
+// primary samples' any-hit result from the frustum bins, one u64 per tile of
+// TW x TH pixels, lane = pixel * spp + sample): only the samples that hit are
+// queued for bounce 0, compacted per wave (ballot + mbcnt, one atomic on
+// counts[0], zeroed before the launch); a sample the bins prove to miss has no
+// closest hit either (the same visit set and test), so its depth stays 0.
 __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, uint32_t *counts,
-                                                uint8_t *hits, uint32_t *sort_hist) {
+                                                uint8_t *hits, uint32_t *sort_hist,
+                                                const unsigned long long *hit_mask, uint32_t tiles_x,
+                                                uint32_t log2spp) {
     const uint64_t P = (uint64_t)a.nrows * a.w;
     const uint64_t rays = P * a.spp;
     const uint64_t gid = (uint64_t)blockIdx.x * kWT + threadIdx.x;
     // k_wh_sort_*'s histogram (zeroed again by each scan), whatever the grid
     for (uint64_t k = gid; k < kWSortBucketsGen; k += (uint64_t)gridDim.x * kWT) sort_hist[k] = 0u;
-    if (gid == 0) {
+    if (gid == 0 && !hit_mask) {
         counts[0] = (uint32_t)rays;
         for (uint32_t k = 1; k < kWCounts; ++k) counts[k] = 0u;
     }
-    if (gid >= rays) return;
-    const uint64_t lp = gid / a.spp;
+    const bool in = gid < rays;
+    const uint64_t lp = in ? gid / a.spp : 0;
     const uint32_t s = (uint32_t)(gid % a.spp);
+    const uint32_t lr = (uint32_t)(lp / a.w), x = (uint32_t)(lp % a.w);
+    bool hit = in;
+    if (hit_mask && in) {
+        // TileShape: TW x TH pixels, TW * TH = 64 >> log2(spp)
+        const uint32_t lpx = 6 - log2spp, tw = 1u << ((lpx + 1) / 2), th = 1u << (lpx / 2);
+        const uint32_t tile = (lr / th) * tiles_x + x / tw;
+        const uint32_t bit = (((lr % th) * tw + (x % tw)) << log2spp) + s;
+        hit = (hit_mask[tile] >> bit) & 1ull;
+    }
+    uint64_t slot = gid;
+    if (hit_mask) {
+        const unsigned long long b = __ballot(hit);
+        uint32_t base = 0;
+        if (threadIdx.x == 0 && b) base = atomicAdd(counts, (uint32_t)__popcll(b));
+        base = __builtin_amdgcn_readfirstlane(base);
+        slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    }
+    if (in) hits[gid] = 0;
+    if (!hit) return;
     // draws 2s, 2s+1 of this pixel's frame (cudaRender :413-415)
     uint32_t v[5];
     for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
@@ -271,12 +297,10 @@ __global__ void __launch_bounds__(kWT) k_wh_gen(const RenderArgs a, WQueue q, ui
         ru = xorwow_uniform(v, d);
         rv = xorwow_uniform(v, d);
     }
-    const uint32_t lr = (uint32_t)(lp / a.w), x = (uint32_t)(lp % a.w);
     const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
     float dir[3];
     camera_dir(a, ((float)x + ru) / (float)a.w, ((float)y + rv) / (float)a.h, dir[0], dir[1], dir[2]);
-    q.put(gid, a.cam, dir, (uint32_t)gid);
-    hits[gid] = 0;
+    q.put(slot, a.cam, dir, (uint32_t)gid);
 }
 
 __global__ void __launch_bounds__(kWT) k_wh_trace(const RenderArgs a, uint32_t depth, WQueue qin, WQueue qout,
@@ -831,7 +855,7 @@ int whitted_work(const void *mem, uint64_t rays, uint32_t ray_counts[9], unsigne
 }
 
 int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hits, void *stream, void *ev_k0,
-                   void *ev_k1, bool count) {
+                   void *ev_k1, bool count, const unsigned long long *hit_mask, uint32_t tiles_x) {
     const hipStream_t st = (hipStream_t)stream;
     if (rays == 0) return 0;
     float *base = reinterpret_cast<float *>(mem);
@@ -845,8 +869,13 @@ int launch_whitted(const RenderArgs &a, void *mem, uint64_t rays, uint32_t *d_hi
         const hipError_t ez = hipMemsetAsync(work, 0, kWWorkWords * 8, st);
         if (ez != hipSuccess) return (int)ez;
     }
+    if (hit_mask) {
+        // k_wh_gen appends the primary samples that hit to queue 0
+        const hipError_t ez = hipMemsetAsync(counts, 0, kWCounts * 4, st);
+        if (ez != hipSuccess) return (int)ez;
+    }
     hipLaunchKernelGGL(k_wh_gen, dim3((uint32_t)((rays + kWT - 1) / kWT)), dim3(kWT), 0, st, a, q0, counts, hits,
-                       hist);
+                       hist, hit_mask, tiles_x, (uint32_t)__builtin_ctz(a.spp));
     hipError_t e = ev_k0 ? hipEventRecord((hipEvent_t)ev_k0, st) : hipSuccess;
     if (e != hipSuccess) return (int)e;
     const uint32_t grid = whitted_grid(rays);

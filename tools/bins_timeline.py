@@ -17,7 +17,9 @@ def blocks(path):
     data = open(path, "rb").read()
     off = 0
     while off + 16 <= len(data):
-        magic, n, _, _ = struct.unpack_from("<4I", data, off)
+        magic, n, lost, _ = struct.unpack_from("<4I", data, off)
+        if lost:
+            print(f"(block with {lost} records dropped: more items per wave than the buffer holds)")
         off += 16
         if magic != 0x544C4942:
             raise SystemExit("bad block header")

@@ -24,10 +24,12 @@ def main():
     ap.add_argument("--dispatch-csv", default="")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    # a call starts at its k_rng_advance, or at its k_render_bins when the
+    # render advances the XORWOW state itself (no advance launch)
     calls, cur = [], None
     for r in rows:
         n = name(r)
-        if n == "k_rng_advance":
+        if n == "k_rng_advance" or (n == "k_render_bins" and (cur is None or any(x[0] == n for x in cur))):
             cur = []
             calls.append(cur)
         if cur is not None:
@@ -49,11 +51,13 @@ def main():
 
     for i, c in enumerate(half):
         d = {n: (s, e) for n, s, e, _ in c}
-        if not all(k in d for k in ("k_rng_advance", "k_render_bins", "k_render_fallback")):
+        if not all(k in d for k in ("k_render_bins", "k_render_fallback")):
             continue
-        adv, ren, fb = d["k_rng_advance"], d["k_render_bins"], d["k_render_fallback"]
-        add("advance", adv[1] - adv[0])
-        add("gap advance->render", ren[0] - adv[1])
+        ren, fb = d["k_render_bins"], d["k_render_fallback"]
+        if "k_rng_advance" in d:
+            adv = d["k_rng_advance"]
+            add("advance", adv[1] - adv[0])
+            add("gap advance->render", ren[0] - adv[1])
         add("render", ren[1] - ren[0])
         add("gap render->fallback", fb[0] - ren[1])
         add("fallback", fb[1] - fb[0])
