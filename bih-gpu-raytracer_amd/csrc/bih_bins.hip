@@ -1092,11 +1092,20 @@ __global__ void k_bin_status(uint32_t *__restrict__ g, uint32_t cap) {
 // Work queue of one launch's tiles (local tile ids t = ty * tiles_x + tx of
 // its rows, bih_rows), in kRegions bands of tile rows, one per XCD (the
 // render kernel's waves on XCD x draw from band x first, then from the
-// others): per band the tiles with a non-empty list, by descending list
-// length in power-of-two classes (longest processing time first), then the
-// tiles no triangle touches (background).  Built once per camera, image and
-// row set (bih_render.hip draws from it).
-constexpr uint32_t kQBands = 8, kQClasses = 34;   // classes 0..32: clz(length); 33: background
+// others): per band the tiles with a non-empty list, longest processing time
+// first, then the tiles no triangle touches (background).  Without measured
+// costs the order is by power-of-two classes of the list length; with them
+// (the cycles per frame an earlier launch of this camera measured for each
+// tile, RenderArgs::bin_cost) by quarter-power-of-two classes of the cost,
+// and each band's tiles costing at least kHeavyFactor x the mean -- their
+// items would otherwise run for most of a multi-frame launch on one wave --
+// come first and are counted (qw[kQHeavy + band]) for the kernel to split over
+// frame ranges.  Built once per camera, image, row set and cost state.
+constexpr uint32_t kQBands = 8, kQClasses = 65;   // live classes 0..63 (costliest first), 64: background
+constexpr uint32_t kQCount = 0, kQStart = kQBands * kQClasses, kQCur = 2 * kQBands * kQClasses,
+                   kQHdr = 3 * kQBands * kQClasses, kQHeavy = kQHdr + 4 * kQBands, kQWords = 2048;
+static_assert(kQHeavy + kQBands <= kQWords, "queue words");
+constexpr uint32_t kHeavyFactor = 2;
 __device__ __forceinline__ uint32_t queue_bin(uint32_t t, uint32_t tiles_x, uint32_t row0,
                                               uint32_t band_h, uint32_t band_step, uint32_t th,
                                               uint32_t bins_x) {
@@ -1105,14 +1114,28 @@ __device__ __forceinline__ uint32_t queue_bin(uint32_t t, uint32_t tiles_x, uint
     const uint32_t gy = row0 + (lr / band_h) * band_h * band_step + (lr % band_h);
     return (gy / th) * bins_x + tx;
 }
-// qw: [0, 272) class counts, [288, 560) class starts, [576, 848) fill
-// cursors, [896, 928) per band {start, live, background, items}
+// cost -> class: key = 4 log2(cost) (two fraction bits), class 95 - key
+// clamped to [0, 63]: the costliest first, a quarter power of two apart
+// (k_render_bins' cost = 256 x (entries pre-tested + 4 x intersector calls)
+// per frame, ~2^11 .. 2^16: classes ~31 .. 51)
+__device__ __forceinline__ uint32_t cost_class(uint32_t cost) {
+    const uint32_t c = cost | 1u, lz = __clz(c);
+    const uint32_t frac = (lz < 30u) ? ((c << (lz + 1u)) >> 30) : 0u;
+    const int key = (int)(31u - lz) * 4 + (int)frac;
+    const int k = 95 - key;
+    return (uint32_t)(k < 0 ? 0 : (k > 63 ? 63 : k));
+}
+// the class's representative cost (the low end of its range)
+__device__ __forceinline__ float class_cost(uint32_t k) { return exp2f((float)(95 - (int)k) * 0.25f); }
+// qw: class counts, class starts, fill cursors (kQBands x kQClasses each),
+// per band {start, live, background, items}, per band heavy count
 __global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__restrict__ off,
                                                           const uint32_t *__restrict__ gstat,
                                                           uint32_t ntiles, uint32_t tiles_x,
                                                           uint32_t tiles_y, uint32_t row0,
                                                           uint32_t band_h, uint32_t band_step,
                                                           uint32_t th, uint32_t bins_x, uint32_t lpt,
+                                                          const uint32_t *__restrict__ cost,
                                                           uint16_t *__restrict__ cls,
                                                           uint32_t *__restrict__ qw) {
     // class counts aggregated per block in LDS: one global atomic per class
@@ -1127,21 +1150,23 @@ __global__ void __launch_bounds__(kThreads) k_queue_class(const uint32_t *__rest
         const uint32_t g = *gstat, gn = g == kBinsUnusable ? 1u : g;
         const uint32_t len = off[b + 1] - off[b] + gn;
         const uint32_t band = (uint32_t)(((uint64_t)(t / tiles_x) * kQBands) / tiles_y);
-        const uint32_t k = band * kQClasses + (len ? (lpt ? (uint32_t)__clz(len) : 0u) : kQClasses - 1);
+        const uint32_t lc = !lpt ? 0u : (cost ? cost_class(cost[b]) : (uint32_t)__clz(len));
+        const uint32_t k = band * kQClasses + (len ? lc : kQClasses - 1);
         cls[t] = (uint16_t)k;
         atomicAdd(&hist[k], 1u);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < kQBands * kQClasses; k += kThreads)
-        if (hist[k]) atomicAdd(qw + k, hist[k]);
+        if (hist[k]) atomicAdd(qw + kQCount + k, hist[k]);
 }
-__global__ void __launch_bounds__(kThreads) k_queue_scan(uint32_t *__restrict__ qw) {
+__global__ void __launch_bounds__(kThreads) k_queue_scan(uint32_t *__restrict__ qw, uint32_t heavy) {
     // one block: the counts to LDS in one parallel load, band totals and
     // starts from LDS, then each band's class starts (a serial chain of
     // global loads took 19 us)
     __shared__ uint32_t c[kQBands * kQClasses], bstart[kQBands + 1];
+    __shared__ uint32_t hthr;
     const uint32_t t = threadIdx.x;
-    for (uint32_t k = t; k < kQBands * kQClasses; k += kThreads) c[k] = qw[k];
+    for (uint32_t k = t; k < kQBands * kQClasses; k += kThreads) c[k] = qw[kQCount + k];
     __syncthreads();
     if (t == 0) {
         uint32_t acc = 0;
@@ -1150,22 +1175,39 @@ __global__ void __launch_bounds__(kThreads) k_queue_scan(uint32_t *__restrict__ 
             for (uint32_t k = 0; k < kQClasses; ++k) acc += c[b * kQClasses + k];
         }
         bstart[kQBands] = acc;
+        // heavy tiles (measured costs only): classes whose cost reaches
+        // kHeavyFactor x the mean live cost
+        uint32_t thr = 0;
+        if (heavy) {
+            float n = 0.f, sum = 0.f;
+            for (uint32_t k = 0; k + 1 < kQClasses; ++k) {
+                float m = 0.f;
+                for (uint32_t b = 0; b < kQBands; ++b) m += (float)c[b * kQClasses + k];
+                n += m;
+                sum += m * class_cost(k);
+            }
+            const float lim = n > 0.f ? (float)kHeavyFactor * sum / n : 0.f;
+            while (thr + 1 < kQClasses && class_cost(thr) >= lim) ++thr;   // classes [0, thr) are heavy
+        }
+        hthr = thr;
     }
     __syncthreads();
     if (t < kQBands) {
         const uint32_t b = t, start = bstart[b];
-        uint32_t acc = start;
+        uint32_t acc = start, hv = 0;
         for (uint32_t k = 0; k < kQClasses; ++k) {
-            qw[288 + b * kQClasses + k] = acc;
-            qw[576 + b * kQClasses + k] = 0;
+            qw[kQStart + b * kQClasses + k] = acc;
+            qw[kQCur + b * kQClasses + k] = 0;
             acc += c[b * kQClasses + k];
+            if (k < hthr) hv += c[b * kQClasses + k];
         }
         const uint32_t bg = c[b * kQClasses + kQClasses - 1];
         const uint32_t live = acc - start - bg;
-        qw[896 + 4 * b] = start;
-        qw[896 + 4 * b + 1] = live;
-        qw[896 + 4 * b + 2] = bg;
-        qw[896 + 4 * b + 3] = live + (bg + 63u) / 64u;
+        qw[kQHdr + 4 * b] = start;
+        qw[kQHdr + 4 * b + 1] = live;
+        qw[kQHdr + 4 * b + 2] = bg;
+        qw[kQHdr + 4 * b + 3] = live + (bg + 63u) / 64u;
+        qw[kQHeavy + b] = hv;
     }
 }
 __global__ void __launch_bounds__(kThreads) k_queue_fill(const uint16_t *__restrict__ cls, uint32_t ntiles,
@@ -1184,7 +1226,7 @@ __global__ void __launch_bounds__(kThreads) k_queue_fill(const uint16_t *__restr
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < kQBands * kQClasses; j += kThreads)
-        if (hist[j]) base[j] = qw[288 + j] + atomicAdd(qw + 576 + j, hist[j]);
+        if (hist[j]) base[j] = qw[kQStart + j] + atomicAdd(qw + kQCur + j, hist[j]);
     __syncthreads();
     if (t < ntiles) queue[base[k] + r] = t;
 }
@@ -1320,18 +1362,21 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
     return (int)hipGetLastError();
 }
 
-size_t bin_queue_bytes(uint32_t ntiles) { return ((size_t)ntiles * 6 + 1024 * 4 + 255) & ~(size_t)255; }
+size_t bin_queue_bytes(uint32_t ntiles) {
+    return ((size_t)ntiles * 6 + kQWords * 4 + 255) & ~(size_t)255;
+}
 
 int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
                      uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
-                     uint32_t **queue, uint32_t **qhdr, void *stream) {
+                     uint32_t **queue, uint32_t **qhdr, void *stream, const uint32_t *cost, uint32_t **qheavy) {
     const hipStream_t st = (hipStream_t)stream;
     uint32_t *qw = reinterpret_cast<uint32_t *>(mem);
-    uint32_t *q = qw + 1024;
+    uint32_t *q = qw + kQWords;
     uint16_t *cls = reinterpret_cast<uint16_t *>(q + ntiles);
     *queue = q;
-    *qhdr = qw + 896;
-    hipError_t e = hipMemsetAsync(qw, 0, 1024 * sizeof(uint32_t), st);
+    *qhdr = qw + kQHdr;
+    if (qheavy) *qheavy = qw + kQHeavy;
+    hipError_t e = hipMemsetAsync(qw, 0, kQWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     const uint32_t tiles_y = tiles_x ? (ntiles + tiles_x - 1) / tiles_x : 0;
     // BIH_QUEUE_LPT=0: live tiles in tile order (A/B)
@@ -1342,9 +1387,9 @@ int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x
     if (ntiles > 0) {
         const dim3 g((ntiles + kThreads - 1) / kThreads);
         hipLaunchKernelGGL(k_queue_class, g, dim3(kThreads), 0, st, off, gstat, ntiles, tiles_x, tiles_y, row0,
-                           band_h, band_step, th, bins_x, lpt, cls, qw);
+                           band_h, band_step, th, bins_x, lpt, cost, cls, qw);
     }
-    hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(kThreads), 0, st, qw);
+    hipLaunchKernelGGL(k_queue_scan, dim3(1), dim3(kThreads), 0, st, qw, (cost && lpt) ? 1u : 0u);
     if (ntiles > 0)
         hipLaunchKernelGGL(k_queue_fill, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0, st, cls,
                            ntiles, qw, q);

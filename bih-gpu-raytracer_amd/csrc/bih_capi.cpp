@@ -93,6 +93,11 @@ struct CamSet {
     bool q_valid = false;
     uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t *q_list = nullptr, *q_hdr = nullptr;
+    bool q_cost = false;             // the queue is ordered by measured tile costs (launch_bin_queue's cost)
+    // the last launch that measured tile costs (bins.cost) was over q_key ==
+    // cost_key: the next queue of those rows is built from them
+    bool cost_known = false;
+    uint32_t cost_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
 };
 
@@ -159,7 +164,6 @@ struct bih_tree {
     // records.
     hipEvent_t ev_rng = nullptr;
     bool rng_pending = false;
-    bool rng_after_render = false;   // ev_rng follows the last render (it wrote the next state itself)
     // after the last (re)build of the tree: the per-camera builds order after
     // it (and after the renders that read their set), not after each other
     hipEvent_t ev_tree = nullptr;
@@ -416,10 +420,7 @@ int finish_build(bih_tree *tr) {
     hipError_t he = hipEventRecord(tr->ev_tree, tr->stream);
     if (he == hipSuccess && !had) he = hipEventRecord(tr->ev_rng, tr->stream);
     if (he != hipSuccess) return map_hip((int)he);
-    if (!had) {
-        tr->rng_pending = true;
-        tr->rng_after_render = false;
-    }
+    if (!had) tr->rng_pending = true;
     tr->tree_pending = true;
     return BIH_OK;
 }
@@ -825,13 +826,12 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
     return BIH_OK;
 }
 
-// The XORWOW advance inside k_render_bins (RenderArgs::rng_out) with
-// BIH_FUSED_ADVANCE=1 (experimental, A/B); default: the k_rng_advance launch
-// ahead of every render.
-static bool fused_advance_enabled() {
+// k_render_bins' queue in LPT order of measured tile costs (prepare_bin_queue)
+// unless BIH_COST_QUEUE=0 (A/B); it never changes a pixel.
+static bool cost_queue_enabled() {
     static const bool on = [] {
-        const char *e = getenv("BIH_FUSED_ADVANCE");
-        return e && strcmp(e, "1") == 0;
+        const char *e = getenv("BIH_COST_QUEUE");
+        return !(e && strcmp(e, "0") == 0);
     }();
     return on;
 }
@@ -902,14 +902,14 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
                  s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
                  s_bpart = al(bih::scan_partials_words(nblk) * 4),
                  s_blkcnt = al((size_t)nblk * bih::kBinBlockTiles * 8),
-                 s_pbase = al((size_t)nblk * 4);
+                 s_pbase = al((size_t)nblk * 4), s_cost = al(nb * 4);
     // pair results (k_bin_count -> k_bin_fill): 4 B per (triangle, tile)
     // pair; blocks past the buffer recompute in the fill
     uint32_t pres_cap = (uint32_t)std::min<uint64_t>(4ull * n + (1u << 20), 0x3FFFFFFFull);
     pres_cap = std::min<uint32_t>(pres_cap, tr->prm.pair_cap);   // tests: blocks past a small buffer recompute
     const size_t s_pres = al((size_t)pres_cap * 4);
     const size_t need = s_brect + s_cnt + s_cntq + s_cur + s_off + s_g + s_glist + s_part + s_rec + s_path + s_gent +
-                        s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt + s_pbase + s_pres;
+                        s_live + s_bmask + s_bcnt + s_boff + s_bpart + s_blkcnt + s_pbase + s_pres + s_cost;
     if (c.bins_mem_cap < need) {
         hipError_t e = hipStreamSynchronize(st);   // renders that read the old bins
         if (e != hipSuccess) return map_hip((int)e);
@@ -940,8 +940,10 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
     b.bpart = reinterpret_cast<uint32_t *>(p); p += s_bpart;
     b.blkcnt = reinterpret_cast<uint32_t *>(p); p += s_blkcnt;
     b.pbase = reinterpret_cast<uint32_t *>(p); p += s_pbase;
-    b.pres = reinterpret_cast<uint32_t *>(p);
+    b.pres = reinterpret_cast<uint32_t *>(p); p += s_pres;
     b.pres_cap = pres_cap;
+    b.cost = reinterpret_cast<uint32_t *>(p);
+    c.cost_known = false;   // the tiles' measured costs belong to the previous bins
     // the scans' look-back words (partials, bpart) must start at tag 0 (never
     // a call's tag) wherever this layout puts them: stale data there must not
     // pass for a published prefix.  Later calls leave older, unique tags.
@@ -1073,18 +1075,34 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     const uint32_t key[8] = {w, h, spp, rows.row0, rows.nrows, rows.band_h, rows.band_step, c.gen};
     int rc = ensure_qcount(tr);
     if (rc) return rc;
-    if (!c.q_valid || memcmp(key, c.q_key, sizeof key) != 0) {
+    // Queue order: the first launch over these rows (and bins) orders the
+    // tiles by list length and measures each live tile's cycles per frame
+    // (bins.cost); the next one rebuilds the queue in LPT order of those costs,
+    // with the heaviest tiles split over frame ranges (RenderArgs::hsplit) --
+    // once per camera and row set (BIH_COST_QUEUE=0: list length only, A/B).
+    // Only the order of the work changes, never a pixel.
+    const bool measured = cost_queue_enabled() && c.cost_known && memcmp(key, c.cost_key, sizeof key) == 0;
+    if (!c.q_valid || memcmp(key, c.q_key, sizeof key) != 0 || (measured && !c.q_cost)) {
+        // (after every render that reads the old queue -- and the one that
+        // measured the costs)
         rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
         rc = ensure_queue_mem(tr, c, ntiles);
         if (rc) return rc;
         int le = bih::launch_bin_queue(c.bins.off, c.bins.gcount + 1, c.bins.bins_x, tiles_x, ntiles, rows.row0,
                                        rows.band_h, rows.band_step, th, c.q_mem, &c.q_list, &c.q_hdr,
-                                       st);
+                                       st, measured ? c.bins.cost : nullptr);
         if (le) return map_hip(le);
         memcpy(c.q_key, key, sizeof key);
         c.q_valid = true;
+        c.q_cost = measured;
     }
+    if (!c.q_cost && !measured && cost_queue_enabled()) {
+        a.bin_cost = c.bins.cost;
+        memcpy(c.cost_key, key, sizeof key);
+        c.cost_known = true;
+    }
+    a.hsplit = c.q_cost && nframes >= 4 ? (nframes >= 8 ? 4u : 2u) : 1u;
     rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, nrec, 8);
     if (rc) return rc;
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
@@ -1317,20 +1335,11 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
         a.rng_split = split;
     }
-    // nsplit == 1 through the bins: the render writes the next call's state
-    // itself (RenderArgs::rng_out), so no k_rng_advance launch sits ahead of
-    // it; the next render then orders after this one (ev_rng below).  Split
-    // launches read stored split states, which the advance kernel makes.
-    const bool fused = use_bins && a.nsplit == 1 && fused_advance_enabled() && !hit_mask;
     if (hit_mask) {
         // the ring stays at this frame: the Whitted render of the same frame
         // draws the same jitter and advances it
         a.hit_mask = hit_mask;
         tr->next_frame = frame;
-    } else if (fused) {
-        a.rng_out = rng_buf(tr, nxt);
-        const uint32_t steps = 2 * spp * nframes;
-        a.adv_ppl = steps >= 256 ? 1u : steps >= 128 ? 2u : steps >= 64 ? 4u : 8u;
     } else {
         rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
                                              2 * spp * a.fpi, a.nsplit));
@@ -1349,6 +1358,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         a.bin_gstat = c.bins.gcount + 1;
         rc = prepare_bin_queue(tr, c, ci, w, h, spp, rows, slot, st, a, nframes);
         if (rc) return rc;
+        if (hit_mask && a.bin_cost) {   // (the mask pass's kernel does not measure)
+            a.bin_cost = nullptr;
+            c.cost_known = false;
+        }
     } else {
         // the cost order pays off for the long BIH walks; with the bins the
         // packets are short and the order's own launch costs more (A/B)
@@ -1382,13 +1395,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     }
     // the next render (on any stream) orders after the advance above, the
     // per-camera records, the shortcut boxes and the tile queue, which it
-    // reads as they stand now (a render that writes the next state itself:
-    // after the render, below)
-    if (!fused) {
-        e = hipEventRecord(tr->ev_rng, st);
-        if (e != hipSuccess) return map_hip((int)e);
-        tr->rng_pending = true;
-    }
+    // reads as they stand now
+    e = hipEventRecord(tr->ev_rng, st);
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->rng_pending = true;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;
@@ -1424,22 +1434,13 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // resident blocks so that the two overlap (bih_render.hip,
     // bins_grid_blocks); alone, it takes every slot
     // (a render queued on this same stream cannot overlap this one)
-    // (not behind a render that wrote this render's input state: this one
-    // starts after it ends)
-    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid && !tr->rng_after_render; ++k)
+    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid; ++k)
         if (k != slot && tr->used[k] && tr->slot_stream[k] != st && hipEventQuery(tr->evd[k]) == hipErrorNotReady)
             a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
     if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
-    if (fused) {
-        // the next render reads the state this one wrote
-        e = hipEventRecord(tr->ev_rng, st);
-        if (e != hipSuccess) return map_hip((int)e);
-        tr->rng_pending = true;
-    }
-    tr->rng_after_render = fused;
     if (tr->timing) {
         e = hipEventRecord(tr->ev2[slot], st);
         if (e != hipSuccess) return map_hip((int)e);
@@ -1656,7 +1657,6 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     hipError_t e = hipEventRecord(tr->ev_rng, st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->rng_pending = true;
-    tr->rng_after_render = false;
     bih::RenderArgs a;
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;

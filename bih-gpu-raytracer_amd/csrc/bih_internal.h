@@ -110,6 +110,11 @@ struct RenderArgs {
     // state (kBinSetWords, zero at launch: band heads, fallback count, per-CU
     // slots), plus the other set, which this launch zeroes for the slot's next one
     const uint32_t *bin_queue = nullptr;
+    // (nsplit == 1 launches, a queue ordered by measured cost) each band's
+    // first heavy tiles -- their count follows the band headers -- are taken
+    // as `hsplit` items each, over frame ranges; 1: no heavy items
+    uint32_t hsplit = 1;
+    uint32_t *bin_cost = nullptr;           // non-null: k_render_bins records each live tile's cycles per frame
     const uint32_t *bin_qhdr = nullptr;
     uint32_t *bin_heads = nullptr;
     uint32_t *bin_heads_next = nullptr;
@@ -128,14 +133,6 @@ struct RenderArgs {
     uint32_t fpi = 1;
     uint32_t nsplit = 1;
     const uint32_t *rng_split = nullptr;    // split s >= 1's start states at (s-1) * 5 planes (k_rng_advance)
-    // k_render_bins with nsplit == 1: the XORWOW state after the launch's
-    // frames (the next call's rng_in) written by the render itself -- live
-    // items store the state their frame loop ends with, and advance items
-    // (after each band's background items, adv_ppl pixels per lane) step the
-    // background pixels' states -- instead of a k_rng_advance launch ahead
-    // of the render.  null: the advance kernel ran.
-    uint32_t *rng_out = nullptr;
-    uint32_t adv_ppl = 1;
     // one-frame k_render_bins (config C4's primary rays): per local tile the
     // 64-bit mask of its samples that hit (lane = pixel * spp + sample), 0 for
     // background tiles; k_render_fallback writes the undecided packets'
@@ -177,6 +174,8 @@ struct BinBuffers {
     uint32_t *pres = nullptr;     // [pres_cap] per (triangle, tile) pair: k_bin_count's class / pixel mask / bucket
     uint32_t pres_cap = 0;
     uint32_t *pbase = nullptr;    // [blocks] each count block's base in pres (~0: none)
+    uint32_t *cost = nullptr;     // [nb] cycles per frame of each live tile's packet, written by
+                                  // k_render_bins launches that measure (RenderArgs::bin_cost)
 };
 
 // Device buffers of one tree.
@@ -288,10 +287,16 @@ int launch_bin_fill(uint32_t n, const BinCamera &c, const BinBuffers &b, float *
 // bands of tile rows: per band the live tiles by descending list length,
 // then the background tiles; qhdr (device) = per band {start, live,
 // background, items}.  mem: bin_queue_bytes(ntiles)
+// cost (optional): per bin the measured cycles per frame of its packet
+// (RenderArgs::bin_cost); with it the live tiles go in LPT order of their
+// measured cost (finer classes than the list length) and each band's tiles
+// costing over kHeavyFactor x the launch's mean come first and are counted in
+// *qheavy (k_render_bins splits them over frame ranges: RenderArgs::hsplit).
 size_t bin_queue_bytes(uint32_t ntiles);
 int launch_bin_queue(const uint32_t *off, const uint32_t *gstat, uint32_t bins_x, uint32_t tiles_x, uint32_t ntiles,
                      uint32_t row0, uint32_t band_h, uint32_t band_step, uint32_t th, void *mem,
-                     uint32_t **queue, uint32_t **qhdr, void *stream);
+                     uint32_t **queue, uint32_t **qhdr, void *stream, const uint32_t *cost = nullptr,
+                     uint32_t **qheavy = nullptr);
 // exclusive scan of n u32 (bih_build.hip); *total_dev = the sum
 int scan_exclusive(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
                    uint32_t *total_dev, void *stream);

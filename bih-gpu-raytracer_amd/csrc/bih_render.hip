@@ -1575,7 +1575,9 @@ __device__ __forceinline__ uint32_t pixels_of(unsigned long long m) {
     m = (m | (m >> 12)) & 0x000000FF000000FFull;
     return (uint32_t)((m | (m >> 24)) & 0xFFFFull);
 }
-template <bool PMASK>
+// COUNT: count the entries pre-tested and the intersector calls into fc_ent /
+// fc_mt (the work a launch that measures tile costs records)
+template <bool PMASK, bool COUNT = false>
 __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, const cprim_t *prims,
                                                       uint32_t bin, float uf, float vf, float dx,
                                                       float dy, float dz, unsigned long long live,
@@ -1644,8 +1646,10 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 const unsigned long long in =
                     rem & __ballot(!(f0 < 0.0f) && !(f1 < 0.0f) && !(f2 < 0.0f));
                 BIH_FC(++fc_ent);
+                if (COUNT && !BIH_FAST_COUNTERS) ++fc_ent;
                 if (!in) continue;
                 BIH_FC(++fc_mt);
+                if (COUNT && !BIH_FAST_COUNTERS) ++fc_mt;
                 const uint32_t ti = (a.dbg & 1024u) ? 0u : __builtin_amdgcn_readlane(__float_as_uint(d2.y), j);
                 const sf32x16 r = prim_rec(prims, ti);
                 const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
@@ -1926,9 +1930,13 @@ struct BinQueue {
     unsigned long long pending;        // a position claimed ahead (claim()), lane 0
     bool has_pending;
     uint32_t nf;                       // frames per launch: a band holds hb.w * nf items
-    uint32_t adv_tpi;                  // background tiles per advance item (0: none), after them
-    __device__ __forceinline__ uint32_t items(const uint4 &h) const {
-        return h.w * nf + (adv_tpi ? (h.z + adv_tpi - 1u) / adv_tpi : 0u);
+    // heavy tiles (RenderArgs::hsplit > 1): the band's first heavy[b] tiles
+    // take hs items each (frame ranges), so a band holds (hs - 1) * heavy[b]
+    // more; hv = the heavy count of the band of the item next() returned
+    // (the heavy counts follow the 8 band headers: launch_bin_queue's kQHeavy)
+    uint32_t hs, hv;
+    __device__ __forceinline__ uint32_t extra(uint32_t b) const {
+        return hs > 1u ? reinterpret_cast<const uint32_t *>(hdr + 8)[b] : 0u;
     }
 
     // Claims the slot position next() will use, so that its round trip
@@ -1955,7 +1963,8 @@ struct BinQueue {
             if (hi != 0 && lo < kBinBatch) {
                 const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch;
                 hb = hdr[b];
-                if (start + lo < items(hb)) {
+                hv = extra(b);
+                if (start + lo < hb.w * nf + (hs - 1u) * hv) {
                     item = start + lo;
                     band = b;
                     return true;
@@ -1965,13 +1974,15 @@ struct BinQueue {
             if ((hi == 0 && lo == 0) || (hi != 0 && lo == kBinBatch)) {
                 while (left) {
                     const uint4 h = hdr[band];
+                    const uint32_t x = extra(band);
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    if (c < items(h)) {
+                    if (c < h.w * nf + (hs - 1u) * x) {
                         if (lane == 0)
                             atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
                         hb = h;
+                        hv = x;
                         item = c;
                         return true;
                     }
@@ -1985,8 +1996,14 @@ struct BinQueue {
         }
     }
 };
-template <int LOG2SPP>
+// MODE 1: also write the per-tile hit masks (RenderArgs::hit_mask; the C4
+// primary pass); MODE 2: also record each live tile's cycles per frame
+// (RenderArgs::bin_cost; the launch after which the queue is ordered by
+// measured cost) -- separate instantiations, so the headline kernel keeps its
+// registers
+template <int LOG2SPP, int MODE = 0>
 __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const RenderArgs a) {
+    constexpr bool MASK = MODE == 1, COST = MODE == 2;
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -2012,8 +2029,9 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.left = 8;
     q.has_pending = false;
     q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
-    constexpr uint32_t PT = 64u >> LOG2SPP;   // pixels per tile
-    q.adv_tpi = a.rng_out ? (64u * a.adv_ppl) / PT : 0u;
+    q.hs = a.nsplit == 1u ? a.hsplit : 1u;
+    q.hv = 0;
+    const uint32_t fhv = (a.nframes + q.hs - 1u) / q.hs;   // frames per item of a heavy tile
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
     // timing experiment: items dealt round-robin over the waves (no atomics)
@@ -2058,65 +2076,28 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         // multi-frame launch: an item covers its tile in frames [f0, nf)
         const uint32_t fs = a.nsplit > 1 ? it / hb.w : 0u;
         it -= fs * hb.w;
-        const uint32_t f0 = fs * a.fpi;
-        const uint32_t nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
-        if (q.adv_tpi && it >= hb.w) {
-            // advance item: the XORWOW state of background pixels (no
-            // triangle can be hit there, so the render never draws their
-            // jitter) stepped over the launch's 2*SPP*nframes draws into
-            // rng_out, adv_ppl pixels per lane, loads issued together
-            const uint64_t P = (uint64_t)a.nrows * a.w;
-            const uint32_t k0 = (it - hb.w) * q.adv_tpi;
-            const uint32_t steps = 2u * SPP * a.nframes;
-            // two pixels per pass (both loads in flight; the walk's registers
-            // are dead here, but all eight at once took 148 VGPRs)
-#pragma unroll 1
-            for (uint32_t i = 0; i < a.adv_ppl; i += 2) {
-                uint32_t v[2][5];
-                uint64_t lpx[2];
-                bool ok[2];
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-                    const uint32_t p = (i + h) * 64u + lane, k = k0 + p / PT;
-                    ok[h] = false;
-                    lpx[h] = 0;
-                    if (i + h < a.adv_ppl && k < hb.z) {
-                        const uint32_t t = a.bin_queue[hb.x + hb.y + k];
-                        uint32_t x, lr, ss;
-                        ray_coords<LOG2SPP>((uint64_t)t * 64 + (p % PT) * SPP, tiles_x, x, lr, ss);
-                        ok[h] = x < a.w && lr < a.nrows;
-                        lpx[h] = (uint64_t)lr * a.w + x;
-                    }
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) v[h][j] = ok[h] ? a.rng_in[(uint64_t)j * P + lpx[h]] : 0u;
-                }
-#pragma unroll 4
-                for (uint32_t k = 0; k < steps; ++k) {
-#pragma unroll
-                    for (uint32_t h = 0; h < 2; ++h) {
-                        const uint32_t t = v[h][0] ^ (v[h][0] >> 2);
-                        v[h][0] = v[h][1]; v[h][1] = v[h][2]; v[h][2] = v[h][3]; v[h][3] = v[h][4];
-                        v[h][4] = (v[h][4] ^ (v[h][4] << 4)) ^ (t ^ (t << 1));
-                    }
-                }
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h)
-                    if (ok[h]) {
-#pragma unroll
-                        for (int j = 0; j < 5; ++j) a.rng_out[(uint64_t)j * P + lpx[h]] = v[h][j];
-                    }
+        uint32_t f0 = fs * a.fpi;
+        uint32_t nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
+        if (q.hv) {
+            // the band's first hv tiles (measured cost >= kHeavyFactor x the
+            // mean): hs items each, frames [sp * fhv, (sp + 1) * fhv), so that
+            // no tile's frames run for most of the launch on one wave
+            const uint32_t hx = q.hv * q.hs;
+            if (it < hx) {
+                const uint32_t j = it / q.hs, sp = it - j * q.hs;
+                it = j;
+                f0 = sp * fhv;
+                nf = f0 + fhv < a.nframes ? f0 + fhv : a.nframes;
+            } else {
+                it -= hx - q.hv;
             }
-#if BIH_BINS_TIMELINE
-            tl_rec(lane, 1u, tl_t0, __builtin_amdgcn_s_memrealtime(), 1u);
-#endif
-            continue;
         }
         if (it >= hb.y) {
             // background: every sample misses (Color's background), whatever its jitter
             const uint32_t k = (it - hb.y) * 64u + lane;
             if (k < hb.z && !(a.dbg & 1u)) {
                 const uint32_t t = a.bin_queue[hb.x + hb.y + k];
-                if (a.hit_mask) a.hit_mask[t] = 0ull;      // (one-frame launches)
+                if (MASK) a.hit_mask[t] = 0ull;      // (one-frame launches)
                 const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
                 const uint32_t x0 = tx * TW;
                 for (uint32_t fj = f0; fj < nf; ++fj) {
@@ -2155,12 +2136,33 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         uint32_t dfr = a.d_base + f0 * (2u * SPP * kWeyl);   // Weyl counter at the start of frame fj
         if (valid) {
             // frame f0's state: the launch's first frame's, or the split's
-            // start that k_rng_advance stored (f0 frames of 2*SPP draws on)
+            // start that k_rng_advance stored (f0 frames of 2*SPP draws on),
+            // or (a heavy tile's later frame range) the first frame's stepped
+            // 2*SPP*f0 draws on here
             const uint64_t P = (uint64_t)a.nrows * a.w;
             const uint32_t *src = fs ? a.rng_split + (uint64_t)(fs - 1) * 5 * P : a.rng_in;
+            uint32_t v[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) s_rs[i][tid] = src[(uint64_t)i * P + lp];
+            for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
+            const uint32_t pre = fs ? 0u : 2u * SPP * f0;
+#pragma unroll 4
+            for (uint32_t k = 0; k < pre; ++k) {
+                const uint32_t t = v[0] ^ (v[0] >> 2);
+                v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+                v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) s_rs[i][tid] = v[i];
         }
+        // (measuring launches) the item's work: entries pre-tested + 4 x
+        // intersector calls -- each call a dependent scalar load of the
+        // record, which is what makes a tile slow; wall time on a SIMD shared
+        // with five other waves orders the tiles worse
+        uint32_t work = 0;
+#if BIH_BINS_TIMELINE
+        uint32_t tl_ent = 0, tl_mt = 0, tl_pv = 0, tl_pl = 0;   // per item: entries, intersector calls, lanes
+                                                               // through the path table / a plan
+#endif
         for (uint32_t fj = f0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
             uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
             float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
@@ -2180,9 +2182,7 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                     if (k == 2u * s + 1u) xv = x;
                 }
                 const float ru = dev::xorwow_to_uniform(xu), rv = dev::xorwow_to_uniform(xv);
-                // (after the launch's last frame too when the render writes
-                // the next call's state: stored once the item is done)
-                if (fj + 1u < nf || a.rng_out) {
+                if (fj + 1u < nf) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
                 }
@@ -2200,8 +2200,15 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             const bool bins_ok = *a.bin_gstat != kBinsUnusable;
             if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
                 uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
-                const unsigned long long found = bin_walk<LOG2SPP == 2>(a, prims, bin, uf, vf, dx, dy, dz, live, lane,
-                                                                        cand, cmeta, cent, fc_ent, fc_mt, pf);
+                const unsigned long long found = bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
+                    a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand, cmeta, cent, fc_ent, fc_mt, pf);
+                if (COST) work += fc_ent + 4u * fc_mt;
+#if BIH_BINS_TIMELINE
+                tl_ent += fc_ent;
+                tl_mt += fc_mt;
+                tl_pv += (uint32_t)__popcll(__ballot(((found >> lane) & 1ull) && !(cand >> 31) && (cmeta & 3u) == 3u));
+                tl_pl += (uint32_t)__popcll(__ballot(((found >> lane) & 1ull) && !(cand >> 31) && (cmeta & 3u) != 3u));
+#endif
                 if (pf == 0x7f7f7f7fu && a.dbg == 0xdeadbeefu) a.out[0] = pf;   // (never: keeps the touches)
                 BIH_PH(3);
 #if BIH_SLAB_AGAIN
@@ -2261,19 +2268,14 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 const unsigned long long m = (SPP == 64) ? ~0ull : ((1ull << SPP) - 1ull);
                 fout[lp] = pixel_from_hits(__popcll((hits >> (pix * SPP)) & m), SPP);
             }
-            if (a.hit_mask && lane == 0) a.hit_mask[tile] = hits;
+            if (MASK && lane == 0) a.hit_mask[tile] = hits;
             BIH_PH(5);
         }
-        if (a.rng_out && valid && s == 0u) {
-            // the pixel's state after the launch's frames: the next call's
-            // input (cudaRender's write-back, CUDAKernels.cu:419)
-            const uint64_t P = (uint64_t)a.nrows * a.w;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) a.rng_out[(uint64_t)i * P + lp] = s_rs[i][tid];
-        }
+        if (COST && lane == 0) a.bin_cost[bin] = (work << 8) / (nf - f0);
 #if BIH_BINS_TIMELINE
         tl_rec(lane, 0u, tl_t0, __builtin_amdgcn_s_memrealtime(),
-               ((const uint32_t *)a.bin_off)[bin + 1] - ((const uint32_t *)a.bin_off)[bin]);
+               (((const uint32_t *)a.bin_off)[bin + 1] - ((const uint32_t *)a.bin_off)[bin]) | ((nf - f0) << 24));
+        tl_rec(lane, 4u, tl_ent, tl_ent + tl_mt, tl_pv | (tl_pl << 16));   // {ent, mt, pv | pl << 16}
 #endif
     }
 #if BIH_BINS_TIMELINE
@@ -3179,7 +3181,7 @@ uint32_t bins_grid_blocks(int device, uint32_t nframes) {
         int cus = 0, per = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, reinterpret_cast<const void *>(k_render_bins<2>), kThreads, 0);
+            &per, reinterpret_cast<const void *>(k_render_bins<2, 0>), kThreads, 0);
         if (cus <= 0) cus = 256;
         if (per <= 0) per = 1;
         int multi = BIH_BINS_MULTI_PER_CU < per ? BIH_BINS_MULTI_PER_CU : per;
@@ -3202,7 +3204,12 @@ static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t bloc
                               hipEvent_t k0, hipEvent_t k1) {
     hipError_t e = k0 ? hipEventRecord(k0, st) : hipSuccess;
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_render_bins<L>, dim3(blocks), dim3(kThreads), 0, st, a);
+    if (a.hit_mask)
+        hipLaunchKernelGGL((k_render_bins<L, 1>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else if (a.bin_cost)
+        hipLaunchKernelGGL((k_render_bins<L, 2>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_render_bins<L, 0>), dim3(blocks), dim3(kThreads), 0, st, a);
     e = k1 ? hipEventRecord(k1, st) : hipSuccess;
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_render_fallback<L>, dim3(fb_blocks), dim3(kThreads), 0, st, a);

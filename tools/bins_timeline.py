@@ -29,6 +29,21 @@ def blocks(path):
 
 
 def analyse(rec):
+    # kind 4 (item counters) follows its live item (kind 0) in the wave's run:
+    # pair them, then drop them from the time records
+    kind_all = rec[:, 0] >> 28
+    stats = {}
+    if (kind_all == 4).any():
+        idx4 = np.nonzero(kind_all == 4)[0]
+        prev = idx4 - 1
+        ok = (prev >= 0) & (kind_all[np.maximum(prev, 0)] == 0)
+        for i4, p in zip(idx4[ok], prev[ok]):
+            ent, mt = int(rec[i4, 1]), int((rec[i4, 2] - rec[i4, 1]) & 0xFFFFFFFF)
+            stats[int(p)] = (ent, mt, int(rec[i4, 3] & 0xFFFF), int(rec[i4, 3] >> 16))
+        keep = kind_all != 4
+        remap = np.cumsum(keep) - 1
+        stats = {int(remap[k]): v for k, v in stats.items()}
+        rec = rec[keep]
     wave = rec[:, 0] & 0xFFFFFF
     xcc = (rec[:, 0] >> 24) & 15
     kind = rec[:, 0] >> 28
@@ -36,7 +51,8 @@ def analyse(rec):
     t = (t - t[0] + (1 << 31)) % (1 << 32) - (1 << 31)    # unwrap relative to the first record
     t -= t.min()
     dur = rec[:, 2]
-    ln = rec[:, 3]
+    ln = rec[:, 3] & 0xFFFFFF             # live items: list length | frames << 24
+    frames = rec[:, 3] >> 24
     starts, exits = t[kind == 2], t[kind == 3]
     span = (exits.max() - starts.min()) / 100.0          # us
     items = kind <= 1
@@ -67,8 +83,31 @@ def analyse(rec):
     # the longest live items: start, duration, list length
     if live.any():
         idx = np.argsort(-dur[live])[:5]
-        ls, ld, ll = t[live][idx] / 100.0, dur[live][idx] / 100.0, ln[live][idx]
-        out["longest_live"] = [(round(float(a), 1), round(float(b), 1), int(c)) for a, b, c in zip(ls, ld, ll)]
+        ls, ld, ll, lf = t[live][idx] / 100.0, dur[live][idx] / 100.0, ln[live][idx], frames[live][idx]
+        out["longest_live (start us, us, list length, frames)"] = [
+            (round(float(a), 1), round(float(b), 1), int(c), int(f)) for a, b, c, f in zip(ls, ld, ll, lf)]
+        out["live_items_by_frames"] = {int(f): int((frames[live] == f).sum()) for f in np.unique(frames[live])}
+        if stats:
+            li = np.nonzero(live)[0]
+            order = li[np.argsort(-dur[li])]
+            rows = []
+            for k in order[:8]:
+                e, m, pv, pl = stats.get(int(k), (0, 0, 0, 0))
+                f = max(1, int(frames[k]))
+                rows.append((round(float(dur[k]) / 100.0 / f, 1), int(ln[k]), round(e / f, 1), round(m / f, 1),
+                             round(pv / f, 1), round(pl / f, 1)))
+            out["longest per frame (us, list, entries, mt, path-table lanes, plan lanes)"] = rows
+            # correlation of per-frame duration with each counter
+            d = np.array([dur[k] / 100.0 / max(1, frames[k]) for k in li if int(k) in stats])
+            cs = np.array([stats[int(k)] for k in li if int(k) in stats], dtype=float)
+            fr = np.array([max(1, frames[k]) for k in li if int(k) in stats], dtype=float)[:, None]
+            cs = cs / fr
+            if d.size > 10:
+                out["corr(us/frame; entries, mt, path, plan)"] = [round(float(np.corrcoef(d, cs[:, j])[0, 1]), 3)
+                                                                 for j in range(4)]
+                top = d >= np.quantile(d, 0.99)
+                out["mean per frame, top 1% vs all (entries, mt, path, plan)"] = [
+                    [round(float(x), 1) for x in cs[top].mean(0)], [round(float(x), 1) for x in cs.mean(0)]]
         # items that end in the last 10 % of the span
         late = (it_e > 0.9 * span) & (kind[items] == 0)
         out["live_items_ending_in_last_tenth"] = int(late.sum())
