@@ -1105,7 +1105,10 @@ constexpr uint32_t kQBands = 8, kQClasses = 65;   // live classes 0..63 (costlie
 constexpr uint32_t kQCount = 0, kQStart = kQBands * kQClasses, kQCur = 2 * kQBands * kQClasses,
                    kQHdr = 3 * kQBands * kQClasses, kQHeavy = kQHdr + 4 * kQBands, kQWords = 2048;
 static_assert(kQHeavy + kQBands <= kQWords, "queue words");
-constexpr uint32_t kHeavyFactor = 2;
+#ifndef BIH_HEAVY_FACTOR
+#define BIH_HEAVY_FACTOR 2.0f
+#endif
+constexpr float kHeavyFactor = BIH_HEAVY_FACTOR;
 __device__ __forceinline__ uint32_t queue_bin(uint32_t t, uint32_t tiles_x, uint32_t row0,
                                               uint32_t band_h, uint32_t band_step, uint32_t th,
                                               uint32_t bins_x) {
@@ -1186,7 +1189,7 @@ __global__ void __launch_bounds__(kThreads) k_queue_scan(uint32_t *__restrict__ 
                 n += m;
                 sum += m * class_cost(k);
             }
-            const float lim = n > 0.f ? (float)kHeavyFactor * sum / n : 0.f;
+            const float lim = n > 0.f ? kHeavyFactor * sum / n : 0.f;
             while (thr + 1 < kQClasses && class_cost(thr) >= lim) ++thr;   // classes [0, thr) are heavy
         }
         hthr = thr;

@@ -1551,6 +1551,9 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #ifndef BIH_BIN_SETBITS
 #define BIH_BIN_SETBITS 1   // 0: the per-entry mask check (v_readlane + scalar test per entry)
 #endif
+#ifndef BIH_REC_LDS
+#define BIH_REC_LDS 0   // multi-frame items: the records of the tile's first 64 entries in LDS
+#endif
 #ifndef BIH_REC_PREFETCH
 #define BIH_REC_PREFETCH 0   // 1: neutral to slightly slower (0.0964 vs 0.094 ms/frame)
 #endif
@@ -1583,10 +1586,12 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                                                       float dy, float dz, unsigned long long live,
                                                       uint32_t lane, uint32_t &cand, uint32_t &cmeta,
                                                       uint32_t &cent, uint32_t &fc_ent,
-                                                      uint32_t &fc_mt, uint32_t &pf) {
+                                                      uint32_t &fc_mt, uint32_t &pf,
+                                                      const float4 *lrec = nullptr, uint32_t lrec_n = 0) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
     const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
+    const uint32_t e_first = e;
     unsigned long long rem = live;
     const unsigned long long me = lane_bit(lane);
     // spp 4: an entry whose pixel mask (word 11 >> 16, bih_bins.hip
@@ -1651,7 +1656,27 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 BIH_FC(++fc_mt);
                 if (COUNT && !BIH_FAST_COUNTERS) ++fc_mt;
                 const uint32_t ti = (a.dbg & 1024u) ? 0u : __builtin_amdgcn_readlane(__float_as_uint(d2.y), j);
-                const sf32x16 r = prim_rec(prims, ti);
+                sf32x16 r;
+                const uint32_t rel = e + j - e_first;          // (part 0: the tile's list)
+                if (BIH_REC_LDS && part == 0 && rel < lrec_n) {
+                    // the item's copy of the record in LDS (bin_rec_fill): an
+                    // LDS round trip instead of a scalar load from L2/MALL
+                    // one 16-byte read at a time straight into SGPRs (four
+                    // VGPRs live, not 13: the walk is at its register peak)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float4 q = lrec[4 * rel + k];
+                        r[4 * k] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.x)));
+                        if (k < 3) {
+                            r[4 * k + 1] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.y)));
+                            r[4 * k + 2] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.z)));
+                            r[4 * k + 3] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(q.w)));
+                        }
+                        asm volatile("" ::: "memory");
+                    }
+                } else {
+                    r = prim_rec(prims, ti);
+                }
                 const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
                 if (h & me) {
                     cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
@@ -1938,6 +1963,17 @@ struct BinQueue {
     __device__ __forceinline__ uint32_t extra(uint32_t b) const {
         return hs > 1u ? reinterpret_cast<const uint32_t *>(hdr + 8)[b] : 0u;
     }
+    // Start-up without atomics: each wave's first item is static -- block
+    // k's waves take items (k >> 3) * 4 + w of band k & 7 (blocks are dealt
+    // round-robin over the XCDs, so that is mostly the XCD's own band; only
+    // the speed depends on it) -- and the band heads hand out the items after
+    // those: stat(b) per band.  (Every wave starting in the per-CU slot made
+    // the 24 waves of a CU wait for three serial refills: 5.6 us median to a
+    // wave's first item in a one-frame launch, 12 us at q90.)
+    bool first;
+    __device__ __forceinline__ uint32_t stat(uint32_t b) const {
+        return gridDim.x > b ? ((gridDim.x - b + 7u) >> 3) * (kThreads / 64) : 0u;
+    }
 
     // Claims the slot position next() will use, so that its round trip
     // overlaps the current item's loads (BIH_QUEUE_AHEAD).
@@ -1949,6 +1985,19 @@ struct BinQueue {
 
     // next item: band (this->hb / band) and index within the band
     __device__ bool next(uint32_t lane, uint32_t &item) {
+        if (first) {
+            first = false;
+            const uint32_t b = blockIdx.x & 7u;
+            const uint32_t idx = (blockIdx.x >> 3) * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const uint4 h = hdr[b];
+            const uint32_t x = extra(b);
+            if (idx < h.w * nf + (hs - 1u) * x) {
+                hb = h;
+                hv = x;
+                item = idx;
+                return true;
+            }
+        }
         for (;;) {
             unsigned long long v = 0;
             if (has_pending) {
@@ -1961,7 +2010,7 @@ struct BinQueue {
             const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
             if (hi == 0xFFFFFFFFu) return false;
             if (hi != 0 && lo < kBinBatch) {
-                const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch;
+                const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch + stat(b);
                 hb = hdr[b];
                 hv = extra(b);
                 if (start + lo < hb.w * nf + (hs - 1u) * hv) {
@@ -1978,12 +2027,12 @@ struct BinQueue {
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    if (c < h.w * nf + (hs - 1u) * x) {
+                    if (c + stat(band) < h.w * nf + (hs - 1u) * x) {
                         if (lane == 0)
                             atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
                         hb = h;
                         hv = x;
-                        item = c;
+                        item = c + stat(band);
                         return true;
                     }
                     band = (band + 1u) & 7u;
@@ -2008,6 +2057,16 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     __shared__ uint32_t s_rs[5][kThreads];   // each lane's XORWOW state between the frames of an item
+#if BIH_REC_LDS
+    // per wave: the intersector records (tri_prim, 13 of 16 words) of its
+    // item's first 64 list entries, loaded once and read by every frame of
+    // the item (a multi-frame item walks the same list each frame; each
+    // record's scalar load was a dependent round trip to L2/MALL per frame)
+    __shared__ float4 s_rec[kThreads / 64][64 * 4];
+    const float4 *lrec = s_rec[tid >> 6];
+#else
+    const float4 *lrec = nullptr;
+#endif
     // the slot's next launch starts from a zeroed set: every one of the 1024
     // per-CU slot lines (cu_key() spans 0..1023 sparsely, whatever the grid)
     if (tid == 0)
@@ -2027,6 +2086,10 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     q.slot = reinterpret_cast<unsigned long long *>(a.bin_heads + kBinSlot0 + cu_key() * 32);
     q.band = xcc_id();
     q.left = 8;
+    // (not while another render holds CU slots: this launch's blocks then
+    // start as that one's waves exit, and a late block's static item -- the
+    // band's costliest first -- would start late)
+    q.first = a.shared_grid == 0u;
     q.has_pending = false;
     q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
     q.hs = a.nsplit == 1u ? a.hsplit : 1u;
@@ -2154,6 +2217,29 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
 #pragma unroll
             for (int i = 0; i < 5; ++i) s_rs[i][tid] = v[i];
         }
+        uint32_t lrec_n = 0;
+#if BIH_REC_LDS
+        if (nf - f0 >= 2u) {
+            const uint32_t e0 = ((const uint32_t *)a.bin_off)[bin];
+            const uint32_t len = ((const uint32_t *)a.bin_off)[bin + 1] - e0;
+            lrec_n = len < 64u ? len : 64u;
+            if (lane < lrec_n) {
+                const uint32_t ti = __float_as_uint(
+                    reinterpret_cast<const float4 *>(a.bin_list)[(uint64_t)kBinEntryF4 * (e0 + lane) + 2].y);
+                const float4 *src = reinterpret_cast<const float4 *>(a.tri_prim) + 4ull * ti;
+                const float4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
+                float4 *dst = s_rec[tid >> 6] + 4 * lane;
+                dst[0] = q0;
+                dst[1] = q1;
+                dst[2] = q2;
+                dst[3] = q3;
+            }
+            // the wave's own LDS writes before its reads (lanes read other lanes' slots)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#endif
         // (measuring launches) the item's work: entries pre-tested + 4 x
         // intersector calls -- each call a dependent scalar load of the
         // record, which is what makes a tile slow; wall time on a SIMD shared
@@ -2201,7 +2287,8 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
                 uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
                 const unsigned long long found = bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
-                    a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand, cmeta, cent, fc_ent, fc_mt, pf);
+                    a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand, cmeta, cent, fc_ent, fc_mt, pf, lrec,
+                    lrec_n);
                 if (COST) work += fc_ent + 4u * fc_mt;
 #if BIH_BINS_TIMELINE
                 tl_ent += fc_ent;

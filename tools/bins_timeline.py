@@ -38,7 +38,7 @@ def analyse(rec):
         prev = idx4 - 1
         ok = (prev >= 0) & (kind_all[np.maximum(prev, 0)] == 0)
         for i4, p in zip(idx4[ok], prev[ok]):
-            ent, mt = int(rec[i4, 1]), int((rec[i4, 2] - rec[i4, 1]) & 0xFFFFFFFF)
+            ent, mt = int(rec[i4, 1]), int(rec[i4, 2])
             stats[int(p)] = (ent, mt, int(rec[i4, 3] & 0xFFFF), int(rec[i4, 3] >> 16))
         keep = kind_all != 4
         remap = np.cumsum(keep) - 1
@@ -68,8 +68,21 @@ def analyse(rec):
         prof.append(ov / (nwaves * (b - a)))
     d_live = dur[live] / 100.0
     q = lambda v, f: float(np.quantile(v, f)) if v.size else 0.0
+    # per wave: its start (kind 2) and its first item's start (the queue's
+    # start-up cost), its last item's end and its exit
+    first_item, wstart = {}, {}
+    for w_, k_, t_ in zip(wave.tolist(), kind.tolist(), t.tolist()):
+        if k_ == 2:
+            wstart[w_] = t_
+        elif k_ <= 1 and w_ not in first_item:
+            first_item[w_] = t_
+    gaps = np.array([first_item[w_] - wstart[w_] for w_ in first_item if w_ in wstart]) / 100.0
+    ws = np.array(list(wstart.values())) / 100.0
     out = {
-        "span_us": span, "waves": nwaves, "items_live": int(live.sum()), "items_bg": int(bg.sum()),
+        "span_us": span, "waves": nwaves,
+        "wave_start_us_q50_q90_max": [float(np.quantile(ws, .5)), float(np.quantile(ws, .9)), float(ws.max())]
+        if ws.size else None,
+        "start_to_first_item_us_q10_q50_q90": [float(np.quantile(gaps, f)) for f in (.1, .5, .9)] if gaps.size else None, "items_live": int(live.sum()), "items_bg": int(bg.sum()),
         "utilisation": busy / (nwaves * span),
         "queue_dry_us": float(last_start), "tail_us": span - float(last_start),
         "wave_exit_q10_q50_q90_us": [q(exits / 100.0, 0.1), q(exits / 100.0, 0.5), q(exits / 100.0, 0.9)],

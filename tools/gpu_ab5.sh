@@ -1,0 +1,21 @@
+# A/B of library variants on the driver's bench command (legs: one-frame,
+# camera, rebuild, band share, C2): bash tools/gpu_ab5.sh TAG ROUNDS VARIANT... (base = the in-tree library)
+set -u
+T=$1; N=$2; shift 2
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$T
+mkdir -p $O
+cd $R
+V=$R/bih-gpu-raytracer_amd/lib/variants
+for k in $(seq 1 $N); do
+  for X in "$@"; do
+    L=""; [ $X != base ] && L=$V/libbih_amd_$X.so
+    BIH_LIB=$L timeout -k 10 300 python -u bench.py --c5 0 --whitted-frames 0 --cpu-baseline 0 --traffic 0 \
+        --no-reference-leg > $O/bench_${X}_$k.json 2> $O/bench_${X}_$k.err || { tail -20 $O/bench_${X}_$k.err; exit 1; }
+    python3 -c "
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], 'head %.4f' % d['ms_per_step'], 'launch %.4f' % (d['roofline']['launch_ms']/16), 'one %.4f' % d['one_in_flight']['ms_per_step'], 'cam %.4f' % d['moving_camera']['ms_per_step'], 'rb %.4f' % d['with_rebuild']['ms_per_step'], 'share %.3f' % d['band_share']['projected_efficiency'], 'c2 %.4f' % d['c2_torus']['ms_per_step'])
+" $O/bench_${X}_$k.json $X | tee -a $O/ab.txt
+  done
+done
