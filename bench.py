@@ -500,6 +500,25 @@ def main():
         W5, H5 = 3840, 2160
         w5 = Workload(C, t5, W5, H5, shapes=shapes)
         el5, _, fps5 = w5.timed(mode, bihrt.TRAVERSE_ANYHIT, 0)
+        # N = 1: each of the --share-world ranks' interleaved bands of C5's
+        # frame alone (C5 is "row-tiled across 8 x MI355X"; north_star), as
+        # band_share does for the headline: projected per-GPU efficiency
+        share5 = None
+        if world == 1 and Q > 1:
+            for q in range(Q):
+                w5.arrays.reserve(W5, H5, SPP, tiling.band_rows(H5, args.band, q, Q), G)
+            elf5, _, _ = w5.timed("weak", bihrt.TRAVERSE_ANYHIT, 7000)
+            full5 = 1e3 * elf5 / args.steps
+            sh5 = []
+            for q in range(Q):
+                els, _, _ = w5.timed("weak", bihrt.TRAVERSE_ANYHIT, 8000 + 1000 * q,
+                                     rows=tiling.band_rows(H5, args.band, q, Q))
+                sh5.append(1e3 * els / args.steps)
+            share5 = {"world": Q, "band": args.band, "share_ms_per_step": sh5, "full_frame_ms_per_step": full5,
+                      "projected_efficiency": full5 / (Q * max(sh5)),
+                      "note": f"each of the {Q} ranks' interleaved {args.band}-row bands of the 3840x2160 frame "
+                              f"rendered alone on this GPU, {G} frames per call, as the full frame timed beside "
+                              "it; excludes the gather"}
         w5.arrays.rebuild()
         torch.cuda.synchronize()
         b5 = w5.arrays.info().build_ms
@@ -511,6 +530,7 @@ def main():
                   "parallelism": parallelism(mode, args.band, world),
                   "build_ms": w5.info.build_ms, "rebuild_ms": b5,
                   "bins": {"usable": bool(st5.usable), "list_entries": int(st5.list_entries)},
+                  "band_share": share5,
                   "note": "parity: tests/test_gpu_parity.py::test_10m_4k_* (oracle rows, exact walk)"}
         w5.close()
         del w5, t5
@@ -619,7 +639,7 @@ def main():
     # so the isolated launches give the duration (what rocprofv3 reports for
     # `--headline-only --in-flight 1`)
     launch_ms = kernel_launch_ms if kernel_launch_ms else (serial_leg["kernel_ms"] if serial_leg else kernel_ms)
-    work_gbs = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9
+    work_gbs = b_ray * launch_rays / (launch_ms * 1e-3) / 1e9 if launch_ms else None
     achieved = traffic["bytes_per_launch"] / (launch_ms * 1e-3) / 1e9 if traffic else None
 
     bst = arrays.bins_stats()

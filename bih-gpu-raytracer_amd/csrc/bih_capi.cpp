@@ -185,6 +185,16 @@ struct bih_tree {
     uint32_t key_w = 0, key_spp = 0, key_row0 = 0, key_nrows = 0, key_bh = 0, key_bs = 0;
     uint64_t key_seed = 0;
     uint32_t next_frame = 0;
+    // stamped XORWOW state (RenderArgs::stamps): frustum-bin launches on one
+    // stream read and write per-tile state in ring buffers st_a and st_a + 1,
+    // no k_rng_advance; any other consumer leaves the mode (prepare_rng)
+    unsigned long long *stamps = nullptr;
+    size_t stamp_cap = 0;            // tiles
+    bool stamped = false;
+    int st_a = 0;
+    uint32_t st_seq = 0;             // the last launch's sequence number (1 .. 1023)
+    uint32_t st_sync = 0;            // frame of the last k_rng_sync / k_stamp_init
+    uint32_t stream_run = 0;         // renders in a row on the last render's stream
     bool owns_stream = false;
     uint32_t *work = nullptr;        // persistent-kernel tile counters, kWorkWords per slot
     uint32_t *spill = nullptr;       // traversal stack spill area, spill_words per slot
@@ -204,8 +214,6 @@ struct bih_tree {
     // draws from set q_par[slot] and zeroes the other for the slot's next launch
     uint32_t *q_count = nullptr;
     uint32_t q_par[kSlots] = {};
-    uint32_t *rsplit = nullptr;      // per slot: XORWOW start states of a launch's later item splits
-    size_t rsplit_cap = 0;           // words per slot
     uint32_t *fb_mem = nullptr;      // per slot: fallback records of k_render_bins (8 words per tile)
     size_t fbq_cap = 0;              // tiles per slot
     // config C4 (bih_whitted.hip): two ray queues, counters and per-sample hits
@@ -607,7 +615,7 @@ void bih_free(bih_tree *tr) {
     }
     if (tr->q_count) (void)hipFree(tr->q_count);
     if (tr->fb_mem) (void)hipFree(tr->fb_mem);
-    if (tr->rsplit) (void)hipFree(tr->rsplit);
+    if (tr->stamps) (void)hipFree(tr->stamps);
     if (tr->wh_mem) (void)hipFree(tr->wh_mem);
     if (tr->wh_mask) (void)hipFree(tr->wh_mask);
     for (int k = 0; k < kSlots; ++k) {
@@ -665,8 +673,8 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
-                          (size_t)kSlots * tr->fbq_cap * 8 + (size_t)kSlots * tr->rsplit_cap) * 4 +
-                         (tr->wh_mem ? bih::whitted_bytes(tr->wh_rays) : 0) + tr->wh_mask_cap * 8;
+                          (size_t)kSlots * tr->fbq_cap * 8) * 4 +
+                         (tr->wh_mem ? bih::whitted_bytes(tr->wh_rays) : 0) + tr->wh_mask_cap * 8 + tr->stamp_cap * 8;
     info->build_ms = tr->build_ms;
     info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
     return BIH_OK;
@@ -727,6 +735,11 @@ static int drain_renders(bih_tree *tr) {
     return BIH_OK;
 }
 
+// The next render's stream waits for the state every render reads (ev_rng).
+static hipError_t wait_rng(bih_tree *tr, hipStream_t st) {
+    return tr->rng_pending ? hipStreamWaitEvent(st, tr->ev_rng, 0) : hipSuccess;
+}
+
 // The XORWOW ring (kRngBufs x 5 planes) and the per-slot accumulators for P
 // pixels; a new ring holds no state (the next render seeds it).
 static int ensure_rng(bih_tree *tr, size_t P, hipStream_t st) {
@@ -743,7 +756,58 @@ static int ensure_rng(bih_tree *tr, size_t P, hipStream_t st) {
     tr->rng_cap = P;
     tr->rng_cur = 0;
     tr->rng_valid = false;
+    tr->stamped = false;
     return BIH_OK;
+}
+
+// Stamped state (RenderArgs::stamps) unless BIH_STAMPED=0 (A/B); it never
+// changes a pixel.
+constexpr uint32_t kStampRun = 3;
+
+// k_render_bins' static queue rounds in one-frame launches (BinQueue;
+// BIH_STATIC_ROUNDS for A/B: one-frame calls 1 round 0.0824 ms, 2 0.0822,
+// 3 0.086, 5 0.106 -- a wave cannot hand on its later static items, r05n)
+static uint32_t static_rounds_one() {
+    static const uint32_t n = [] {
+        const char *e = getenv("BIH_STATIC_ROUNDS");
+        const int v = e ? atoi(e) : -1;
+        return v >= 0 && v <= 64 ? (uint32_t)v : 1u;
+    }();
+    return n;
+}
+
+// The render in `slot` was issued on `st` (before last_slot moves to it).
+static void note_stream(bih_tree *tr, int slot, hipStream_t st) {
+    const bool same = tr->last_slot >= 0 && tr->slot_stream[tr->last_slot] == st;
+    tr->stream_run = same ? tr->stream_run + 1 : 1;
+    tr->slot_stream[slot] = st;
+}
+
+static bool stamps_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("BIH_STAMPED");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+static int ensure_stamps(bih_tree *tr, size_t ntiles) {
+    if (tr->stamp_cap >= ntiles) return BIH_OK;
+    int rc = drain_renders(tr);
+    if (rc) return rc;
+    if (tr->stamps) (void)hipFree(tr->stamps);
+    tr->stamps = nullptr;
+    tr->stamp_cap = 0;
+    tr->stamped = false;
+    hipError_t e = tree_malloc(tr, &tr->stamps, ntiles * sizeof(unsigned long long));
+    if (e != hipSuccess) return map_hip((int)e);
+    tr->stamp_cap = ntiles;
+    return BIH_OK;
+}
+
+static uint32_t next_stamp_seq(bih_tree *tr) {
+    tr->st_seq = tr->st_seq % 1023u + 1u;
+    return tr->st_seq;
 }
 
 // The persistent render kernels' work words and stack spill areas.
@@ -786,19 +850,52 @@ struct RngGuard {
     bih_tree *tr;
     bool armed = true;
     ~RngGuard() {
-        if (armed) tr->rng_valid = false;
+        if (armed) {
+            tr->rng_valid = false;
+            tr->stamped = false;
+        }
     }
 };
+
+static bool rng_same_px(const bih_tree *tr, uint32_t w, uint32_t spp, uint64_t seed, const bih_rows &rows) {
+    return tr->rng_valid && tr->key_w == w && tr->key_spp == spp && tr->key_seed == seed &&
+           tr->key_row0 == rows.row0 && tr->key_nrows == rows.nrows && tr->key_bh == rows.band_h &&
+           tr->key_bs == rows.band_step;
+}
+
+// Leaves stamped mode: every pixel's state at next_frame into a ring buffer
+// of its own, which becomes rng_cur (after the stamped launches: they order
+// ev_rng, which every render waits on first).
+static int unstamp(bih_tree *tr, hipStream_t st) {
+    if (!tr->stamped) return BIH_OK;
+    tr->stamped = false;
+    const int c = (tr->st_a + 2) % kRngBufs;
+    tr->rng_cur = c;
+    const int e = bih::launch_rng_sync(tr->stamps, rng_buf(tr, tr->st_a), rng_buf(tr, (tr->st_a + 1) % kRngBufs),
+                                       rng_buf(tr, c), tr->key_w, tr->key_nrows, tr->key_spp, tr->next_frame,
+                                       0xFFFFu, tr->t.device, st);
+    if (e) tr->rng_valid = false;
+    return map_hip(e);
+}
 
 static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, uint64_t seed,
                        const bih_rows &rows, hipStream_t st) {
     const size_t P = (size_t)rows.nrows * w;
     int rc = ensure_rng(tr, P, st);
     if (rc) return rc;
-    const bool same_px = tr->rng_valid && tr->key_w == w && tr->key_spp == spp &&
-                         tr->key_seed == seed && tr->key_row0 == rows.row0 &&
-                         tr->key_nrows == rows.nrows && tr->key_bh == rows.band_h &&
-                         tr->key_bs == rows.band_step;
+    bool same_px = rng_same_px(tr, w, spp, seed, rows);
+    if (tr->stamped) {
+        // the stamped state back into the ring, or dropped (re-seeded below)
+        if (same_px && frame >= tr->next_frame) {
+            rc = unstamp(tr, st);
+            if (rc) return rc;
+        } else {
+            tr->stamped = false;
+            tr->rng_cur = (tr->st_a + 2) % kRngBufs;
+            tr->rng_valid = false;
+            same_px = false;
+        }
+    }
     const bool same = same_px && tr->next_frame == frame;
     if (same_px && frame > tr->next_frame && (uint64_t)(frame - tr->next_frame) * 2 * spp <= 4096) {
         // a short gap in the frame sequence: run the generators forward
@@ -1286,12 +1383,10 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         e = hipStreamWaitEvent(st, tr->evd[slot], 0);
         if (e != hipSuccess) return map_hip((int)e);
     }
-    if (tr->rng_pending) {
-        // (also after the structures of a camera an earlier render on
-        // another stream built, when this render reuses them)
-        e = hipStreamWaitEvent(st, tr->ev_rng, 0);
-        if (e != hipSuccess) return map_hip((int)e);
-    }
+    // (also after the structures of a camera an earlier render on another
+    // stream built, when this render reuses them)
+    e = wait_rng(tr, st);
+    if (e != hipSuccess) return map_hip((int)e);
     bih::RenderArgs a;
     bool use_bins = false;
     if (c.bins_usable && c.bins_valid && c.bins_key[0] == w && c.bins_key[1] == h &&
@@ -1302,16 +1397,66 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         use_bins = rows.row0 % th == 0 && rows.band_h % th == 0;
     }
     if ((nframes > 1 || hit_mask) && !use_bins) return kRenderPerFrame;
-    // the frame's per-pixel XORWOW state (InitRandGPU / the state earlier
-    // frames left), and the state cudaRender leaves behind for the frame
-    // after this launch's last (CUDAKernels.cu:419)
-    rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
-    if (rc) return rc;
+    const size_t P = (size_t)rows.nrows * w;
+    // stamped state (RenderArgs::stamps): a frustum-bin launch that follows
+    // kStampRun renders on its own stream reads and writes per-tile state and
+    // runs no k_rng_advance.  Stamped launches order after each other (ev_rng
+    // after the render), which would take away the overlap of frames issued
+    // on several streams: a render on another stream leaves the mode
+    // (prepare_rng), and renders alternating streams never enter it.
+    const bool same_stream = tr->last_slot >= 0 && tr->slot_stream[tr->last_slot] == st;
+    const bool stamp_ok = use_bins && !hit_mask && stamps_enabled() &&
+                          (uint64_t)frame + nframes <= bih::kStampFrameMax && same_stream &&
+                          (tr->stamped || tr->stream_run >= kStampRun);
+    const bool stamped = stamp_ok && tr->stamped && rng_same_px(tr, w, spp, seed, rows) && frame >= tr->next_frame &&
+                         (uint64_t)(frame - tr->next_frame) * 2 * spp <= 4096;
+    if (stamped) {
+        // bound the steps a tile's state lags behind (background tiles are
+        // not stepped): every kStampJumpFrames frames all tiles to the frame
+        // a whole number of those after the last sync (background tiles
+        // then jump by one table, k_rng_sync); a tile lags at most two runs
+        if (frame - tr->st_sync >= bih::kStampJumpFrames) {
+            const uint32_t T = frame - (frame - tr->st_sync) % bih::kStampJumpFrames;
+            rc = map_hip(bih::launch_rng_sync(tr->stamps, rng_buf(tr, tr->st_a), rng_buf(tr, (tr->st_a + 1) % kRngBufs),
+                                              nullptr, w, rows.nrows, spp, T, next_stamp_seq(tr), tr->t.device, st));
+            if (rc) {
+                tr->stamped = false;
+                tr->rng_valid = false;
+                return rc;
+            }
+            tr->st_sync = T;
+        }
+    } else {
+        // the frame's per-pixel XORWOW state (InitRandGPU / the state earlier
+        // frames left), and the state cudaRender leaves behind for the frame
+        // after this launch's last (CUDAKernels.cu:419)
+        rc = prepare_rng(tr, w, spp, frame, seed, rows, st);
+        if (rc) return rc;
+    }
     // next_frame now points past this launch while rng_cur still holds its
     // first frame's state: a failure before the launch is issued makes the
     // next call re-seed instead of rendering from stale state
     RngGuard rng_guard{tr};
-    const size_t P = (size_t)rows.nrows * w;
+    if (!stamped && stamp_ok) {
+        // into stamped mode: every tile at this frame in rng_cur; after every
+        // render in flight (they may read the ring buffers)
+        uint32_t tw = 0, th = 0;
+        tile_shape(spp, &tw, &th);
+        const size_t ntiles = (size_t)((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
+        rc = ensure_stamps(tr, ntiles);
+        if (rc) return rc;
+        for (int k = 0; k < kSlots; ++k)
+            if (tr->used[k]) {
+                e = hipStreamWaitEvent(st, tr->evd[k], 0);
+                if (e != hipSuccess) return map_hip((int)e);
+            }
+        rc = map_hip(bih::launch_stamp_init(tr->stamps, (uint32_t)ntiles, frame, st));
+        if (rc) return rc;
+        tr->stamped = true;
+        tr->st_a = tr->rng_cur;
+        tr->st_sync = frame;
+    }
+    const bool use_stamps = stamp_ok;   // (stamped mode from here on)
     const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
     a.nframes = nframes;
     a.out_stride = out_stride;
@@ -1325,24 +1470,28 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         a.fpi = nframes;
         a.nsplit = 1;
     }
-    // the launch's XORWOW state after its frames (the next launch's input),
-    // and the start states of the item splits after the first (rng_split,
-    // per slot: this render reads them, the slot's next one rewrites them)
-    uint32_t *split = nullptr;
-    if (a.nsplit > 1) {
-        rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(a.nsplit - 1) * 5 * P, 1);
-        if (rc) return rc;
-        split = tr->rsplit + (size_t)slot * tr->rsplit_cap;
-        a.rng_split = split;
+    // queue rounds dealt without atomics: one-frame items are short (~10 us),
+    // so a refill's round trip is a large part of each
+    a.static_rounds = nframes == 1 ? static_rounds_one() : 1u;
+    if (use_stamps) {
+        // (each item steps its tile's state to its first frame itself)
+        a.stamps = tr->stamps;
+        a.st_buf0 = rng_buf(tr, tr->st_a);
+        a.st_buf1 = rng_buf(tr, (tr->st_a + 1) % kRngBufs);
+        a.st_f0 = frame;
+        a.st_seq = next_stamp_seq(tr);
     }
     if (hit_mask) {
         // the ring stays at this frame: the Whitted render of the same frame
         // draws the same jitter and advances it
         a.hit_mask = hit_mask;
         tr->next_frame = frame;
-    } else {
-        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st, split,
-                                             2 * spp * a.fpi, a.nsplit));
+    } else if (!use_stamps) {
+        // the state after this launch's frames (the next launch's input;
+        // the render reads rng_cur only).  (On a stream of its own beside the
+        // render, the next render's wait across queues cost more than the
+        // advance: one-frame calls 0.107 against 0.087 ms, r05m.)
+        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st));
         if (rc) return rc;
     }
     if (!hit_mask) tr->next_frame = frame + nframes;
@@ -1396,9 +1545,12 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // the next render (on any stream) orders after the advance above, the
     // per-camera records, the shortcut boxes and the tile queue, which it
     // reads as they stand now
-    e = hipEventRecord(tr->ev_rng, st);
-    if (e != hipSuccess) return map_hip((int)e);
-    tr->rng_pending = true;
+    // (stamped: after the render instead -- the next launch reads its stamps)
+    if (!use_stamps) {
+        e = hipEventRecord(tr->ev_rng, st);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->rng_pending = true;
+    }
     memcpy(a.cam, cam, sizeof a.cam);
     a.w = w;
     a.h = h;
@@ -1434,13 +1586,18 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     // resident blocks so that the two overlap (bih_render.hip,
     // bins_grid_blocks); alone, it takes every slot
     // (a render queued on this same stream cannot overlap this one)
-    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid; ++k)
+    for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid && !use_stamps; ++k)
         if (k != slot && tr->used[k] && tr->slot_stream[k] != st && hipEventQuery(tr->evd[k]) == hipErrorNotReady)
             a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
     if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
+    if (use_stamps) {
+        e = hipEventRecord(tr->ev_rng, st);
+        if (e != hipSuccess) return map_hip((int)e);
+        tr->rng_pending = true;
+    }
     if (tr->timing) {
         e = hipEventRecord(tr->ev2[slot], st);
         if (e != hipSuccess) return map_hip((int)e);
@@ -1450,12 +1607,12 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
     tr->slot_gen[slot] = tr->gen;
-    tr->slot_stream[slot] = st;
+    note_stream(tr, slot, st);
     tr->slot_cs[slot] = ci;
     tr->cs_cur = ci;
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;
-    if (!hit_mask) tr->rng_cur = nxt;  // frame+1's state
+    if (!hit_mask && !use_stamps) tr->rng_cur = nxt;  // frame+1's state
     rng_guard.armed = false;
     return BIH_OK;
 }
@@ -1503,22 +1660,13 @@ int bih_reserve(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_ro
     if (!rc) rc = ensure_qcount(tr);
     if (rc) return rc;
     // the frustum-bin path: tile queues of every camera set, fallback records
-    // (one per packet and frame at most), the start states of item splits
+    // (one per packet and frame at most), the stamps
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     const uint32_t ntiles = ((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
     for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles);
     if (!rc) rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, (size_t)ntiles * max_frames, 8);
-    // split start states: item_split's split count does not grow steadily
-    // with the frame count (3 frames may split 3 ways, 4 frames 2 ways), so
-    // the largest over every call of 1 .. max_frames frames
-    uint32_t most = 1;
-    for (uint32_t nf = 1; nf <= max_frames; ++nf) {
-        uint32_t fpi = 1, nsplit = 1;
-        item_split(tr, w, rows.nrows, spp, nf, &fpi, &nsplit);
-        most = std::max(most, nsplit);
-    }
-    if (!rc && most > 1) rc = ensure_per_slot(tr, &tr->rsplit, &tr->rsplit_cap, (size_t)(most - 1) * 5 * P, 1);
+    if (!rc && stamps_enabled()) rc = ensure_stamps(tr, ntiles);
     if (rc) return rc;
     return map_hip((int)hipStreamSynchronize(tr->stream));
 }
@@ -1623,8 +1771,8 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     // every render in flight (and after the last writer of the RNG ring)
     int rc = wait_renders(tr, st);
     if (rc) return rc;
-    if (tr->rng_pending) {
-        hipError_t e = hipStreamWaitEvent(st, tr->ev_rng, 0);
+    {
+        hipError_t e = wait_rng(tr, st);
         if (e != hipSuccess) return map_hip((int)e);
     }
     if (tr->tree_pending && hipEventQuery(tr->ev_tree) == hipSuccess) tr->tree_pending = false;
@@ -1693,7 +1841,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
     tr->slot_gen[slot] = tr->gen;
-    tr->slot_stream[slot] = st;
+    note_stream(tr, slot, st);
     tr->slot_cs[slot] = -1;            // reads no camera set
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;

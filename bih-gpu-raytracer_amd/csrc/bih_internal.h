@@ -132,12 +132,31 @@ struct RenderArgs {
     // item so that the items still outnumber the waves
     uint32_t fpi = 1;
     uint32_t nsplit = 1;
-    const uint32_t *rng_split = nullptr;    // split s >= 1's start states at (s-1) * 5 planes (k_rng_advance)
+    // k_render_bins: queue rounds each wave takes without atomics (BinQueue)
+    uint32_t static_rounds = 1;
     // one-frame k_render_bins (config C4's primary rays): per local tile the
     // 64-bit mask of its samples that hit (lane = pixel * spp + sample), 0 for
     // background tiles; k_render_fallback writes the undecided packets'
     unsigned long long *hit_mask = nullptr;
+    // Stamped XORWOW state (bih_capi.cpp, round 5): per local tile of the
+    // launch rows a u64 stamp {cur frame:26 | cur buffer:1, prev frame:26 |
+    // prev buffer:1, seq:10}; the tile's pixels' state at frame F sits in
+    // st_buf[b] (5 planes of nrows*w).  A launch reads each live tile's state
+    // from its stamp (`prev` when this launch already rewrote the stamp: its
+    // seq), steps it to the item's first frame, and the item that ends at the
+    // launch's last frame writes the state after it into the other buffer and
+    // the new stamp.  Background tiles (no triangle can be hit) are not
+    // touched: their states catch up when they turn live (k_rng_sync bounds
+    // the gap).  null: rng_in (the k_rng_advance ring).
+    unsigned long long *stamps = nullptr;
+    uint32_t *st_buf0 = nullptr, *st_buf1 = nullptr;
+    uint32_t st_f0 = 0;     // the launch's first frame
+    uint32_t st_seq = 0;    // this launch's sequence number (1 .. 1023)
 };
+
+// stamp word (RenderArgs::stamps)
+constexpr uint32_t kStampFrameBits = 26;
+constexpr uint32_t kStampFrameMax = (1u << kStampFrameBits) - 1u;
 
 // Camera of the frustum bins (bih_bins.hip), f64: forward normal n (A.n > 0,
 // A = lower_left - O), and the (u, v) of a camera-relative point X:
@@ -221,6 +240,13 @@ void free_tree_device(DeviceTree &t);
 // render (bih_render.hip)
 int upload_rng_tables(int device);
 long bins_timeline_dump(const char *path);         // diagnostic builds (BIH_BINS_TIMELINE)
+// stamped XORWOW state (RenderArgs::stamps): every tile's stamp = frame F in
+// buffer 0; and k_rng_sync: every pixel's state brought to frame T -- into
+// its tile's other buffer with a new stamp (seq), or (full != null) into
+// `full` for every pixel (leaving the stamped state)
+int launch_stamp_init(unsigned long long *stamps, uint32_t ntiles, uint32_t frame, void *stream);
+int launch_rng_sync(unsigned long long *stamps, uint32_t *buf0, uint32_t *buf1, uint32_t *full, uint32_t w,
+                    uint32_t nrows, uint32_t spp, uint32_t target, uint32_t seq, int device, void *stream);
 const uint32_t *rng_tables_device(int device);      // xorwow_init_tables_host() on the device
 // config C4 (bih_whitted.hip): device bytes of the ray queues for `rays`
 // samples, and the frame's launches (k_wh_gen, 9 x k_wh_trace, k_wh_shade);
@@ -234,7 +260,7 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
 int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
-                       void *stream, uint32_t *split = nullptr, uint32_t every = 0, uint32_t nsplit = 0);
+                       void *stream);
 // ev_k0 / ev_k1 (hipEvent_t or null): recorded right before and after the
 // main render kernel (bih_last_render_ms)
 int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev_k0 = nullptr,
@@ -309,7 +335,12 @@ const uint32_t *xorwow_tables_host();   // [32 seq][160][5] ++ [64 step][160][5]
 // v = M^skip v (skip draws ahead, host)
 void xorwow_skip(uint32_t v[5], uint64_t skip);
 // k_rng_init's device tables: jump bytes [4][256][160][5] ++ J, J^64 by nibbles [2][40][16][5]
-constexpr size_t kRngInitWords = (size_t)4 * 256 * 800 + 2 * 40 * 16 * 5;
+constexpr size_t kRngNibWords = 40 * 16 * 5;      // one nibble table (bih_render.hip jump_lds)
+// ++ nibble tables of M^(2^(7+l)), l = 0..6: kStampJumpFrames frames of 2 * 2^l draws
+// (k_rng_sync, one per spp = 2^l)
+constexpr uint32_t kStampJumpFrames = 64;
+constexpr size_t kRngJumpOffset = (size_t)4 * 256 * 800 + 2 * kRngNibWords;
+constexpr size_t kRngInitWords = kRngJumpOffset + 7 * kRngNibWords;
 const uint32_t *xorwow_init_tables_host();
 
 }  // namespace bih

@@ -134,39 +134,93 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
 }
 
 // dst = every pixel's XORWOW xorshift state `steps` draws after src's (dst
-// may be src).  2*spp steps: the state the next frame starts from
-// (cudaRender's write-back, CUDAKernels.cu:419); more: a gap in the frame
-// sequence.  The Weyl counter d is derived from the frame index, not stored.
-// split (optional): the states after every `every` steps, s = 1 .. nsplit-1
-// at split + (s-1) * 5 * P (the starts of a multi-frame k_render_bins
-// launch's later frame splits, RenderArgs::rng_split)
+// may be src).  2*spp*nframes steps: the state the launch after a render of
+// nframes frames starts from (cudaRender's write-back, CUDAKernels.cu:419);
+// more: a gap in the frame sequence.  The Weyl counter d is derived from the
+// frame index, not stored.
 __global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst,
-                                                          uint64_t P, uint32_t steps, uint32_t *split,
-                                                          uint32_t every, uint32_t nsplit) {
+                                                          uint64_t P, uint32_t steps) {
     const uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (lp >= P) return;
     uint32_t v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
-    // segments of `every` steps (no per-step division: the split test once
-    // per segment); split s is the state after s*every < steps steps
-    uint32_t k = 0;
-    for (uint32_t s = 1;; ++s) {
-        const bool store = split && s < nsplit && (uint64_t)s * every < steps;
-        const uint32_t end = store ? s * every : steps;
 #pragma unroll 8
-        for (; k < end; ++k) {
-            const uint32_t t = v[0] ^ (v[0] >> 2);
-            v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-            v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
-        }
-        if (!store) break;
-        uint32_t *o = split + (uint64_t)(s - 1) * 5 * P;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) o[(uint64_t)i * P + lp] = v[i];
+    for (uint32_t k = 0; k < steps; ++k) {
+        const uint32_t t = v[0] ^ (v[0] >> 2);
+        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
+}
+
+// Stamped state (RenderArgs::stamps): the frame and buffer a tile's state is
+// read from in launch `seq` -- the stamp's prev when this launch already
+// rewrote it, else its cur.
+struct StampBase {
+    uint32_t F, b;
+};
+__device__ __forceinline__ StampBase stamp_base(unsigned long long st, uint32_t seq) {
+    const bool mine = (uint32_t)(st >> 54) == seq;
+    const uint32_t w = mine ? (uint32_t)(st >> 27) & 0x7FFFFFFu : (uint32_t)st & 0x7FFFFFFu;
+    return {w & kStampFrameMax, w >> kStampFrameBits};
+}
+__device__ __forceinline__ unsigned long long stamp_pack(uint32_t F, uint32_t b, StampBase prev, uint32_t seq) {
+    return (unsigned long long)(F | (b << kStampFrameBits)) |
+           ((unsigned long long)(prev.F | (prev.b << kStampFrameBits)) << 27) | ((unsigned long long)seq << 54);
+}
+__device__ __forceinline__ void xorwow_steps(uint32_t v[5], uint32_t n) {
+#pragma unroll 4
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t t = v[0] ^ (v[0] >> 2);
+        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+    }
+}
+
+// Stamped state (RenderArgs::stamps): every tile at frame F in buffer 0.
+__global__ void __launch_bounds__(kThreads) k_stamp_init(unsigned long long *__restrict__ stamps, uint32_t ntiles,
+                                                         uint32_t frame) {
+    const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+    if (t < ntiles)
+        stamps[t] = (unsigned long long)frame | ((unsigned long long)frame << 27);   // cur = prev = (F, 0), seq 0
+}
+// Every pixel's stamped state brought to frame `target` (2*spp draws per
+// frame): into its tile's other buffer with the tile's new stamp (launch
+// `seq`; the tile's first pixel writes it), or -- full != null -- into `full`
+// for every pixel, leaving the stamps as they are (back to the ring).  Whole
+// kStampJumpFrames runs jump through the nibble table of their matrix (40
+// lookups against 64 * 2 * spp steps: background tiles lag by exactly that
+// much between syncs), the rest is stepped.  Grid-stride, so that few blocks
+// load the table into LDS.
+__global__ void __launch_bounds__(kThreads) k_rng_sync(unsigned long long *__restrict__ stamps, uint32_t *buf0,
+                                                       uint32_t *buf1, uint32_t *__restrict__ full, uint32_t w,
+                                                       uint32_t nrows, uint32_t log2spp, uint32_t target,
+                                                       uint32_t seq, const uint32_t *__restrict__ jump) {
+    __shared__ uint32_t s_nib[kRngNibWords];
+    for (uint32_t k = threadIdx.x; k < kRngNibWords; k += kThreads) s_nib[k] = jump[k];
+    __syncthreads();
+    const uint64_t P = (uint64_t)nrows * w;
+    const uint32_t lpx = 6 - log2spp, tw = 1u << ((lpx + 1) / 2), th = 1u << (lpx / 2);
+    const uint32_t tiles_x = (w + tw - 1) / tw;
+    for (uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x; lp < P; lp += (uint64_t)gridDim.x * kThreads) {
+        const uint32_t lr = (uint32_t)(lp / w), x = (uint32_t)(lp - (uint64_t)lr * w);
+        const uint32_t t = (lr / th) * tiles_x + x / tw;
+        const StampBase sb = stamp_base(stamps[t], seq);
+        if (!full && sb.F >= target) continue;   // already at the frame
+        const uint32_t *src = sb.b ? buf1 : buf0;
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
+        const uint32_t lag = target - sb.F;
+        for (uint32_t q = 0; q < lag / kStampJumpFrames; ++q) jump_lds(s_nib, v);
+        xorwow_steps(v, (lag % kStampJumpFrames) << (log2spp + 1));
+        uint32_t *dst = full ? full : (sb.b ? buf0 : buf1);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
+        if (!full && lr % th == 0 && x % tw == 0) stamps[t] = stamp_pack(target, sb.b ^ 1u, sb, seq);
+    }
 }
 
 // Pixel of k hits out of spp samples.  Color() returns (255,255,0) or
@@ -449,18 +503,22 @@ __device__ __forceinline__ void ray_coords(uint64_t rid, uint32_t tiles_x, uint3
 // its frame's state, so consecutive frames can be in flight together.
 template <uint32_t SPP>
 __device__ __forceinline__ void ray_jitter(const RenderArgs &a, uint64_t lp, uint32_t s, float &ru,
-                                           float &rv, uint32_t fj = 0) {
+                                           float &rv, uint32_t fj = 0, uint32_t tile = 0) {
     const uint64_t P = (uint64_t)a.nrows * a.w;
     uint32_t v[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) v[i] = a.rng_in[(uint64_t)i * P + lp];
-    uint32_t d = a.d_base;
     // frame j of a multi-frame launch: its draws start 2*spp*j past rng_in's
-    for (uint32_t k = 0; k < 2 * SPP * fj; ++k) {
-        const uint32_t t = v[0] ^ (v[0] >> 2);
-        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+    // (stamped state: past the tile's stamp frame)
+    uint32_t pre = 2 * SPP * fj;
+    const uint32_t *src = a.rng_in;
+    if (a.stamps) {
+        const StampBase sb = stamp_base(a.stamps[tile], a.st_seq);
+        src = sb.b ? a.st_buf1 : a.st_buf0;
+        pre = 2 * SPP * (a.st_f0 + fj - sb.F);
     }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
+    uint32_t d = a.d_base;
+    xorwow_steps(v, pre);
     d += 2 * SPP * fj * kWeyl;
     for (uint32_t k = 0; k <= s; ++k) {
         ru = xorwow_uniform(v, d);
@@ -1963,17 +2021,20 @@ struct BinQueue {
     __device__ __forceinline__ uint32_t extra(uint32_t b) const {
         return hs > 1u ? reinterpret_cast<const uint32_t *>(hdr + 8)[b] : 0u;
     }
-    // Start-up without atomics: each wave's first item is static -- block
-    // k's waves take items (k >> 3) * 4 + w of band k & 7 (blocks are dealt
-    // round-robin over the XCDs, so that is mostly the XCD's own band; only
-    // the speed depends on it) -- and the band heads hand out the items after
-    // those: stat(b) per band.  (Every wave starting in the per-CU slot made
-    // the 24 waves of a CU wait for three serial refills: 5.6 us median to a
-    // wave's first item in a one-frame launch, 12 us at q90.)
-    bool first;
-    __device__ __forceinline__ uint32_t stat(uint32_t b) const {
+    // Start-up without atomics: each wave's first `rounds` items are static
+    // -- in round r, block k's waves take items r * W(b) + (k >> 3) * 4 + w
+    // of band b = k & 7, W(b) the band's waves (blocks are dealt round-robin
+    // over the XCDs, so that is mostly the XCD's own band; only the speed
+    // depends on it) -- and the band heads hand out the items after those:
+    // stat(b) per band.  (Every wave starting in the per-CU slot made the 24
+    // waves of a CU wait for three serial refills: 5.6 us median to a wave's
+    // first item in a one-frame launch, 12 us at q90.)  rounds = 0 with a
+    // shared grid, whose heads then hand out every item.
+    uint32_t rounds, round;
+    __device__ __forceinline__ uint32_t band_waves(uint32_t b) const {
         return gridDim.x > b ? ((gridDim.x - b + 7u) >> 3) * (kThreads / 64) : 0u;
     }
+    __device__ __forceinline__ uint32_t stat(uint32_t b) const { return rounds * band_waves(b); }
 
     // Claims the slot position next() will use, so that its round trip
     // overlaps the current item's loads (BIH_QUEUE_AHEAD).
@@ -1985,10 +2046,11 @@ struct BinQueue {
 
     // next item: band (this->hb / band) and index within the band
     __device__ bool next(uint32_t lane, uint32_t &item) {
-        if (first) {
-            first = false;
+        if (round < rounds) {
             const uint32_t b = blockIdx.x & 7u;
-            const uint32_t idx = (blockIdx.x >> 3) * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const uint32_t idx = round * band_waves(b) + (blockIdx.x >> 3) * (kThreads / 64) +
+                                 __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            ++round;
             const uint4 h = hdr[b];
             const uint32_t x = extra(b);
             if (idx < h.w * nf + (hs - 1u) * x) {
@@ -1997,6 +2059,7 @@ struct BinQueue {
                 item = idx;
                 return true;
             }
+            round = rounds;   // (the band's items end before this wave's next round)
         }
         for (;;) {
             unsigned long long v = 0;
@@ -2048,11 +2111,17 @@ struct BinQueue {
 // MODE 1: also write the per-tile hit masks (RenderArgs::hit_mask; the C4
 // primary pass); MODE 2: also record each live tile's cycles per frame
 // (RenderArgs::bin_cost; the launch after which the queue is ordered by
-// measured cost) -- separate instantiations, so the headline kernel keeps its
-// registers
+// measured cost); | kBinsStamped: the XORWOW state per tile
+// (RenderArgs::stamps) -- separate instantiations, so the headline kernel
+// keeps its registers
+constexpr int kBinsStamped = 4;
+#ifndef BIH_STAMPED_WAVES
+#define BIH_STAMPED_WAVES 1   // 6: the stamped instance held to 6 waves per SIMD (scratch spills; one-frame calls 0.093 against 0.082 ms at its own 5)
+#endif
 template <int LOG2SPP, int MODE = 0>
-__global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const RenderArgs a) {
-    constexpr bool MASK = MODE == 1, COST = MODE == 2;
+__global__ void __launch_bounds__(kThreads, (MODE & kBinsStamped) ? BIH_STAMPED_WAVES : 1) BIH_BINS_OCC
+k_render_bins(const RenderArgs a) {
+    constexpr bool MASK = (MODE & 3) == 1, COST = (MODE & 3) == 2, STAMP = (MODE & kBinsStamped) != 0;
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -2089,7 +2158,8 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
     // (not while another render holds CU slots: this launch's blocks then
     // start as that one's waves exit, and a late block's static item -- the
     // band's costliest first -- would start late)
-    q.first = a.shared_grid == 0u;
+    q.rounds = a.shared_grid ? 0u : a.static_rounds;
+    q.round = 0;
     q.has_pending = false;
     q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
     q.hs = a.nsplit == 1u ? a.hsplit : 1u;
@@ -2198,22 +2268,22 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
         // (kept in LDS between frames: registers stay those of the list walk)
         uint32_t dfr = a.d_base + f0 * (2u * SPP * kWeyl);   // Weyl counter at the start of frame fj
         if (valid) {
-            // frame f0's state: the launch's first frame's, or the split's
-            // start that k_rng_advance stored (f0 frames of 2*SPP draws on),
-            // or (a heavy tile's later frame range) the first frame's stepped
-            // 2*SPP*f0 draws on here
+            // frame f0's state: the launch's first frame's stepped 2*SPP*f0
+            // draws on (a later item split or a heavy tile's later frame
+            // range: at most ~100 steps, against the frames the item renders)
             const uint64_t P = (uint64_t)a.nrows * a.w;
-            const uint32_t *src = fs ? a.rng_split + (uint64_t)(fs - 1) * 5 * P : a.rng_in;
+            const uint32_t *src = a.rng_in;
+            uint32_t pre = 2u * SPP * f0;
+            if (STAMP) {
+                // the tile's stamped state, stepped to frame st_f0 + f0
+                const StampBase sb = stamp_base(a.stamps[tile], a.st_seq);
+                src = sb.b ? a.st_buf1 : a.st_buf0;
+                pre = 2u * SPP * (a.st_f0 + f0 - sb.F);
+            }
             uint32_t v[5];
 #pragma unroll
             for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
-            const uint32_t pre = fs ? 0u : 2u * SPP * f0;
-#pragma unroll 4
-            for (uint32_t k = 0; k < pre; ++k) {
-                const uint32_t t = v[0] ^ (v[0] >> 2);
-                v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-                v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
-            }
+            xorwow_steps(v, pre);
 #pragma unroll
             for (int i = 0; i < 5; ++i) s_rs[i][tid] = v[i];
         }
@@ -2271,6 +2341,16 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
                 if (fj + 1u < nf) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) s_rs[i][tid] = rs[i];
+                } else if (STAMP && nf == a.nframes && s == 0u) {
+                    // stamped: the state after the launch's last frame
+                    // (cudaRender's write-back, CUDAKernels.cu:419) into the
+                    // tile's other buffer; other items of the tile read the
+                    // base buffer, which nobody writes in this launch
+                    const StampBase sb = stamp_base(a.stamps[tile], a.st_seq);
+                    uint32_t *dst = sb.b ? a.st_buf0 : a.st_buf1;
+                    const uint64_t P = (uint64_t)a.nrows * a.w;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = rs[i];
                 }
                 uf = ((float)x + ru) / fw;       // CUDAKernels.cu:414-415
                 vf = ((float)y + rv) / fh;
@@ -2359,6 +2439,11 @@ __global__ void __launch_bounds__(kThreads) BIH_BINS_OCC k_render_bins(const Ren
             BIH_PH(5);
         }
         if (COST && lane == 0) a.bin_cost[bin] = (work << 8) / (nf - f0);
+        if (STAMP && nf == a.nframes && lane == 0) {
+            // (the item ending at the launch's last frame) the tile's new stamp
+            const StampBase sb = stamp_base(a.stamps[tile], a.st_seq);
+            a.stamps[tile] = stamp_pack(a.st_f0 + a.nframes, sb.b ^ 1u, sb, a.st_seq);
+        }
 #if BIH_BINS_TIMELINE
         tl_rec(lane, 0u, tl_t0, __builtin_amdgcn_s_memrealtime(),
                (((const uint32_t *)a.bin_off)[bin + 1] - ((const uint32_t *)a.bin_off)[bin]) | ((nf - f0) << 24));
@@ -2417,7 +2502,7 @@ __global__ void __launch_bounds__(kThreads) k_render_fallback(const RenderArgs a
         float dx = 0.f, dy = 0.f, dz = 1.f;
         if (mine) {
             float ru = 0.f, rv = 0.f;
-            ray_jitter<SPP>(a, lp, s, ru, rv, fj);
+            ray_jitter<SPP>(a, lp, s, ru, rv, fj, tile);
             const uint32_t y = global_row(lr, a.row0, a.band_h, a.band_step);
             camera_dir(a, ((float)x + ru) / fw, ((float)y + rv) / fh, dx, dy, dz);
         }
@@ -3090,12 +3175,32 @@ int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, ui
     return (int)hipGetLastError();
 }
 
-int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
-                       void *stream, uint32_t *split, uint32_t every, uint32_t nsplit) {
+int launch_stamp_init(unsigned long long *stamps, uint32_t ntiles, uint32_t frame, void *stream) {
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(k_stamp_init, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       (hipStream_t)stream, stamps, ntiles, frame);
+    return (int)hipGetLastError();
+}
+
+int launch_rng_sync(unsigned long long *stamps, uint32_t *buf0, uint32_t *buf1, uint32_t *full, uint32_t w,
+                    uint32_t nrows, uint32_t spp, uint32_t target, uint32_t seq, int device, void *stream) {
+    const uint64_t P = (uint64_t)nrows * w;
+    if (P == 0) return 0;
+    const uint32_t *tab = rng_tables_device(device);
+    if (!tab || spp == 0 || spp > 64 || (spp & (spp - 1))) return (int)hipErrorInvalidValue;
+    const uint32_t L = (uint32_t)__builtin_ctz(spp);
+    // 8 pixels per thread: 1/8 of the blocks load the 12.8 KB table
+    const uint64_t blocks = (P + 8 * kThreads - 1) / (8 * kThreads);
+    hipLaunchKernelGGL(k_rng_sync, dim3((uint32_t)blocks), dim3(kThreads), 0, (hipStream_t)stream, stamps, buf0, buf1,
+                       full, w, nrows, L, target, seq, tab + kRngJumpOffset + L * kRngNibWords);
+    return (int)hipGetLastError();
+}
+
+int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps, void *stream) {
     if (pixels == 0 || (steps == 0 && src == dst)) return 0;
     const uint32_t blocks = (uint32_t)((pixels + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, src,
-                       dst, (uint64_t)pixels, steps, split, every ? every : 1u, split ? nsplit : 0u);
+                       dst, (uint64_t)pixels, steps);
     return (int)hipGetLastError();
 }
 
@@ -3259,16 +3364,17 @@ int launch_chunk_order(const uint32_t *cost, uint32_t chunks_x, uint32_t nchunks
 #ifndef BIH_BINS_MULTI_PER_CU
 #define BIH_BINS_MULTI_PER_CU 4
 #endif
-uint32_t bins_grid_blocks(int device, uint32_t nframes) {
+uint32_t bins_grid_blocks(int device, uint32_t nframes, bool stamped) {
     static std::mutex mu;
-    static uint32_t cache[64][2] = {{0}};
+    static uint32_t cache[64][2][2] = {{{0}}};
     std::lock_guard<std::mutex> lk(mu);
     if (device < 0 || device >= 64) return 0;
-    if (!cache[device][0]) {
+    if (!cache[device][stamped][0]) {
         int cus = 0, per = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, reinterpret_cast<const void *>(k_render_bins<2, 0>), kThreads, 0);
+            &per, stamped ? reinterpret_cast<const void *>(k_render_bins<2, kBinsStamped>)
+                          : reinterpret_cast<const void *>(k_render_bins<2, 0>), kThreads, 0);
         if (cus <= 0) cus = 256;
         if (per <= 0) per = 1;
         int multi = BIH_BINS_MULTI_PER_CU < per ? BIH_BINS_MULTI_PER_CU : per;
@@ -3280,10 +3386,10 @@ uint32_t bins_grid_blocks(int device, uint32_t nframes) {
             const int v = atoi(e);
             if (v > 0 && v <= 32) multi = v;
         }
-        cache[device][0] = (uint32_t)(cus * per);
-        cache[device][1] = (uint32_t)(cus * multi);
+        cache[device][stamped][0] = (uint32_t)(cus * per);
+        cache[device][stamped][1] = (uint32_t)(cus * multi);
     }
-    return cache[device][nframes > 1 ? 1 : 0];
+    return cache[device][stamped][nframes > 1 ? 1 : 0];
 }
 
 template <int L>
@@ -3293,8 +3399,12 @@ static hipError_t launch_bins(const RenderArgs &a, hipStream_t st, uint32_t bloc
     if (e != hipSuccess) return e;
     if (a.hit_mask)
         hipLaunchKernelGGL((k_render_bins<L, 1>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else if (a.bin_cost && a.stamps)
+        hipLaunchKernelGGL((k_render_bins<L, 2 | kBinsStamped>), dim3(blocks), dim3(kThreads), 0, st, a);
     else if (a.bin_cost)
         hipLaunchKernelGGL((k_render_bins<L, 2>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else if (a.stamps)
+        hipLaunchKernelGGL((k_render_bins<L, kBinsStamped>), dim3(blocks), dim3(kThreads), 0, st, a);
     else
         hipLaunchKernelGGL((k_render_bins<L, 0>), dim3(blocks), dim3(kThreads), 0, st, a);
     e = k1 ? hipEventRecord(k1, st) : hipSuccess;
@@ -3346,7 +3456,7 @@ int launch_render(const RenderArgs &a, uint32_t traverse, void *stream, void *ev
         // frustum bins: the list-walk kernel, then the exact walk for what it
         // left undecided (the fallback grid stays within the spill area)
         const uint32_t fb = grid < 64u ? grid : 64u;
-        const uint32_t gb = bins_grid_blocks(dev, a.shared_grid ? 2u : 1u);
+        const uint32_t gb = bins_grid_blocks(dev, a.shared_grid ? 2u : 1u, a.stamps != nullptr);
         if (BIH_FAST_COUNTERS || BIH_PHASES) {
             const hipError_t e = hipMemsetAsync(a.work, 0, kWorkWords * sizeof(uint32_t), st);
             if (e != hipSuccess) return (int)e;

@@ -122,7 +122,7 @@ void xorwow_skip(uint32_t v[5], uint64_t skip) {
 // with J = M^(2^67) (one subsequence), so a pixel's subsequence start is at
 // most 4 matrix applies; then J and J^64 by 4-bit input groups [2][40][16][5]
 // (entry (g, n) = XOR of the matrix's columns 4g + set bits of n), a lane's
-// step to its next pixel from LDS.
+// step to its next pixel from LDS; then the frame jumps [7][40][16][5].
 static void build_init_tables() {
     const uint32_t *seqt = xorwow_tables_host();
     std::vector<Gf2> seq(32);
@@ -139,8 +139,14 @@ static void build_init_tables() {
     }
     // nibble tables of J (k_rng_init's per-pixel step) and of J^64 (a lane's
     // step when the 64 lanes of a wave seed 64 consecutive pixels at a time)
-    const Gf2 *steps[2] = {&seq[0], &seq[6]};
-    for (int t = 0; t < 2; ++t) {
+    // ... and of M^(2^(7+l)), l = 0..6: k_rng_sync's jump of kStampJumpFrames
+    // = 64 frames of 2 * 2^l draws at spp 2^l
+    std::vector<Gf2> fj(7);
+    const uint32_t *stept = seqt + 32 * 800;
+    for (int l = 0; l < 7; ++l) memcpy(fj[l].c, stept + (7 + l) * 800, 800 * 4);
+    const Gf2 *steps[9] = {&seq[0], &seq[6], &fj[0], &fj[1], &fj[2], &fj[3], &fj[4], &fj[5], &fj[6]};
+    static_assert(kStampJumpFrames == 64, "the frame-jump tables are M^(2^(7+l))");
+    for (int t = 0; t < 9; ++t) {
         uint32_t *nib = bytes + 4 * 256 * 800 + t * 40 * 16 * 5;
         for (int g = 0; g < 40; ++g)
             for (int n = 0; n < 16; ++n)

@@ -868,3 +868,75 @@ def test_failed_back_tree_allocation_leaves_tree_usable(gpu, bihrt_mod, oracle_m
             ref, _ = ot.render(w, h, frame=f)
             assert np.array_equal(img, ref), (k, f)
         g.close()
+
+
+@pytest.mark.gpu
+def test_stamped_state_panning_sequence_matches_oracle(gpu, bihrt_mod, oracle_mod):
+    """Frustum-bin launches on one stream keep each tile's XORWOW state with
+    a stamp (bih_capi.cpp stamped mode): a tile no triangle covers is not
+    stepped and catches up when it turns live, every 64 frames all tiles are
+    brought level (k_rng_sync), and a render of another kind takes the state
+    back into the ring.  A small object crosses the view over 160 frames in
+    calls of 1 .. 16 frames, so tiles turn live after long background runs;
+    sampled frames equal the oracle's, then a Whitted frame, a jump back and
+    a frame after it continue the sequence."""
+    import torch
+    S = bihrt_mod.scenes
+    tris = S.soup(20_000, seed=3).copy()
+    v = tris.reshape(-1, 3)
+    v[:] = 0.25 * (v - v.mean(0)) + v.mean(0)     # the object covers a small part of the view
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 96, 64
+    r = bihrt_mod.Renderer(g, w, h)
+    sizes = [1, 16, 3, 1, 8, 16, 2, 1, 16, 5]
+    stride = h * w
+    frame, calls = 0, []
+    while frame < 160:
+        n = min(sizes[len(calls) % len(sizes)], 160 - frame)
+        cam = _moved_camera(bihrt_mod, w, h, -0.9 + 1.8 * frame / 160, 0.0, 0.0)
+        buf = torch.full((n * stride,), -1, dtype=torch.int32, device="cuda")
+        r.camera = cam
+        if n == 1:
+            r.render_device(buf.data_ptr(), frame)
+        else:
+            r.render_device_frames(buf.data_ptr(), frame, n, stride)
+        calls.append((frame, n, cam, buf))
+        frame += n
+    r.sync()
+    checked = 0
+    for k, (f0, n, cam, buf) in enumerate(calls):
+        if k % 3 and k != len(calls) - 1:
+            continue
+        b = buf.cpu().numpy().view(np.uint32)
+        for j in sorted({0, n - 1}):
+            ref, _ = ot.render(w, h, frame=f0 + j, cam=np.array(cam.as_list(), np.float32))
+            got = b[j * stride:(j + 1) * stride].reshape(h, w)
+            assert np.array_equal(got, ref), (f0 + j, int((got != ref).sum()))
+            checked += 1
+    assert checked >= 10
+    # another kind of render, then back
+    cam = calls[-1][2]
+    r.camera = cam
+    camf = np.array(cam.as_list(), np.float32)
+    out = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    # a Whitted frame, a frame on another stream, four in a row (back into
+    # stamped mode), a gap of two sync runs (whole-run jumps), a jump back
+    plan = [(160, "whitted", None), (161, "bins", side), (162, "bins", None), (163, "bins", None),
+            (164, "bins", None), (165, "bins", None), (300, "bins", None), (301, "bins", None),
+            (40, "bins", None), (41, "bins", None)]
+    for f, kind, stream in plan:
+        if kind == "whitted":
+            r.render_whitted_device(out.data_ptr(), f)
+            ref, _ = ot.render_whitted(w, h, frame=f, cam=camf)
+        else:
+            r.render_device(out.data_ptr(), f, stream=stream.cuda_stream if stream else None)
+            ref, _ = ot.render(w, h, frame=f, cam=camf)
+        if stream is not None:
+            stream.synchronize()
+        r.sync()
+        got = out.cpu().numpy().view(np.uint32).reshape(h, w)
+        assert np.array_equal(got, ref), (f, kind, int((got != ref).sum()))
+    g.close()

@@ -9,8 +9,9 @@ cd $R
 V=$R/bih-gpu-raytracer_amd/lib/variants
 for k in $(seq 1 $N); do
   for X in "$@"; do
-    L=""; [ $X != base ] && L=$V/libbih_amd_$X.so
-    BIH_LIB=$L timeout -k 10 300 python -u bench.py --c5 0 --whitted-frames 0 --cpu-baseline 0 --traffic 0 \
+    B=${X%%+*}; E=""; [ "$B" != "$X" ] && E=${X#*+}; E=${E//,/ }
+    L=""; [ $B != base ] && L=$V/libbih_amd_$B.so
+    env $E BIH_LIB=$L timeout -k 10 300 python -u bench.py --c5 0 --whitted-frames 0 --cpu-baseline 0 --traffic 0 \
         --no-reference-leg > $O/bench_${X}_$k.json 2> $O/bench_${X}_$k.err || { tail -20 $O/bench_${X}_$k.err; exit 1; }
     python3 -c "
 import json,sys

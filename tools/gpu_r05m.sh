@@ -1,0 +1,22 @@
+# Round 5: stamped per-tile XORWOW state (no k_rng_advance in frustum-bin
+# launches) -- tests, A/B against the ring (BIH_STAMPED=0) and the forced 6-wave build, traces.
+set -u
+T=${1:-r05m}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$T
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --durations=5 --timeout 300 --timeout-method thread \
+    > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash tools/gpu_ab5.sh $T 2 base base+BIH_STAMPED=0 base+BIH_STAMPED=0,BIH_AUX_ADVANCE=0 || exit 1
+cd /tmp && export TMPDIR=/tmp
+trace() {   # trace NAME ARGS...
+  local N=$1; shift
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/$N -o k --output-format csv -- \
+      python3 $R/tools/call_breakdown.py "$@" > $O/$N.log 2>&1 || { tail -20 $O/$N.log; return 1; }
+  grep "^calls" $O/$N.log
+  python3 $R/tools/call_timeline.py $O/$N/k_kernel_trace.csv --show 1 --dispatch-csv $O/${N}_dispatches.csv > $O/${N}_timeline.txt; tail -8 $O/${N}_timeline.txt
+}
+trace g16_sync --frames 16 --calls 20 --sync 1 &&
+trace one_sync --frames 1 --calls 60 --sync 1
