@@ -902,7 +902,7 @@ static int prepare_rng(bih_tree *tr, uint32_t w, uint32_t spp, uint32_t frame, u
         // (cheaper than re-seeding with the 2^67-subsequence jump)
         const uint32_t steps = (frame - tr->next_frame) * 2 * spp;
         uint32_t *b = rng_buf(tr, tr->rng_cur);
-        int e = bih::launch_rng_advance(b, b, P, steps, st);
+        int e = bih::launch_rng_advance(b, b, P, steps, tr->t.device, st);
         if (e) return map_hip(e);
     } else if (!same) {
         uint64_t skip = (uint64_t)2 * spp * frame;
@@ -1491,7 +1491,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         // the render reads rng_cur only).  (On a stream of its own beside the
         // render, the next render's wait across queues cost more than the
         // advance: one-frame calls 0.107 against 0.087 ms, r05m.)
-        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, st));
+        rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp * nframes, tr->t.device, st));
         if (rc) return rc;
     }
     if (!hit_mask) tr->next_frame = frame + nframes;
@@ -1790,7 +1790,7 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     const size_t P = (size_t)rows.nrows * w;
     const uint64_t rays = (uint64_t)P * spp;
     const int cur = tr->rng_cur, nxt = (cur + 1) % kRngBufs;
-    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, st));
+    rc = map_hip(bih::launch_rng_advance(rng_buf(tr, cur), rng_buf(tr, nxt), P, 2 * spp, tr->t.device, st));
     if (rc) return rc;
     if (tr->wh_rays < rays) {
         hipError_t e = hipStreamSynchronize(st);   // the previous Whitted render's readers

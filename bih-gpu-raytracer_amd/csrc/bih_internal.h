@@ -259,7 +259,7 @@ int whitted_work(const void *mem, uint64_t rays, uint32_t ray_counts[9], unsigne
 int launch_rng_init(uint32_t *rng, uint32_t w, uint32_t row0, uint32_t nrows, uint32_t band_h,
                     uint32_t band_step, uint64_t seed, uint64_t skip, int device, void *stream);
 // dst = src's per-pixel state advanced by `steps` draws (planes of `pixels`; dst may be src)
-int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps,
+int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps, int device,
                        void *stream);
 // ev_k0 / ev_k1 (hipEvent_t or null): recorded right before and after the
 // main render kernel (bih_last_render_ms)

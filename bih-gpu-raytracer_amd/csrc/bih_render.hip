@@ -137,22 +137,34 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
 // may be src).  2*spp*nframes steps: the state the launch after a render of
 // nframes frames starts from (cudaRender's write-back, CUDAKernels.cu:419);
 // more: a gap in the frame sequence.  The Weyl counter d is derived from the
-// frame index, not stored.
-__global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst,
-                                                          uint64_t P, uint32_t steps) {
-    const uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (lp >= P) return;
-    uint32_t v[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
-#pragma unroll 8
-    for (uint32_t k = 0; k < steps; ++k) {
-        const uint32_t t = v[0] ^ (v[0] >> 2);
-        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+// frame index, not stored.  Up to two of the powers 2^7 .. 2^13 of `steps`
+// jump through their nibble tables in LDS (40 lookups each, against 128 ..
+// 8192 steps; the frame-jump tables of k_rng_sync), the rest is stepped;
+// grid-stride, so that few blocks load the tables.
+__global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t P,
+                                                          uint32_t steps, const uint32_t *__restrict__ jumps,
+                                                          uint32_t k0, uint32_t k1) {
+    __shared__ uint32_t s_nib[2][kRngNibWords];
+    const uint32_t nj = (k0 < 7u) + (k1 < 7u);
+    for (uint32_t t = 0; t < nj; ++t) {
+        const uint32_t *tab = jumps + (t ? k1 : k0) * kRngNibWords;
+        for (uint32_t k = threadIdx.x; k < kRngNibWords; k += kThreads) s_nib[t][k] = tab[k];
     }
+    if (nj) __syncthreads();
+    for (uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x; lp < P; lp += (uint64_t)gridDim.x * kThreads) {
+        uint32_t v[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
+        for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
+        for (uint32_t t = 0; t < nj; ++t) jump_lds(s_nib[t], v);
+#pragma unroll 8
+        for (uint32_t k = 0; k < steps; ++k) {
+            const uint32_t t = v[0] ^ (v[0] >> 2);
+            v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+            v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
+    }
 }
 
 // Stamped state (RenderArgs::stamps): the frame and buffer a tile's state is
@@ -3196,11 +3208,34 @@ int launch_rng_sync(unsigned long long *stamps, uint32_t *buf0, uint32_t *buf1, 
     return (int)hipGetLastError();
 }
 
-int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps, void *stream) {
+int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint32_t steps, int device,
+                       void *stream) {
     if (pixels == 0 || (steps == 0 && src == dst)) return 0;
-    const uint32_t blocks = (uint32_t)((pixels + kThreads - 1) / kThreads);
+    const uint32_t *tab = rng_tables_device(device);
+    if (!tab) return (int)hipErrorNotInitialized;
+    // the two highest powers 2^7 .. 2^13 of `steps` through tables (index
+    // k - 7; 7 = none), unless BIH_ADVANCE_JUMP=0 (A/B)
+    static const bool jump = [] {
+        const char *e = getenv("BIH_ADVANCE_JUMP");
+        return !(e && e[0] == '0');
+    }();
+    uint32_t k0 = 7, k1 = 7, rest = steps;
+    for (int k = 13; k >= 7 && jump && k1 == 7u; --k)
+        if (rest >> k & 1u) {
+            rest &= ~(1u << k);
+            if (k0 == 7u) k0 = (uint32_t)k - 7;
+            else k1 = (uint32_t)k - 7;
+        }
+    // with tables: up to 8 pixels per thread (fewer blocks load them), at
+    // least 2048 blocks (a rank's share of the rows is 1/8 of the frame)
+    uint64_t per = kThreads;
+    if (k0 < 7u) {
+        const uint64_t ppt = (pixels + 2048ull * kThreads - 1) / (2048ull * kThreads);
+        per = (ppt < 8 ? ppt : 8) * kThreads;
+    }
+    const uint32_t blocks = (uint32_t)((pixels + per - 1) / per);
     hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, src,
-                       dst, (uint64_t)pixels, steps);
+                       dst, (uint64_t)pixels, rest, tab + kRngJumpOffset, k0, k1);
     return (int)hipGetLastError();
 }
 
