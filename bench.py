@@ -304,6 +304,10 @@ class Workload:
         calls = call_sizes(steps, g)
         warm = call_sizes(a.warmup, g)
         warm += [m for m in sorted(set(calls)) if m not in warm]
+        # every stream in play takes a call before the timed ones: a stream's
+        # first kernel creates its hardware queue (~7 ms)
+        while len(warm) < (nf or C.F):
+            warm.append(calls[0])
         k = c = 0
         for m in warm:
             self.step(mode, rows, c, frame_of(base, k), traverse, rebuild=rebuild, nf=nf, m=m, first=first)
@@ -606,11 +610,14 @@ def main():
     # on the render stream right around the render kernel (bih_last_render_ms),
     # over isolated launches (each call synchronised before the next) -- the
     # figure rocprofv3's kernel trace reports for the same kernel
-    # (the headline's launches: a call of G frames, one k_render_bins launch)
+    # (the headline's launches: a call of G frames, one k_render_bins launch;
+    # the calls rotate over the headline's streams as its do, so the render
+    # runs through the XORWOW ring -- k_render_bins<L, 0>, the headline's
+    # instance; a run of calls on one stream switches to the stamped state)
     kms_iso, tails_iso = [], []
     r.set_timing(True)
     for k in range(args.kernel_samples):
-        wl.step(mode, rows, k, frame_of(5000, k * G), trav, nf=1, m=G)
+        wl.step(mode, rows, k, frame_of(5000, k * G), trav, m=G)
         torch.cuda.synchronize()
         km, tm = r.last_render_times()
         kms_iso.append(km)
@@ -938,6 +945,7 @@ def measure_traffic(args):
     L2-to-fabric bytes: Infinity Cache hits are included."""
     import csv
     import glob
+    import re
     import shutil
     import subprocess
     import tempfile
@@ -948,6 +956,10 @@ def measure_traffic(args):
     tmp = tempfile.mkdtemp(prefix="bih_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     traverse = args.traverse
+    # the headline's renders run with calls in flight on several streams, so
+    # through the XORWOW ring (k_render_bins<L, 0>); the traffic driver issues
+    # its calls on one stream, which would switch to the stamped instance
+    env["BIH_STAMPED"] = "0"
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         out = os.path.join(tmp, ctr)
         cmd = [prof, "--pmc", ctr, "-d", out, "-o", ctr, "--output-format", "csv", "--",
@@ -961,14 +973,26 @@ def measure_traffic(args):
         if p.returncode != 0:
             return None
         # the dominant render kernel: k_render_bins (any-hit with frustum
-        # bins), else the BIH packet kernel
-        vals = {}
+        # bins; the plain instance <L, 0>, not the first launch's cost
+        # measuring <L, 2>), else the BIH packet kernel; per dispatch (a
+        # counter may come split over dimensions: summed)
+        per = {}
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 name = row["Kernel_Name"]
-                for key in ("k_render_bins", "k_render_packet_asm"):
-                    if key in name:
-                        vals.setdefault(key, []).append(float(row["Counter_Value"]))
+                if "k_render_bins" in name:
+                    if not re.search(r"k_render_bins<\d+, 0>", name):
+                        continue
+                    key = "k_render_bins"
+                elif "k_render_packet_asm" in name:
+                    key = "k_render_packet_asm"
+                else:
+                    continue
+                did = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(per))
+                per[(key, did)] = per.get((key, did), 0.0) + float(row["Counter_Value"])
+        vals = {}
+        for (key, _), v in sorted(per.items(), key=lambda kv: int(kv[0][1]) if kv[0][1].isdigit() else 0):
+            vals.setdefault(key, []).append(v)
         key = "k_render_bins" if "k_render_bins" in vals else "k_render_packet_asm"
         if not vals.get(key):
             return None

@@ -94,6 +94,7 @@ struct CamSet {
     uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t *q_list = nullptr, *q_hdr = nullptr;
     bool q_cost = false;             // the queue is ordered by measured tile costs (launch_bin_queue's cost)
+    uint32_t uses = 0;               // frustum-bin renders since these bins were built
     // the last launch that measured tile costs (bins.cost) was over q_key ==
     // cost_key: the next queue of those rows is built from them
     bool cost_known = false;
@@ -971,6 +972,7 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
                       uint32_t h, uint32_t spp, bool need_prim, hipStream_t st) {
     c.bins_valid = true;
     c.bins_usable = false;
+    c.uses = 0;
     c.gen = ++tr->bins_gen;
     c.bins_key[0] = w;
     c.bins_key[1] = h;
@@ -1194,12 +1196,18 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
         c.q_valid = true;
         c.q_cost = measured;
     }
-    if (!c.q_cost && !measured && cost_queue_enabled()) {
+    // (measured from the camera's second render on: a camera that moves every
+    // frame never renders twice, and the measuring instance costs ~1.4x)
+    if (!c.q_cost && !measured && cost_queue_enabled() && c.uses >= 1) {
         a.bin_cost = c.bins.cost;
         memcpy(c.cost_key, key, sizeof key);
         c.cost_known = true;
     }
-    a.hsplit = c.q_cost && nframes >= 4 ? (nframes >= 8 ? 4u : 2u) : 1u;
+    // heavy tiles: as many items as the others (RenderArgs::nsplit), or --
+    // with measured costs -- 2 or 4 times as many, up to one frame each
+    a.hsplit = a.nsplit;
+    if (c.q_cost && nframes >= 4)
+        a.hsplit = std::max(a.nsplit, std::min(nframes, a.nsplit * (nframes >= 8 ? 4u : 2u)));
     rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, nrec, 8);
     if (rc) return rc;
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
@@ -1609,6 +1617,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     tr->slot_gen[slot] = tr->gen;
     note_stream(tr, slot, st);
     tr->slot_cs[slot] = ci;
+    if (use_bins) ++c.uses;
     tr->cs_cur = ci;
     tr->last_slot = slot;
     tr->slot = (slot + 1) % kSlots;

@@ -110,9 +110,10 @@ struct RenderArgs {
     // state (kBinSetWords, zero at launch: band heads, fallback count, per-CU
     // slots), plus the other set, which this launch zeroes for the slot's next one
     const uint32_t *bin_queue = nullptr;
-    // (nsplit == 1 launches, a queue ordered by measured cost) each band's
-    // first heavy tiles -- their count follows the band headers -- are taken
-    // as `hsplit` items each, over frame ranges; 1: no heavy items
+    // (a queue ordered by measured cost) each band's first heavy tiles --
+    // their count follows the band headers -- are taken as `hsplit` items
+    // each, over frame ranges (the other live tiles: nsplit); hsplit ==
+    // nsplit: no heavy items
     uint32_t hsplit = 1;
     uint32_t *bin_cost = nullptr;           // non-null: k_render_bins records each live tile's cycles per frame
     const uint32_t *bin_qhdr = nullptr;

@@ -2024,14 +2024,17 @@ struct BinQueue {
     uint4 hb;                          // header of the band of the item next() returned
     unsigned long long pending;        // a position claimed ahead (claim()), lane 0
     bool has_pending;
-    uint32_t nf;                       // frames per launch: a band holds hb.w * nf items
-    // heavy tiles (RenderArgs::hsplit > 1): the band's first heavy[b] tiles
-    // take hs items each (frame ranges), so a band holds (hs - 1) * heavy[b]
-    // more; hv = the heavy count of the band of the item next() returned
+    // items per live tile: ns (RenderArgs::nsplit, frame ranges of a.fpi
+    // frames); the band's first heavy[b] tiles take hs each instead
+    // (RenderArgs::hsplit); a background item covers 64 tiles in every
+    // frame.  hv = the heavy count of the band of the item next() returned
     // (the heavy counts follow the 8 band headers: launch_bin_queue's kQHeavy)
-    uint32_t hs, hv;
+    uint32_t ns, hs, hv;
     __device__ __forceinline__ uint32_t extra(uint32_t b) const {
-        return hs > 1u ? reinterpret_cast<const uint32_t *>(hdr + 8)[b] : 0u;
+        return hs != ns ? reinterpret_cast<const uint32_t *>(hdr + 8)[b] : 0u;
+    }
+    __device__ __forceinline__ uint32_t band_items(const uint4 &h, uint32_t x) const {
+        return x * hs + (h.y - x) * ns + (h.w - h.y);
     }
     // Start-up without atomics: each wave's first `rounds` items are static
     // -- in round r, block k's waves take items r * W(b) + (k >> 3) * 4 + w
@@ -2065,7 +2068,7 @@ struct BinQueue {
             ++round;
             const uint4 h = hdr[b];
             const uint32_t x = extra(b);
-            if (idx < h.w * nf + (hs - 1u) * x) {
+            if (idx < band_items(h, x)) {
                 hb = h;
                 hv = x;
                 item = idx;
@@ -2088,7 +2091,7 @@ struct BinQueue {
                 const uint32_t b = (hi - 1u) >> 24, start = ((hi - 1u) & 0xFFFFFFu) * kBinBatch + stat(b);
                 hb = hdr[b];
                 hv = extra(b);
-                if (start + lo < hb.w * nf + (hs - 1u) * hv) {
+                if (start + lo < band_items(hb, hv)) {
                     item = start + lo;
                     band = b;
                     return true;
@@ -2102,7 +2105,7 @@ struct BinQueue {
                     uint32_t c = 0;
                     if (lane == 0) c = atomicAdd(set + band * 32, kBinBatch);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    if (c + stat(band) < h.w * nf + (hs - 1u) * x) {
+                    if (c + stat(band) < band_items(h, x)) {
                         if (lane == 0)
                             atomicExch(slot, ((unsigned long long)(((band << 24) | (c / kBinBatch)) + 1u) << 32) | 1ull);
                         hb = h;
@@ -2130,9 +2133,21 @@ constexpr int kBinsStamped = 4;
 #ifndef BIH_STAMPED_WAVES
 #define BIH_STAMPED_WAVES 1   // 6: the stamped instance held to 6 waves per SIMD (scratch spills; one-frame calls 0.093 against 0.082 ms at its own 5)
 #endif
+// SGPR cap of k_render_bins (0: the compiler's choice, 106 + spills): below
+// ~100 a wave's SGPR block leaves room in each SIMD's file beside 6 render
+// waves for the waves of a concurrently dispatched kernel (the next call's
+// XORWOW advance), and the stamped instance fits 6 waves' VGPRs
+#ifndef BIH_BINS_SGPR
+#define BIH_BINS_SGPR 0
+#endif
+#if BIH_BINS_SGPR
+#define BIH_BINS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(BIH_BINS_SGPR)))
+#else
+#define BIH_BINS_SGPR_ATTR
+#endif
 template <int LOG2SPP, int MODE = 0>
 __global__ void __launch_bounds__(kThreads, (MODE & kBinsStamped) ? BIH_STAMPED_WAVES : 1) BIH_BINS_OCC
-k_render_bins(const RenderArgs a) {
+BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
     constexpr bool MASK = (MODE & 3) == 1, COST = (MODE & 3) == 2, STAMP = (MODE & kBinsStamped) != 0;
     constexpr uint32_t SPP = 1u << LOG2SPP;
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
@@ -2173,8 +2188,8 @@ k_render_bins(const RenderArgs a) {
     q.rounds = a.shared_grid ? 0u : a.static_rounds;
     q.round = 0;
     q.has_pending = false;
-    q.nf = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
-    q.hs = a.nsplit == 1u ? a.hsplit : 1u;
+    q.ns = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
+    q.hs = a.hsplit;
     q.hv = 0;
     const uint32_t fhv = (a.nframes + q.hs - 1u) / q.hs;   // frames per item of a heavy tile
     uint32_t it = 0;
@@ -2218,15 +2233,15 @@ k_render_bins(const RenderArgs a) {
         const uint64_t tl_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
         const uint4 hb = q.hb;
-        // multi-frame launch: an item covers its tile in frames [f0, nf)
-        const uint32_t fs = a.nsplit > 1 ? it / hb.w : 0u;
-        it -= fs * hb.w;
-        uint32_t f0 = fs * a.fpi;
-        uint32_t nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
-        if (q.hv) {
-            // the band's first hv tiles (measured cost >= kHeavyFactor x the
-            // mean): hs items each, frames [sp * fhv, (sp + 1) * fhv), so that
-            // no tile's frames run for most of the launch on one wave
+        // an item covers its tile in frames [f0, nf) of the launch: the
+        // band's first hv tiles (measured cost >= kHeavyFactor x the mean)
+        // hs items each, frames [sp * fhv, (sp + 1) * fhv), so that no tile's
+        // frames run for most of the launch on one wave; the other live tiles
+        // ns items of a.fpi frames each -- tile-major, so the queue's LPT
+        // order holds for the items; then the background items (`it` past
+        // hb.y: 64 tiles each, every frame)
+        uint32_t f0 = 0, nf = a.nframes;
+        {
             const uint32_t hx = q.hv * q.hs;
             if (it < hx) {
                 const uint32_t j = it / q.hs, sp = it - j * q.hs;
@@ -2234,7 +2249,15 @@ k_render_bins(const RenderArgs a) {
                 f0 = sp * fhv;
                 nf = f0 + fhv < a.nframes ? f0 + fhv : a.nframes;
             } else {
-                it -= hx - q.hv;
+                const uint32_t k = it - hx, nx = (hb.y - q.hv) * q.ns;
+                if (k < nx) {
+                    const uint32_t j = k / q.ns, sp = k - j * q.ns;
+                    it = q.hv + j;
+                    f0 = sp * a.fpi;
+                    nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
+                } else {
+                    it = hb.y + (k - nx);
+                }
             }
         }
         if (it >= hb.y) {
