@@ -765,6 +765,14 @@ static int ensure_rng(bih_tree *tr, size_t P, hipStream_t st) {
 // changes a pixel.
 constexpr uint32_t kStampRun = 3;
 
+static bool share_alternating() {
+    static const bool on = [] {
+        const char *e = getenv("BIH_SHARE_ALTERNATING");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 // k_render_bins' static queue rounds in one-frame launches (BinQueue;
 // BIH_STATIC_ROUNDS for A/B: one-frame calls 1 round 0.0824 ms, 2 0.0822,
 // 3 0.086, 5 0.106 -- a wave cannot hand on its later static items, r05n)
@@ -1597,6 +1605,14 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     for (int k = 0; k < kSlots && (nframes > 1 || kShareOneFrame) && !a.shared_grid && !use_stamps; ++k)
         if (k != slot && tr->used[k] && tr->slot_stream[k] != st && hipEventQuery(tr->evd[k]) == hipErrorNotReady)
             a.shared_grid = 1;
+    // ... and when the caller alternates streams (the last render went to
+    // another one), even if that render has finished: the next call is
+    // likely to follow on another stream, and its advance and first waves
+    // then find free slots instead of waiting for this launch's drain
+    // (BIH_SHARE_ALTERNATING=0: A/B)
+    if (!a.shared_grid && !use_stamps && (nframes > 1 || kShareOneFrame) && share_alternating() &&
+        tr->last_slot >= 0 && tr->slot_stream[tr->last_slot] != st)
+        a.shared_grid = 1;
     rc = bih::launch_render(a, traverse, st, tr->timing ? tr->ev0[slot] : nullptr,
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
