@@ -19,10 +19,13 @@ def main():
     ap.add_argument("--traverse", choices=["anyhit", "reference"], default="anyhit")
     ap.add_argument("--group", type=int, default=1,
                     help="frames per render call (bih_render_device_frames; any-hit only)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="calls rotate over this many streams (the bench's headline shape: 3)")
     a = ap.parse_args()
     import torch
     import bihrt
-    s = torch.cuda.Stream()
+    streams = [torch.cuda.Stream() for _ in range(a.streams)]
+    s = streams[0]
     torch.cuda.set_stream(s)
     tris = bihrt.scenes.soup(a.tris, seed=1)
     d = torch.from_numpy(tris).cuda()
@@ -31,11 +34,13 @@ def main():
     P = a.width * a.height
     out = torch.zeros(a.group * P, dtype=torch.int32, device="cuda")
     trav = bihrt.TRAVERSE_ANYHIT if a.traverse == "anyhit" else bihrt.TRAVERSE_REFERENCE
+    outs = [out] + [torch.zeros(a.group * P, dtype=torch.int32, device="cuda") for _ in streams[1:]]
     for f in range(a.frames):     # --frames render calls
+        s, o = streams[f % len(streams)], outs[f % len(streams)]
         if a.group > 1 and trav == bihrt.TRAVERSE_ANYHIT:
-            r.render_device_frames(out.data_ptr(), f * a.group, a.group, P, stream=s.cuda_stream)
+            r.render_device_frames(o.data_ptr(), f * a.group, a.group, P, stream=s.cuda_stream)
         else:
-            r.render_device(out.data_ptr(), f, traverse=trav, stream=s.cuda_stream)
+            r.render_device(o.data_ptr(), f, traverse=trav, stream=s.cuda_stream)
     torch.cuda.synchronize()
     print("frames", a.frames, "done")
 
