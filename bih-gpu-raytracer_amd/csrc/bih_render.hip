@@ -139,31 +139,64 @@ __global__ void __launch_bounds__(kThreads) k_rng_init(uint32_t *__restrict__ rn
 // more: a gap in the frame sequence.  The Weyl counter d is derived from the
 // frame index, not stored.  Up to two of the powers 2^7 .. 2^13 of `steps`
 // jump through their nibble tables in LDS (40 lookups each, against 128 ..
-// 8192 steps; the frame-jump tables of k_rng_sync), the rest is stepped;
-// grid-stride, so that few blocks load the tables.
+// 8192 steps; the frame-jump tables of k_rng_sync), the rest is stepped.
+// The tables are re-laid in LDS as words 0-3 (one ds_read_b128) + word 4 of
+// each entry; each thread loads its PPT pixels' states before it jumps any
+// (their loads in flight together), PPT pixels a grid's width apart.
+__device__ __forceinline__ void jump_lds4(const uint4 *__restrict__ a, const uint32_t *__restrict__ b, uint32_t x[5]) {
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+#pragma unroll
+    for (int g = 0; g < 40; ++g) {
+        const uint32_t e = g * 16 + ((x[g >> 3] >> ((g & 7) * 4)) & 15u);
+        const uint4 c = a[e];
+        r0 ^= c.x; r1 ^= c.y; r2 ^= c.z; r3 ^= c.w; r4 ^= b[e];
+    }
+    x[0] = r0; x[1] = r1; x[2] = r2; x[3] = r3; x[4] = r4;
+}
+template <int PPT>
 __global__ void __launch_bounds__(kThreads) k_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t P,
                                                           uint32_t steps, const uint32_t *__restrict__ jumps,
                                                           uint32_t k0, uint32_t k1) {
-    __shared__ uint32_t s_nib[2][kRngNibWords];
+    __shared__ uint4 s_a[2][40 * 16];
+    __shared__ uint32_t s_b[2][40 * 16];
     const uint32_t nj = (k0 < 7u) + (k1 < 7u);
     for (uint32_t t = 0; t < nj; ++t) {
         const uint32_t *tab = jumps + (t ? k1 : k0) * kRngNibWords;
-        for (uint32_t k = threadIdx.x; k < kRngNibWords; k += kThreads) s_nib[t][k] = tab[k];
+        for (uint32_t e = threadIdx.x; e < 40 * 16; e += kThreads) {
+            s_a[t][e] = make_uint4(tab[5 * e], tab[5 * e + 1], tab[5 * e + 2], tab[5 * e + 3]);
+            s_b[t][e] = tab[5 * e + 4];
+        }
     }
     if (nj) __syncthreads();
-    for (uint64_t lp = (uint64_t)blockIdx.x * kThreads + threadIdx.x; lp < P; lp += (uint64_t)gridDim.x * kThreads) {
-        uint32_t v[5];
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t lp0 = (uint64_t)blockIdx.x * kThreads + threadIdx.x; lp0 < P; lp0 += stride * PPT) {
+        uint32_t v[PPT][5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) v[i] = src[(uint64_t)i * P + lp];
-        for (uint32_t t = 0; t < nj; ++t) jump_lds(s_nib[t], v);
-#pragma unroll 8
-        for (uint32_t k = 0; k < steps; ++k) {
-            const uint32_t t = v[0] ^ (v[0] >> 2);
-            v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-            v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+        for (int j = 0; j < PPT; ++j) {
+            const uint64_t lp = lp0 + j * stride;
+            if (lp < P) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) v[j][i] = src[(uint64_t)i * P + lp];
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[i];
+        for (int j = 0; j < PPT; ++j) {
+            for (uint32_t t = 0; t < nj; ++t) jump_lds4(s_a[t], s_b[t], v[j]);
+#pragma unroll 8
+            for (uint32_t k = 0; k < steps; ++k) {
+                const uint32_t t = v[j][0] ^ (v[j][0] >> 2);
+                v[j][0] = v[j][1]; v[j][1] = v[j][2]; v[j][2] = v[j][3]; v[j][3] = v[j][4];
+                v[j][4] = (v[j][4] ^ (v[j][4] << 4)) ^ (t ^ (t << 1));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint64_t lp = lp0 + j * stride;
+            if (lp < P) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) dst[(uint64_t)i * P + lp] = v[j][i];
+            }
+        }
     }
 }
 
@@ -3250,15 +3283,22 @@ int launch_rng_advance(const uint32_t *src, uint32_t *dst, uint64_t pixels, uint
             else k1 = (uint32_t)k - 7;
         }
     // with tables: up to 8 pixels per thread (fewer blocks load them), at
-    // least 2048 blocks (a rank's share of the rows is 1/8 of the frame)
-    uint64_t per = kThreads;
-    if (k0 < 7u) {
-        const uint64_t ppt = (pixels + 2048ull * kThreads - 1) / (2048ull * kThreads);
-        per = (ppt < 8 ? ppt : 8) * kThreads;
-    }
+    // least ~2048 blocks (a rank's share of the rows is 1/8 of the frame)
+    uint32_t ppt = 1;
+    if (k0 < 7u)
+        while (ppt < 8u && pixels > 2ull * ppt * 2048ull * kThreads) ppt *= 2;
+    const uint64_t per = (uint64_t)ppt * kThreads;
     const uint32_t blocks = (uint32_t)((pixels + per - 1) / per);
-    hipLaunchKernelGGL(k_rng_advance, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, src,
-                       dst, (uint64_t)pixels, rest, tab + kRngJumpOffset, k0, k1);
+    const uint32_t *jt = tab + kRngJumpOffset;
+    const hipStream_t st = (hipStream_t)stream;
+    if (ppt == 8)
+        hipLaunchKernelGGL(k_rng_advance<8>, dim3(blocks), dim3(kThreads), 0, st, src, dst, (uint64_t)pixels, rest, jt, k0, k1);
+    else if (ppt == 4)
+        hipLaunchKernelGGL(k_rng_advance<4>, dim3(blocks), dim3(kThreads), 0, st, src, dst, (uint64_t)pixels, rest, jt, k0, k1);
+    else if (ppt == 2)
+        hipLaunchKernelGGL(k_rng_advance<2>, dim3(blocks), dim3(kThreads), 0, st, src, dst, (uint64_t)pixels, rest, jt, k0, k1);
+    else
+        hipLaunchKernelGGL(k_rng_advance<1>, dim3(blocks), dim3(kThreads), 0, st, src, dst, (uint64_t)pixels, rest, jt, k0, k1);
     return (int)hipGetLastError();
 }
 
