@@ -891,18 +891,24 @@ def test_stamped_state_panning_sequence_matches_oracle(gpu, bihrt_mod, oracle_mo
     r = bihrt_mod.Renderer(g, w, h)
     sizes = [1, 16, 3, 1, 8, 16, 2, 1, 16, 5]
     stride = h * w
-    frame, calls = 0, []
+    shapes, frame = [], 0
     while frame < 160:
-        n = min(sizes[len(calls) % len(sizes)], 160 - frame)
+        n = min(sizes[len(shapes) % len(sizes)], 160 - frame)
+        shapes.append((frame, n))
+        frame += n
+    # (filled before any render: the library's stream does not order after
+    # torch's default stream)
+    bufs = [torch.full((n * stride,), -1, dtype=torch.int32, device="cuda") for _, n in shapes]
+    torch.cuda.synchronize()
+    calls = []
+    for (frame, n), buf in zip(shapes, bufs):
         cam = _moved_camera(bihrt_mod, w, h, -0.9 + 1.8 * frame / 160, 0.0, 0.0)
-        buf = torch.full((n * stride,), -1, dtype=torch.int32, device="cuda")
         r.camera = cam
         if n == 1:
             r.render_device(buf.data_ptr(), frame)
         else:
             r.render_device_frames(buf.data_ptr(), frame, n, stride)
         calls.append((frame, n, cam, buf))
-        frame += n
     r.sync()
     checked = 0
     for k, (f0, n, cam, buf) in enumerate(calls):
@@ -939,4 +945,43 @@ def test_stamped_state_panning_sequence_matches_oracle(gpu, bihrt_mod, oracle_mo
         r.sync()
         got = out.cpu().numpy().view(np.uint32).reshape(h, w)
         assert np.array_equal(got, ref), (f, kind, int((got != ref).sum()))
+    g.close()
+
+
+@pytest.mark.gpu
+def test_ring_advance_jump_tables_match_oracle(gpu, bihrt_mod, oracle_mod):
+    """Frames on two streams in turn (the XORWOW ring, not the stamped
+    state) with gaps of 48 and 148 frames: the ring's advance jumps the
+    powers 2^7 .. 2^13 of the step count through its nibble tables (one or
+    two of them) and steps the rest (bih_render.hip k_rng_advance); a
+    16-frame call advances by exactly one table.  Every frame equals the
+    oracle's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(20_000, seed=4)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 96, 64
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    stride = h * w
+    plan = [(0, 1), (1, 1), (50, 1), (51, 16), (67, 1), (216, 1), (217, 1)]
+    # (filled before any render: the renders' streams do not order after
+    # torch's default stream)
+    bufs = [torch.full((n * stride,), -1, dtype=torch.int32, device="cuda") for _, n in plan]
+    torch.cuda.synchronize()
+    for k, (f, n) in enumerate(plan):
+        buf = bufs[k]
+        s = streams[k % 2].cuda_stream
+        if n == 1:
+            r.render_device(buf.data_ptr(), f, stream=s)
+        else:
+            r.render_device_frames(buf.data_ptr(), f, n, stride, stream=s)
+    torch.cuda.synchronize()
+    for (f, n), buf in zip(plan, bufs):
+        b = buf.cpu().numpy().view(np.uint32)
+        for j in sorted({0, n - 1}):
+            ref, _ = ot.render(w, h, frame=f + j)
+            got = b[j * stride:(j + 1) * stride].reshape(h, w)
+            assert np.array_equal(got, ref), (f + j, int((got != ref).sum()), int((got == 0xFFFFFFFF).sum()))
     g.close()
