@@ -2274,7 +2274,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
         // order holds for the items; then the background items (`it` past
         // hb.y: 64 tiles each, every frame)
         uint32_t f0 = 0, nf = a.nframes;
-        {
+        if (q.ns > 1u || q.hv) {   // (one item per tile: `it` is the tile's position already)
             const uint32_t hx = q.hv * q.hs;
             if (it < hx) {
                 const uint32_t j = it / q.hs, sp = it - j * q.hs;

@@ -1,0 +1,10 @@
+# Round 5: the item decode skipped for one item per tile -- tests, A/B.
+set -u
+T=${1:-r05ao}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$T
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash tools/gpu_ab5.sh $T 3 base hd || exit 1
