@@ -790,7 +790,8 @@ def test_headline_call_shape_equals_oracle(layout, gpu, bihrt_mod, oracle_mod, s
 
 def test_steady_frame_loop_allocates_nothing(gpu, bihrt_mod):
     """After bih_reserve and one call per camera, a frame loop of 16- and
-    4-frame calls on three streams (the bench's headline shape) makes no
+    4-frame calls on three streams (the bench's headline shape), then calls
+    of 1 to 16 frames on one stream (the stamped XORWOW state), make no
     device allocation (bih_tree_info.device_allocs stays put)."""
     import torch
     tris = bihrt_mod.scenes.soup(200_000, seed=3)
@@ -806,6 +807,15 @@ def test_steady_frame_loop_allocates_nothing(gpu, bihrt_mod):
     f = 5
     for k, m in enumerate([16, 4, 16, 16, 4, 1, 16]):
         r.render_device_frames(outs[k % 3].data_ptr(), f, m, h * w, stream=streams[k % 3].cuda_stream)
+        f += m
+    torch.cuda.synchronize()
+    assert g.info().device_allocs == a0
+    # one stream: the stamped state (reserved too), through a k_rng_sync
+    for m in [1, 1, 1, 16, 1, 16, 16, 16, 4, 1]:
+        if m == 1:
+            r.render_device(outs[0].data_ptr(), f, stream=streams[0].cuda_stream)
+        else:
+            r.render_device_frames(outs[0].data_ptr(), f, m, h * w, stream=streams[0].cuda_stream)
         f += m
     torch.cuda.synchronize()
     assert g.info().device_allocs == a0
