@@ -32,6 +32,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bih-gpu-raytracer_amd"))
 
@@ -100,6 +102,11 @@ def parse():
                          "and decomposition (row bands + gather at N > 1); 0 = skip")
     ap.add_argument("--c5-tris", type=int, default=10_000_000)
     ap.add_argument("--no-reference-leg", action="store_true")
+    ap.add_argument("--dynamic-leg", type=int, default=1,
+                    help="time the per-frame rebuild with geometry that changes every step (two soups)")
+    ap.add_argument("--host-loop", type=int, default=1,
+                    help="N=1: time INTEGRATION.md's host loop (bih_rebuild + bih_render into a host "
+                         "framebuffer), pageable and page-locked")
     ap.add_argument("--no-rebuild-leg", action="store_true",
                     help="skip the leg that rebuilds the BIH every frame (as the reference does)")
     ap.add_argument("--headline-only", action="store_true",
@@ -253,7 +260,9 @@ class Workload:
 
     def step(self, mode, rows, c, frame, traverse, ev=None, rebuild=False, nf=None, m=1, first=0):
         """One render call (call index c): frames frame .. frame+m-1, on
-        stream first + c % nf."""
+        stream first + c % nf.  `rebuild`: bih_rebuild before the render; a
+        callable is called with c first (on the tree's stream: the
+        dynamic_rebuild leg writes the call's soup into the tree's input)."""
         C = self.C
         nf = nf or C.F
         j = first + c % nf
@@ -277,6 +286,8 @@ class Workload:
         if ev is None and not rebuild and not strong:
             render()     # the render alone: no torch work on the stream, no stream context
             return
+        if callable(rebuild):
+            rebuild(c)
         with C.torch.cuda.stream(s):
             if rebuild:
                 self.arrays.rebuild()
@@ -318,10 +329,15 @@ class Workload:
         # costs host time per call, which the row-band shares feel
         evs = [(C.torch.cuda.Event(enable_timing=True), C.torch.cuda.Event(enable_timing=True))
                for _ in calls] if a.step_events else []
+        strong = mode == "strong" and C.world > 1
+        self.timed_calls = []
         t0 = time.perf_counter()
         for i, m in enumerate(calls):
             self.step(mode, rows, c, frame_of(base, k), traverse, evs[i] if evs else None, rebuild=rebuild,
                       nf=nf, m=m, first=first)
+            # (bookkeeping after the call is issued: which buffer holds which frames)
+            self.timed_calls.append({"j": first + c % (nf or C.F), "f0": frame_of(base, k), "m": m, "c": c,
+                                     "rows": rows, "strong": strong})
             k, c = k + m, c + 1
         C.sync_all()
         el = C.max_over_ranks(time.perf_counter() - t0)
@@ -331,6 +347,29 @@ class Workload:
         kms = [x.elapsed_time(y) / m for (x, y), m in zip(evs, calls)] if evs else []
         return el, (sum(kms) / len(kms) if kms else None), fps
 
+    def capture(self, i, qs):
+        """Host copies of frames qs (indices inside the call; -1 = its last) of
+        timed call i (-1 = the last) as the timed loop left them in their
+        output buffer, untimed, after the loop: [(frame, global rows, u32
+        (rows, W))].  Strong decomposition: rank 0's gathered full frames
+        (other ranks hold only their bands: nothing)."""
+        import numpy as np
+        C, H, W = self.C, self.H, self.W
+        tc = self.timed_calls[i]
+        res = []
+        for q in sorted({q % tc["m"] for q in qs}):
+            if tc["strong"]:
+                if C.rank != 0:
+                    continue
+                t = self.frame_img[tc["j"]][q * H * W:(q + 1) * H * W]
+                ys = np.arange(H)
+            else:
+                nr = tc["rows"].nrows
+                t = self.outs[tc["j"]][q * H * W:q * H * W + nr * W]
+                ys = rows_global(tc["rows"], H)
+            res.append((tc["f0"] + q, ys, t.cpu().numpy().view(np.uint32).reshape(ys.size, W).copy()))
+        return res
+
     def close(self):
         self.arrays.close()
         del self.d_tris
@@ -338,6 +377,41 @@ class Workload:
 
 class Ctx:
     pass
+
+
+def rows_global(rows, H):
+    """Global row of each local row of a bih_rows tiling (include/bih.h)."""
+    import numpy as np
+    r = np.arange(rows.nrows)
+    return rows.row0 + (r // rows.band_h) * rows.band_h * rows.band_step + r % rows.band_h
+
+
+class TimedOutputs:
+    """What the timed calls wrote, checked: frames the
+    timer timed, captured right after each leg, go to the oracle on rank 0
+    at N = 1 (`pending`, checked in cpu_baseline: the only place bench.py may
+    run the oracle) or are compared on the GPU side with another render of the
+    same frames (`checks`: the 8 band shares reassembled against the full
+    frame; at N > 1 rank 0's gathered frames against its own one-GPU render)."""
+
+    def __init__(self):
+        self.pending, self.checks = [], []
+
+    def oracle(self, leg, caps, row_step, cam=None, soup="A", W=None, H=None):
+        for f, ys, img in caps:
+            pick = np.arange(0, ys.size, row_step)
+            self.pending.append({"leg": leg, "frame": int(f), "ys": ys[pick], "img": img[pick], "cam": cam,
+                                 "soup": soup, "W": W, "H": H, "row_step": row_step})
+
+    def gpu(self, leg, frame, equal, what):
+        self.checks.append({"leg": leg, "frame": int(frame), "equal": bool(equal), "against": what})
+
+    def summary(self):
+        allc = self.checks
+        return {"all_equal": bool(allc) and all(c["equal"] for c in allc), "checks": allc,
+                "unchecked": [{"leg": p["leg"], "frame": p["frame"]} for p in self.pending],
+                "oracle_seconds": getattr(self, "oracle_seconds", None)}
+
 
 
 def main():
@@ -355,7 +429,6 @@ def main():
     if args.stub:
         stub_worker(args, rank, world)
         return
-    import numpy as np
     import torch
 
     # a rank of an N > 1 run needs its own device (counted, not initialised)
@@ -432,6 +505,55 @@ def main():
     elapsed, kernel_ms, fps = wl.timed(mode, trav, 0)
     value = fps * rays_per_frame * args.steps / elapsed
     allocs_headline = wl.timed_allocs
+    # the frames the headline's timed calls wrote: the first and last frame of
+    # each call (N = 1: against the oracle -- the last frame of the first,
+    # G-frame call on every row, the others on every 16th row; N > 1 strong:
+    # rank 0's gathered frames against its own one-GPU render, below)
+    tout = TimedOutputs()
+    head_caps = []
+    for i in range(len(wl.timed_calls)):
+        head_caps += [(i, cap) for cap in wl.capture(i, [0, -1])]
+    if world == 1:
+        for i, cap in head_caps:
+            full = i == 0 and cap[0] == wl.timed_calls[0]["f0"] + wl.timed_calls[0]["m"] - 1
+            tout.oracle("headline", [cap], 1 if full else args.parity_row_step)
+
+    # The roofline's kernel time, from the timed window's own shape: the same
+    # calls on the same streams again (frames further on), with the library's
+    # HIP events around each render kernel (bih_set_timing; they cost host
+    # time per call, so not in the headline itself).  The union of the
+    # launches' kernel intervals over the window's frames is the kernel time
+    # per frame; overlapping launches (the alternating-stream grid) are not
+    # double counted.
+    window = None
+    if trav == bihrt.TRAVERSE_ANYHIT:
+        r.set_timing(True)
+        elw, _, _ = wl.timed(mode, trav, 10000)
+        r.set_timing(False)
+        n_calls = len(wl.timed_calls)
+        try:
+            hist = r.render_history(min(n_calls, 3)) if n_calls <= 3 else None
+        except bihrt.BihError:
+            hist = None
+        if hist is not None:
+            iv = sorted((float(a), float(b)) for a, b, _ in hist)
+            union, cur = 0.0, None
+            for a0, b0 in iv:
+                if cur is None or a0 > cur[1]:
+                    if cur is not None:
+                        union += cur[1] - cur[0]
+                    cur = [a0, b0]
+                else:
+                    cur[1] = max(cur[1], b0)
+            union += cur[1] - cur[0]
+            frames_w = sum(tc["m"] for tc in wl.timed_calls)
+            window = {"calls": [tc["m"] for tc in wl.timed_calls], "frames": frames_w,
+                      "kernel_intervals_ms": [[round(a, 5), round(b, 5)] for a, b in iv],
+                      "kernel_union_ms": union, "kernel_ms_per_frame": union / frames_w,
+                      "kernel_sum_ms": sum(b - a for a, b in iv),
+                      "ms_per_step": 1e3 * elw / args.steps,
+                      "source": "HIP events around each k_render_bins launch of a replica of the timed window "
+                                "(same calls, streams and shapes; bih_render_history), union of the intervals"}
 
     if args.headline_only:
         args.no_reference_leg = args.no_rebuild_leg = True
@@ -448,6 +570,8 @@ def main():
     serial_leg = None
     if F > 1 and not args.headline_only:
         el5, kms5, fps5 = wl.timed(mode, trav, 4000, nf=1, g=1)
+        if world == 1:
+            tout.oracle("one_in_flight", wl.capture(-1, [-1]), args.parity_row_step)
         serial_leg = {"value": fps5 * rays_per_frame * args.steps / el5, "unit": "rays/s",
                       "ms_per_step": 1e3 * el5 / args.steps, "kernel_ms": kms5,
                       "note": "in_flight 1, one frame per call: each frame starts after the previous one ends"}
@@ -466,10 +590,16 @@ def main():
             arrays.reserve(W, H, SPP, tiling.band_rows(H, args.band, q, Q), G)
         elf, _, _ = wl.timed("weak", trav, 7000)
         full_ms = 1e3 * elf / args.steps
-        shares = []
+        full_cap = wl.capture(-1, [-1])
+        tout.oracle("band_share_full_frame", full_cap, args.parity_row_step)
+        shares, parts = [], []
         for q in range(Q):
-            els, _, _ = wl.timed("weak", trav, 8000 + 1000 * q, rows=tiling.band_rows(H, args.band, q, Q))
+            # (the same frames as the full frame: each share's last frame
+            # reassembles into the full frame's last frame)
+            els, _, _ = wl.timed("weak", trav, 7000, rows=tiling.band_rows(H, args.band, q, Q))
             shares.append(1e3 * els / args.steps)
+            parts.append(wl.capture(-1, [-1])[0])
+        check_shares(tout, "band_share", full_cap[0], parts, H, args.band, Q, tiling)
         share_leg = {"world": Q, "band": args.band, "share_ms_per_step": shares,
                      "full_frame_ms_per_step": full_ms,
                      "projected_efficiency": full_ms / (Q * max(shares)),
@@ -487,6 +617,7 @@ def main():
     if world == 1 and not args.headline_only:
         w2 = Workload(C, bihrt.scenes.torus(), W, H, cam=cam, shapes=shapes)
         el2, _, _ = w2.timed("weak", bihrt.TRAVERSE_ANYHIT, 0)
+        tout.oracle("c2_torus", w2.capture(-1, [-1]), args.parity_row_step, soup="torus")
         c2_leg = {"config": "C2 stand-in: 69,432-triangle closed torus (bunny unavailable offline), 1920x1080, "
                             "4 spp, any-hit, call shape as the headline",
                   "tris": int(w2.tris.shape[0]), "value": rays_per_frame * args.steps / el2, "unit": "rays/s",
@@ -513,11 +644,14 @@ def main():
                 w5.arrays.reserve(W5, H5, SPP, tiling.band_rows(H5, args.band, q, Q), G)
             elf5, _, _ = w5.timed("weak", bihrt.TRAVERSE_ANYHIT, 7000)
             full5 = 1e3 * elf5 / args.steps
-            sh5 = []
+            full5_cap = w5.capture(-1, [-1])
+            sh5, parts5 = [], []
             for q in range(Q):
-                els, _, _ = w5.timed("weak", bihrt.TRAVERSE_ANYHIT, 8000 + 1000 * q,
+                els, _, _ = w5.timed("weak", bihrt.TRAVERSE_ANYHIT, 7000,
                                      rows=tiling.band_rows(H5, args.band, q, Q))
                 sh5.append(1e3 * els / args.steps)
+                parts5.append(w5.capture(-1, [-1])[0])
+            check_shares(tout, "c5_band_share", full5_cap[0], parts5, H5, args.band, Q, tiling)
             share5 = {"world": Q, "band": args.band, "share_ms_per_step": sh5, "full_frame_ms_per_step": full5,
                       "projected_efficiency": full5 / (Q * max(sh5)),
                       "note": f"each of the {Q} ranks' interleaved {args.band}-row bands of the 3840x2160 frame "
@@ -583,6 +717,12 @@ def main():
             wl.step(mode, rows_m, k, frame_of_m(6000, k), trav)
         sync_all()
         el6 = max_over_ranks(time.perf_counter() - t0)
+        kl = k0 + args.steps - 1
+        wl.timed_calls = [{"j": kl % C.F, "f0": frame_of_m(6000, kl), "m": 1, "c": kl, "rows": rows_m,
+                           "strong": mode == "strong" and world > 1}]
+        if world == 1:
+            tout.oracle("moving_camera", wl.capture(-1, [0]), args.parity_row_step,
+                        cam=cams[kl % len(cams)].as_list())
         r.camera = cam
         moving_leg = {"value": fps_m * rays_per_frame * args.steps / el6, "unit": "rays/s",
                       "ms_per_step": 1e3 * el6 / args.steps,
@@ -599,12 +739,102 @@ def main():
         sep = C.F > 1 and os.environ.get("BIH_REBUILD_STREAMS", "") != "all"
         el3, _, fps3 = wl.timed(mode, trav, 2000, rebuild=True, g=1, nf=C.F - 1 if sep else None,
                                 first=1 if sep else 0)
+        if world == 1:
+            tout.oracle("with_rebuild", wl.capture(-1, [0]), args.parity_row_step)
         rebuild_leg = {"value": fps3 * rays_per_frame * args.steps / el3, "unit": "rays/s",
                        "ms_per_step": 1e3 * el3 / args.steps,
                        "build_ms": arrays.info().build_ms,
                        "render_streams": (C.F - 1) if sep else C.F,
                        "note": "step = bih_rebuild + render"
                                + (" + gather" if mode == "strong" and world > 1 else "")}
+
+    # The reference's frame loop with geometry that changes: before every step
+    # the tree's device soup is overwritten (soup A and soup B in turn, the
+    # same size, on the tree's stream), then bih_rebuild -- which must now
+    # read the new tree's header back (no BIH_PARAM_STATIC_SOUP: the content
+    # hash changes) -- and the render, whose camera structures (records,
+    # frustum bins, tile queue) are rebuilt for the new tree.
+    dyn_leg = None
+    if not args.no_rebuild_leg and args.dynamic_leg:
+        tris_b = bihrt.scenes.soup(args.tris, seed=2)
+        d_a = wl.d_tris.clone()
+        d_b = torch.from_numpy(tris_b).to(wl.d_tris.device)
+        torch.cuda.synchronize()
+        arrays.set_param(bihrt.PARAM_STATIC_SOUP, 0)
+
+        def swap_soup(c):
+            with torch.cuda.stream(streams[0]):      # the tree's stream: ordered before the rebuild
+                wl.d_tris.copy_(d_b if c % 2 else d_a)
+
+        sep = C.F > 1
+        el7, _, fps7 = wl.timed(mode, trav, 12000, rebuild=swap_soup, g=1, nf=C.F - 1 if sep else None,
+                                first=1 if sep else 0)
+        last_c = wl.timed_calls[-1]["c"]
+        if world == 1:
+            tout.oracle("dynamic_rebuild", wl.capture(-1, [0]), args.parity_row_step,
+                        soup="B" if last_c % 2 else "A")
+        dyn_leg = {"value": fps7 * rays_per_frame * args.steps / el7, "unit": "rays/s",
+                   "ms_per_step": 1e3 * el7 / args.steps, "soups": "1M soups A (seed 1) and B (seed 2) in turn",
+                   "device_allocs_in_leg": wl.timed_allocs,
+                   "note": "step = overwrite the tree's device soup with the other soup + bih_rebuild (header "
+                           "read back: the soup changed) + render; the camera structures are rebuilt for "
+                           "every new tree (src/App.cpp:174-183 -> src/Renderer.cpp:415-501 with moving "
+                           "geometry)"}
+        # soup A back, and the tree of soup A
+        swap_soup(0)
+        arrays.rebuild()
+        arrays.set_param(bihrt.PARAM_STATIC_SOUP, 1)
+        torch.cuda.synchronize()
+        del d_a, d_b
+        if world == 1:
+            C.tris_b = tris_b
+
+    # INTEGRATION.md's C loop: bih_rebuild + bih_render into a host
+    # framebuffer, one frame per call (bih_build tree: the library's own copy
+    # of the soup).  Pageable framebuffer, then the same buffer page-locked
+    # once (bih_host_register): bih_render's device-to-host copy then runs at
+    # DMA rate.
+    host_leg = None
+    if world == 1 and not args.headline_only and args.host_loop:
+        hg = bihrt.GPUArrayManager(tris)
+        hr = bihrt.Renderer(hg, W, H, spp=SPP, seed=1984, camera=cam)
+        fbuf = np.zeros((H, W), np.uint32)
+        hg.reserve(W, H, SPP, None, 1)
+        res_h = {}
+        f = 15000
+        for kind, reb in (("pageable", True), ("pinned", True), ("pinned_render_only", False),
+                          ("pageable_render_only", False)):
+            if kind.startswith("pinned"):
+                bihrt.host_register(fbuf)
+            for k in range(max(3, args.warmup)):
+                if reb:
+                    hg.rebuild()
+                hr.render(f, out=fbuf)
+                f += 1
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                if reb:
+                    hg.rebuild()
+                hr.render(f, out=fbuf)
+                f += 1
+            elh = time.perf_counter() - t0
+            if kind in ("pageable", "pinned"):
+                tout.oracle(f"host_loop_{kind}", [(f - 1, np.arange(H), fbuf.copy())], args.parity_row_step)
+            res_h[kind] = {"ms_per_step": 1e3 * elh / args.steps, "value": rays_per_frame * args.steps / elh}
+            if kind.startswith("pinned"):
+                bihrt.host_unregister(fbuf)
+        host_leg = dict(res_h)
+        host_leg.update({
+            "pinned_speedup": res_h["pageable"]["ms_per_step"] / res_h["pinned"]["ms_per_step"],
+            "pinned_speedup_render_only": (res_h["pageable_render_only"]["ms_per_step"] /
+                                           res_h["pinned_render_only"]["ms_per_step"]),
+            "unit": "rays/s",
+            "note": "step = bih_rebuild + bih_render (one frame, 8.3 MB into a host framebuffer, synchronous) "
+                    "as INTEGRATION.md's C loop; pinned = the same buffer after bih_host_register; "
+                    "*_render_only: bih_render alone (reference: D2D copy into the GL buffer, "
+                    "src/Renderer.cpp:645-655)"})
+        hg.close()
+        del hg, hr
 
     # the dominant kernel's launch duration: HIP events the library records
     # on the render stream right around the render kernel (bih_last_render_ms),
@@ -675,16 +905,50 @@ def main():
                "compulsory_formula": "48 x list entries + 64 x intersector calls + 2 x 20 x pixels "
                                      "(XORWOW in, out) + frames per launch x 4 x pixels",
                "compulsory_gbs": comp_bytes / (launch_ms * 1e-3) / 1e9}
+        if window:
+            # per frame over the timed window's own kernel time (union of its launches)
+            kpf = window["kernel_ms_per_frame"]
+            alg["bytes_per_frame"] = alg_bytes / gl
+            alg["window_gbs"] = alg_bytes / gl / (kpf * 1e-3) / 1e9
+            alg["window_compulsory_gbs"] = comp_bytes / gl / (kpf * 1e-3) / 1e9
+    # the issue roofline of the same kernel: VALU wave-instructions (PMC,
+    # SQ_INSTS_VALU per launch of the headline shape) at 2 cycles each on a
+    # SIMD (a wave64 VALU op issues over 2 cycles: MI355X_MICROARCH.md), over
+    # 1024 SIMDs x 2.4 GHz for the kernel time per frame
+    issue = None
+    sq = (traffic or {}).get("sq")
+    if sq and trav == 0 and (window or launch_ms):
+        gl = G
+        kpf = window["kernel_ms_per_frame"] if window else launch_ms / gl
+        valu_f, salu_f = sq["SQ_INSTS_VALU"] / gl, sq["SQ_INSTS_SALU"] / gl
+        issue = {"valu_per_frame": valu_f, "salu_per_frame": salu_f,
+                 "valu_issue_frac": valu_f * 2 / (1024 * 2.4e9 * kpf * 1e-3),
+                 "kernel_ms_per_frame": kpf,
+                 "formula": "SQ_INSTS_VALU per frame x 2 cycles / (1024 SIMDs x 2.4 GHz x kernel ms per frame)",
+                 "source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU per dispatch of the headline's "
+                           f"{G}-frame k_render_bins launches (tools/prof_render.py)"}
     bins = {"usable": bool(bst.usable), "tiles": [bst.tiles_x, bst.tiles_y],
             "list_entries": int(bst.list_entries), "global_entries": int(bst.global_entries),
             "entry_bytes": 48,
             "note": "frustum bins of the bench camera (bih_bins_get_stats): per 4x4-pixel tile the "
                     "triangles whose edge pre-test a sample of the tile can pass"}
 
+    # N > 1 strong: rank 0's gathered headline frames against rank 0's own
+    # one-GPU render of the same frames (whole frames, one call each)
+    if world > 1 and mode == "strong" and rank == 0:
+        full_rows = tiling.band_rows(H, args.band, 0, 1)
+        arrays.reserve(W, H, SPP, full_rows, G)
+        for i, (f, ys, img) in head_caps:
+            r.render_device_frames(out.data_ptr(), f, 1, H * W, rows=full_rows, stream=sptr)
+            torch.cuda.synchronize()
+            ref = out[: H * W].cpu().numpy().view(np.uint32).reshape(H, W)
+            tout.gpu("headline", f, np.array_equal(img, ref),
+                     "rank 0's gathered frame vs its own one-GPU render of the same frame, every pixel")
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu, parity = cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np)
+        cpu, parity = cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np, tout, getattr(C, "tris_b", None))
 
     rccl = None
     if backend == "nccl":
@@ -692,6 +956,7 @@ def main():
             rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
         except Exception:
             rccl = None
+    ach = (alg["window_gbs"] if alg and "window_gbs" in alg else alg["gbs"] if alg else achieved)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -733,11 +998,13 @@ def main():
             # algorithmic bytes); `frac_compulsory` prices the bytes that must
             # cross HBM once per launch.  What limits the kernel is `limiter`.
             "roofline": {
-                "bound": "hbm", "achieved": alg["gbs"] if alg else achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (alg["gbs"] if alg else achieved) / HBM_PEAK_GBS
-                        if (alg or achieved is not None) else None,
+                "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS if ach is not None else None,
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "achieved_source": ("algorithmic bytes per launch (roofline.algorithmic) / launch_ms" if alg else
+                "achieved_source": ("algorithmic bytes per frame (roofline.algorithmic) / kernel ms per frame of "
+                                    "the timed window's shape (roofline.window: union of its launches' HIP-event "
+                                    "intervals)" if (alg and window) else
+                                    "algorithmic bytes per launch (roofline.algorithmic) / launch_ms" if alg else
                                     "measured bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) / launch_ms"
                                     if achieved is not None else "traffic not measured"),
                 "algorithmic": alg,
@@ -746,6 +1013,9 @@ def main():
                 "achieved_measured": achieved,
                 "frac_measured": achieved / HBM_PEAK_GBS if achieved is not None else None,
                 "launch_ms": launch_ms,
+                "window": window,
+                "issue": issue,
+                "frac_isolated_launches": alg["gbs"] / HBM_PEAK_GBS if alg else None,
                 "fallback_ms": (sum(tails_iso) / len(tails_iso)) if tails_iso else None,
                 "frames_per_launch": G if trav == 0 else 1,
                 "launch_ms_source": (f"HIP events around the render kernel on its stream "
@@ -776,6 +1046,8 @@ def main():
             "cpu_baseline": cpu,
             "other_traversal": ref_leg,
             "with_rebuild": rebuild_leg,
+            "dynamic_rebuild": dyn_leg,
+            "host_loop": host_leg,
             "moving_camera": moving_leg,
             "one_in_flight": serial_leg,
             "other_decomposition": side_leg,
@@ -787,6 +1059,10 @@ def main():
         if parity is not None:
             res["parity_timed_call_shape"] = parity
             res["parity_sample_rows_equal"] = parity["all_equal"]
+        # what the timed calls themselves wrote
+        ts = tout.summary()
+        res["timed_outputs_equal"] = ts["all_equal"] if ts["checks"] else None
+        res["timed_outputs"] = ts
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.barrier()
@@ -842,6 +1118,20 @@ def whitted(args, bihrt, torch, arrays, SPP, sptr):
                     "oracle (tests/test_whitted.py)"}
 
 
+def check_shares(tout, leg, full, parts, H, band, Q, tiling):
+    """The Q band shares' last frames (each rendered alone, timed) laid out
+    in frame order (tiling.assemble) equal the full-frame leg's last frame,
+    the same frame index, on every pixel."""
+    f, _, img = full
+    frames = {p[0] for p in parts}
+    ok = frames == {f} and all(p[2].shape[0] == p[1].size for p in parts)
+    if ok:
+        got = tiling.assemble([p[2] for p in parts], H, band, Q)
+        ok = bool(np.array_equal(got, img))
+    tout.gpu(leg, f, ok, f"the {Q} shares' last frames reassembled (tiling.assemble) vs the full-frame "
+                         "leg's last frame, every pixel")
+
+
 def parallelism(mode, band, world):
     if world == 1:
         return "1 GPU, whole frames"
@@ -871,7 +1161,7 @@ def cpu_threads(args):
     return n, aff, omp
 
 
-def cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np):
+def cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np, tout=None, tris_b=None):
     """The oracle (strict-IEEE C restatement of the reference's render path,
     oracle/bih_oracle.c) timed on the host, on bounded row samples of frame 0
     of the same workload:
@@ -926,6 +1216,31 @@ def cpu_baseline(args, tris, wl, trav, W, H, SPP, torch, np):
               for f, row0, step, img in imgs]
     parity = {"call": f"bih_render_device_frames, frames 0..{G - 1} in one call", "checks": checks,
               "all_equal": all(c["equal"] for c in checks)}
+    # the frames the timed legs wrote (TimedOutputs.pending), against the
+    # oracle of their soup, camera and frame
+    if tout is not None and tout.pending:
+        trees = {"A": ot}
+        t0 = time.perf_counter()
+        for p in tout.pending:
+            key = p["soup"]
+            if key not in trees:
+                import bihrt
+                trees[key] = oracle.OracleTree(tris_b if key == "B" else bihrt.scenes.torus())
+            t = trees[key]
+            ys = p["ys"]
+            step = int(ys[1] - ys[0]) if ys.size > 1 else 1
+            cam = np.array(p["cam"], np.float32) if p["cam"] is not None else None
+            if ys.size and np.array_equal(ys, ys[0] + step * np.arange(ys.size)):
+                ref, _ = t.render(W, H, spp=SPP, frame=p["frame"], cam=cam, rows=(int(ys[0]), int(ys.size), step),
+                                  mode=oracle.MODE_GPU_ANYHIT, threads=threads)
+            else:
+                ref = np.concatenate([t.render(W, H, spp=SPP, frame=p["frame"], cam=cam, rows=(int(y), 1, 1),
+                                               mode=oracle.MODE_GPU_ANYHIT, threads=threads)[0] for y in ys])
+            rows_txt = "every row" if step == 1 and ys.size == H else f"rows {int(ys[0])}::{step}"
+            tout.gpu(p["leg"], p["frame"], np.array_equal(ref, p["img"]),
+                     f"oracle (soup {key}{', moved camera' if cam is not None else ''}), {rows_txt}")
+        tout.oracle_seconds = time.perf_counter() - t0
+        tout.pending = []
     main = legs["reference_walk"]
     res = {"value": main["value"], "unit": "rays/s", "cores": main["cores"], "kind": "port",
            "sample": main["sample"] + ", oracle/bih_oracle.c reference walk (TraverseTree rules), "
@@ -961,9 +1276,10 @@ def measure_traffic(args):
     # traffic driver rotates its calls over as many streams (and keeps the
     # ring even if it did not)
     env["BIH_STAMPED"] = "0"
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        out = os.path.join(tmp, ctr)
-        cmd = [prof, "--pmc", ctr, "-d", out, "-o", ctr, "--output-format", "csv", "--",
+    sq = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU SQ_INSTS_SALU"):
+        out = os.path.join(tmp, ctr.split()[0])
+        cmd = [prof, "--pmc"] + ctr.split() + ["-d", out, "-o", ctr.split()[0], "--output-format", "csv", "--",
                sys.executable, os.path.join(ROOT, "tools", "prof_render.py"), "--frames", "6",
                "--tris", str(args.tris), "--width", str(args.width), "--height", str(args.height),
                "--spp", str(args.spp), "--traverse", traverse, "--group", str(max(1, args.group)),
@@ -971,8 +1287,12 @@ def measure_traffic(args):
         try:
             p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=300)
         except (OSError, subprocess.TimeoutExpired):
+            if ctr.startswith("SQ"):
+                continue
             return None
         if p.returncode != 0:
+            if ctr.startswith("SQ"):
+                continue
             return None
         # the dominant render kernel: k_render_bins (any-hit with frustum
         # bins; the plain instance <L, 0>, not the first launch's cost
@@ -991,23 +1311,29 @@ def measure_traffic(args):
                 else:
                     continue
                 did = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(per))
-                per[(key, did)] = per.get((key, did), 0.0) + float(row["Counter_Value"])
-        vals = {}
-        for (key, _), v in sorted(per.items(), key=lambda kv: int(kv[0][1]) if kv[0][1].isdigit() else 0):
-            vals.setdefault(key, []).append(v)
-        key = "k_render_bins" if "k_render_bins" in vals else "k_render_packet_asm"
-        if not vals.get(key):
-            return None
-        kernel_name = key
-        # (the first launch reads the camera's structures from HBM for the
-        # first time: left out when there are others)
-        v = vals[key][1:] if len(vals[key]) > 2 else vals[key]
-        res[ctr] = sum(v) / len(v)
+                cname = row.get("Counter_Name", ctr)
+                per[(key, did, cname)] = per.get((key, did, cname), 0.0) + float(row["Counter_Value"])
+        for cname in ctr.split():
+            vals = {}
+            for (key, _, cn), v in sorted(per.items(), key=lambda kv: int(kv[0][1]) if kv[0][1].isdigit() else 0):
+                if cn == cname:
+                    vals.setdefault(key, []).append(v)
+            key = "k_render_bins" if "k_render_bins" in vals else "k_render_packet_asm"
+            if not vals.get(key):
+                if ctr.startswith("SQ"):
+                    continue
+                return None
+            kernel_name = key
+            # (the first launch reads the camera's structures from HBM for the
+            # first time: left out when there are others)
+            v = vals[key][1:] if len(vals[key]) > 2 else vals[key]
+            (sq if ctr.startswith("SQ") else res)[cname] = sum(v) / len(v)
     shutil.rmtree(tmp, ignore_errors=True)
     fetch = 2.0 * res["FETCH_SIZE"] * 1024.0
     write = res["WRITE_SIZE"] * 1024.0
     return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
             "raw_kb": res, "correction": "FETCH_SIZE x2 (gfx950), KB x 1024", "kernel": kernel_name,
+            "sq": sq if len(sq) == 2 else None,
             "bin_counters": bin_counters(args, env)}
 
 

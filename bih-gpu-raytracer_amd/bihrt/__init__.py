@@ -145,11 +145,17 @@ class Renderer:
         self.camera = camera if camera is not None else camera_reference(w, h)
         self.frame = 0
 
-    def render(self, frame: int | None = None, rows: tuple[int, int] | None = None) -> np.ndarray:
-        """One frame into a host (h, w) uint32 image (0x00BBGGRR, row 0 = bottom)."""
+    def render(self, frame: int | None = None, rows: tuple[int, int] | None = None,
+               out: np.ndarray | None = None) -> np.ndarray:
+        """One frame into a host (h, w) uint32 image (0x00BBGGRR, row 0 = bottom).
+        `out`: a caller-owned C-contiguous (nrows, w) uint32 framebuffer to render
+        into (a frame loop reuses it; see host_register)."""
         f = self.frame if frame is None else frame
         row0, nrows = rows if rows is not None else (0, self.h)
-        out = np.zeros((nrows, self.w), np.uint32)
+        if out is None:
+            out = np.zeros((nrows, self.w), np.uint32)
+        elif out.shape != (nrows, self.w) or out.dtype != np.uint32 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous ({nrows}, {self.w}) uint32 array")
         fb = Framebuffer(self.w, self.h, self.spp, f, self.seed, out.ctypes.data)
         sc = C.byref(self.arrays.scene) if self.arrays.scene is not None else None
         if rows is None:
@@ -211,6 +217,14 @@ class Renderer:
         check(load().bih_whitted_work(self.arrays.handle, rays, nodes, tris), "bih_whitted_work")
         return {"rays": list(rays), "nodes": list(nodes), "tris": list(tris)}
 
+    def render_history(self, n: int) -> np.ndarray:
+        """(n, 3) ms {kernel start, kernel end, end of the render's work} of the
+        last n renders (issued with set_timing on), after the oldest one's kernel
+        start (bih_render_history)."""
+        t = (C.c_double * (3 * n))()
+        check(load().bih_render_history(self.arrays.handle, n, t), "bih_render_history")
+        return np.array(t[:], np.float64).reshape(n, 3)
+
     def sync(self, stream: int | None = None):
         check(load().bih_sync(self.arrays.handle, C.c_void_p(stream or 0)), "bih_sync")
 
@@ -230,6 +244,17 @@ class Renderer:
         check(load().bih_last_render_times(self.arrays.handle, C.byref(k), C.byref(t)),
               "bih_last_render_times")
         return k.value, t.value
+
+
+def host_register(arr: np.ndarray):
+    """Page-locks a host framebuffer (bih_host_register) so that bih_render's
+    device-to-host copy into it runs at DMA rate; host_unregister before it is
+    freed."""
+    check(load().bih_host_register(C.c_void_p(arr.ctypes.data), arr.nbytes), "bih_host_register")
+
+
+def host_unregister(arr: np.ndarray):
+    check(load().bih_host_unregister(C.c_void_p(arr.ctypes.data)), "bih_host_unregister")
 
 
 def load_obj(path: str) -> np.ndarray:
@@ -274,7 +299,7 @@ def write_ppm(path: str, img: np.ndarray):
         f.write(np.ascontiguousarray(rgb).tobytes())
 
 
-__all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "Camera", "Rows", "BihError", "camera_reference",
+__all__ = ["GPUArrayManager", "Renderer", "Model", "load_obj", "host_register", "host_unregister", "Camera", "Rows", "BihError", "camera_reference",
            "camera_ray_bound", "device_count", "unpack_rgba", "write_ppm", "scenes", "TRAVERSE_ANYHIT",
            "TRAVERSE_REFERENCE", "PARAM_ITEM_TILES", "PARAM_PAIR_CAP", "PARAM_BINS_CAP", "PARAM_FORCE_FALLBACK",
            "PARAM_WHITTED_COUNTERS", "PARAM_STATIC_SOUP", "PARAM_TEST_ALLOC_FAIL"]

@@ -140,11 +140,15 @@ def load():
     L.bih_reserve.argtypes = [vp, u32, u32, u32, C.POINTER(Rows), u32]
     L.bih_tree_set_param.argtypes = [vp, i32, u64]
     L.bih_whitted_work.argtypes = [vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64)]
+    L.bih_host_register.argtypes = [vp, C.c_size_t]
+    L.bih_host_unregister.argtypes = [vp]
+    L.bih_render_history.argtypes = [vp, u32, C.POINTER(C.c_double)]
     for name in ("bih_camera_reference", "bih_camera_ray_bound", "bih_scene_load_obj", "bih_build", "bih_build_device", "bih_rebuild",
                  "bih_tree_get_info", "bih_tree_export", "bih_render", "bih_render_rows",
                  "bih_render_device", "bih_sync", "bih_last_render_ms", "bih_last_render_times", "bih_set_timing",
                  "bih_render_whitted_device", "bih_render_whitted", "bih_render_device_frames",
-                 "bih_bins_get_stats", "bih_reserve", "bih_tree_set_param", "bih_whitted_work"):
+                 "bih_bins_get_stats", "bih_reserve", "bih_tree_set_param", "bih_whitted_work",
+                 "bih_host_register", "bih_host_unregister", "bih_render_history"):
         getattr(L, name).restype = i32
     _lib = L
     return L

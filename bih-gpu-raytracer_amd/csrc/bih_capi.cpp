@@ -99,6 +99,7 @@ struct CamSet {
     // cost_key: the next queue of those rows is built from them
     bool cost_known = false;
     uint32_t cost_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t cost_pending[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // q_key of a measuring launch being prepared
     hipEvent_t ev_bins = nullptr;    // after the readback of the last bins build's {gcount, status, total}
 };
 
@@ -155,6 +156,7 @@ struct bih_tree {
     bool used[kSlots] = {};
     bool timing = false;             // bih_set_timing: record ev0/ev1/ev2 around each render
     bool last_timed = false;
+    bool slot_timed[kSlots] = {};    // the slot's last render recorded ev0/ev1/ev2
     bool built = false;              // a build completed (t.content is its soup's hash)
     int slot = 0;                    // slot of the next render
     int last_slot = -1;              // slot of the last render
@@ -222,6 +224,7 @@ struct bih_tree {
     size_t wh_rays = 0;              // queue capacity (rays)
     uint64_t wh_last_rays = 0;       // rays of the last Whitted render (its buffer layout)
     int wh_last_slot = -1;           // its slot (evd), when it ran with work counters
+    int wh_prev_slot = -1;           // the last Whitted launch's slot (its evd orders the next mask render)
     unsigned long long *wh_mask = nullptr;   // primary samples' hit masks per tile (bounce 0 through the bins)
     size_t wh_mask_cap = 0;                  // tiles
 };
@@ -800,8 +803,20 @@ static bool stamps_enabled() {
     return on;
 }
 
-static int ensure_stamps(bih_tree *tr, size_t ntiles) {
+static int unstamp(bih_tree *tr, hipStream_t st);
+
+// Grows the stamp array.  A stamped run in progress is first folded back into
+// the ring (unstamp: every pixel's state at next_frame, rng_cur), so that the
+// next render continues the sequence from the right state instead of the
+// buffer stamped mode started from.
+static int ensure_stamps(bih_tree *tr, size_t ntiles, hipStream_t st) {
     if (tr->stamp_cap >= ntiles) return BIH_OK;
+    if (tr->stamped) {
+        int rc = unstamp(tr, st);
+        if (rc) return rc;
+        const hipError_t e = hipStreamSynchronize(st);   // the sync kernel reads the stamps
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     int rc = drain_renders(tr);
     if (rc) return rc;
     if (tr->stamps) (void)hipFree(tr->stamps);
@@ -1004,7 +1019,9 @@ static int build_bins(bih_tree *tr, CamSet &c, const bih_camera *cam, const floa
                  s_off = al((nb + 1) * 4),
                  s_g = al(8 * 4), s_glist = al((size_t)n * 4 + 4),
                  s_part = al(bih::scan_partials_words((uint32_t)nb) * 4),
-                 s_rec = al((size_t)n * 64), s_path = al((size_t)U * 256),
+                 // (the path table sized for U = N, its largest: a rebuilt tree of another soup
+                 // of the same size fits the same layout, no allocation per changed soup)
+                 s_rec = al((size_t)n * 64), s_path = al((size_t)n * 256),
                  s_gent = al((size_t)4097 * kEntryBytes), s_live = al((size_t)n * 4 + 4), s_bmask = al((size_t)nblk * 32),
                  s_bcnt = al((size_t)nblk * 4 + 4), s_boff = al((size_t)nblk * 4 + 8),
                  s_bpart = al(bih::scan_partials_words(nblk) * 4),
@@ -1206,10 +1223,10 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     }
     // (measured from the camera's second render on: a camera that moves every
     // frame never renders twice, and the measuring instance costs ~1.4x)
+    // (cost_known is set once the measuring launch is issued: render_device_impl)
     if (!c.q_cost && !measured && cost_queue_enabled() && c.uses >= 1) {
         a.bin_cost = c.bins.cost;
-        memcpy(c.cost_key, key, sizeof key);
-        c.cost_known = true;
+        memcpy(c.cost_pending, key, sizeof key);
     }
     // heavy tiles: as many items as the others (RenderArgs::nsplit), or --
     // with measured costs -- 2 or 4 times as many, up to one frame each
@@ -1265,7 +1282,8 @@ constexpr int kRenderPerFrame = 1;
 static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
                               uint32_t frame, uint64_t seed, const bih_rows *rows_in, uint32_t traverse,
                               uint32_t *d_out, uint32_t *d_ray_stats, void *stream, uint32_t nframes,
-                              uint64_t out_stride, unsigned long long *hit_mask = nullptr) {
+                              uint64_t out_stride, unsigned long long *hit_mask = nullptr,
+                              bool have_lock = false) {
     if (!tr || !cam || !d_out || w == 0 || h == 0 || spp == 0 || traverse > 1) return BIH_ERR_INVALID;
     bih_rows rows = rows_in ? *rows_in : bih_rows{0, h, h, 1};
     if (rows.nrows == 0) return BIH_OK;
@@ -1277,7 +1295,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     if (ylast >= h) return BIH_ERR_INVALID;
     if ((uint64_t)h * w > 0xFFFFFFFFull) return BIH_ERR_TOO_LARGE;
     DeviceGuard g(tr->t.device);
-    std::lock_guard<std::mutex> lk(tr->mu);
+    // (a Whitted call holds the lock across its mask render and its launch)
+    std::unique_lock<std::mutex> lk(tr->mu, std::defer_lock);
+    if (!have_lock) lk.lock();
     hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     // the camera's set of per-camera structures: the one built for this
     // camera, else the next one after the latest render's (with two sets:
@@ -1331,6 +1351,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
     if (bih::render_uses_prim(spp) && tr->t.n > 0) {
         const size_t need = bih::prim_bytes(tr->t.n, n_int);
         const bool grow = c.prim_cap < need;
+        // (grown to the size of U = N, the most a soup of N triangles can have:
+        // trees of other soups of that size reuse it)
+        const size_t alloc = bih::prim_bytes(tr->t.n, tr->t.n > 0 ? tr->t.n - 1 : 0);
         if (grow || !c.prim_valid || memcmp(ob, c.prim_origin, sizeof ob) != 0) {
             // rewritten in place: after every render still reading the records
             rc = wait_set_readers(tr, ci, st);
@@ -1342,9 +1365,9 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
             if (c.prim) (void)hipFree(c.prim);
             c.prim = nullptr;
             c.prim_cap = 0;
-            e = tree_malloc(tr, &c.prim, need);
+            e = tree_malloc(tr, &c.prim, std::max(need, alloc));
             if (e != hipSuccess) return map_hip((int)e);
-            c.prim_cap = need;
+            c.prim_cap = std::max(need, alloc);
             c.prim_valid = false;
         }
         // the frustum bins' build computes the records itself (k_cam_tris)
@@ -1459,7 +1482,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         uint32_t tw = 0, th = 0;
         tile_shape(spp, &tw, &th);
         const size_t ntiles = (size_t)((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
-        rc = ensure_stamps(tr, ntiles);
+        rc = ensure_stamps(tr, ntiles, st);
         if (rc) return rc;
         for (int k = 0; k < kSlots; ++k)
             if (tr->used[k]) {
@@ -1523,10 +1546,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         a.bin_gstat = c.bins.gcount + 1;
         rc = prepare_bin_queue(tr, c, ci, w, h, spp, rows, slot, st, a, nframes);
         if (rc) return rc;
-        if (hit_mask && a.bin_cost) {   // (the mask pass's kernel does not measure)
-            a.bin_cost = nullptr;
-            c.cost_known = false;
-        }
+        if (hit_mask) a.bin_cost = nullptr;   // (the mask pass's kernel does not measure)
     } else {
         // the cost order pays off for the long BIH walks; with the bins the
         // packets are short and the order's own launch costs more (A/B)
@@ -1617,6 +1637,11 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
                             tr->timing ? tr->ev1[slot] : nullptr);
     if (rc) return map_hip(rc);
     if (use_bins) tr->q_par[slot] ^= 1u;   // this launch zeroes the other set for the next
+    if (a.bin_cost) {
+        // the next queue of these rows is ordered by the costs this launch writes
+        memcpy(c.cost_key, c.cost_pending, sizeof c.cost_key);
+        c.cost_known = true;
+    }
     if (use_stamps) {
         e = hipEventRecord(tr->ev_rng, st);
         if (e != hipSuccess) return map_hip((int)e);
@@ -1627,6 +1652,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         if (e != hipSuccess) return map_hip((int)e);
     }
     tr->last_timed = tr->timing;
+    tr->slot_timed[slot] = tr->timing;
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
@@ -1691,7 +1717,7 @@ int bih_reserve(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_ro
     const uint32_t ntiles = ((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
     for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles);
     if (!rc) rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, (size_t)ntiles * max_frames, 8);
-    if (!rc && stamps_enabled()) rc = ensure_stamps(tr, ntiles);
+    if (!rc && stamps_enabled()) rc = ensure_stamps(tr, ntiles, tr->stream);
     if (rc) return rc;
     return map_hip((int)hipStreamSynchronize(tr->stream));
 }
@@ -1755,6 +1781,10 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     // count by at most one 64-ray fetch per wave of its grid (<= 2^20 lanes)
     if ((uint64_t)h * w * spp > 0xFFFFFFFFull - (1ull << 20)) return BIH_ERR_TOO_LARGE;
     DeviceGuard g(tr->t.device);
+    // one lock over the mask render and the Whitted launch: no other call
+    // through this tree slips in between
+    std::lock_guard<std::mutex> lk(tr->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     // Bounce 0 through the frustum bins: the any-hit render of the same
     // frame (the primary render's kernels) leaves per tile the mask of its
     // samples that hit; only those enter the closest-hit walk of bounce 0 (a
@@ -1767,31 +1797,34 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
         const char *e = getenv("BIH_WH_BINS");
         return !(e && e[0] == '0');
     }();
-    if (wh_bins && bins_enabled() && spp <= 64 && (spp & (spp - 1)) == 0 && tr->t.u > 1) {
+    // With work counters on, every primary sample is walked, so that the
+    // counts equal the oracle's on every frame.
+    if (wh_bins && bins_enabled() && !tr->prm.wh_counters && spp <= 64 && (spp & (spp - 1)) == 0 &&
+        tr->t.u > 1) {
         uint32_t tw = 0, th = 0;
         tile_shape(spp, &tw, &th);
         mask_tiles_x = (w + tw - 1) / tw;
         const size_t ntiles = (size_t)mask_tiles_x * ((rows.nrows + th - 1) / th);
-        {
-            std::lock_guard<std::mutex> lk(tr->mu);
-            if (tr->wh_mask_cap < ntiles) {
-                int rc = drain_renders(tr);
-                if (rc) return rc;
-                if (tr->wh_mask) (void)hipFree(tr->wh_mask);
-                tr->wh_mask = nullptr;
-                tr->wh_mask_cap = 0;
-                hipError_t e = tree_malloc(tr, &tr->wh_mask, ntiles * 8);
-                if (e != hipSuccess) return map_hip((int)e);
-                tr->wh_mask_cap = ntiles;
-            }
+        if (tr->wh_mask_cap < ntiles) {
+            int rc = drain_renders(tr);
+            if (rc) return rc;
+            if (tr->wh_mask) (void)hipFree(tr->wh_mask);
+            tr->wh_mask = nullptr;
+            tr->wh_mask_cap = 0;
+            hipError_t e = tree_malloc(tr, &tr->wh_mask, ntiles * 8);
+            if (e != hipSuccess) return map_hip((int)e);
+            tr->wh_mask_cap = ntiles;
+        } else if (tr->wh_prev_slot >= 0 && tr->used[tr->wh_prev_slot]) {
+            // the mask is rewritten in place: after the last Whitted launch
+            // (its k_wh_gen reads the previous mask), whatever stream it ran on
+            hipError_t e = hipStreamWaitEvent(st, tr->evd[tr->wh_prev_slot], 0);
+            if (e != hipSuccess) return map_hip((int)e);
         }
         const int mrc = render_device_impl(tr, cam, w, h, spp, frame, seed, &rows, BIH_TRAVERSE_ANYHIT, d_out,
-                                           nullptr, stream, 1, 0, tr->wh_mask);
+                                           nullptr, stream, 1, 0, tr->wh_mask, true);
         if (mrc == BIH_OK) mask = tr->wh_mask;
         else if (mrc != kRenderPerFrame) return mrc;
     }
-    std::lock_guard<std::mutex> lk(tr->mu);
-    hipStream_t st = stream ? (hipStream_t)stream : tr->stream;
     // the queues are shared by every Whitted render of this tree: order after
     // every render in flight (and after the last writer of the RNG ring)
     int rc = wait_renders(tr, st);
@@ -1857,11 +1890,13 @@ int bih_render_whitted_device(const bih_tree *ctr, const bih_camera *cam, uint32
     if (rc) return map_hip(rc);
     tr->wh_last_rays = rays;
     tr->wh_last_slot = count ? slot : -1;
+    tr->wh_prev_slot = slot;
     if (tr->timing) {
         e = hipEventRecord(tr->ev2[slot], st);
         if (e != hipSuccess) return map_hip((int)e);
     }
     tr->last_timed = tr->timing;
+    tr->slot_timed[slot] = tr->timing;
     e = hipEventRecord(tr->evd[slot], st);
     if (e != hipSuccess) return map_hip((int)e);
     tr->used[slot] = true;
@@ -2094,6 +2129,42 @@ int bih_last_render_times(const bih_tree *tr, double *kernel_ms, double *tail_ms
     *kernel_ms = f0;
     *tail_ms = f1;
     return BIH_OK;
+}
+
+int bih_render_history(const bih_tree *tr, uint32_t n, double *t) {
+    if (!tr || !t || n == 0 || n > (uint32_t)kSlots || tr->last_slot < 0 || !tr->last_timed) return BIH_ERR_INVALID;
+    DeviceGuard g(tr->t.device);
+    std::lock_guard<std::mutex> lk(tr->mu);
+    // slot of the i-th of the last n renders (slots are taken in turn)
+    auto slot_of = [&](uint32_t i) { return (tr->last_slot - (int)(n - 1 - i) + 2 * kSlots) % kSlots; };
+    for (uint32_t i = 0; i < n; ++i)
+        if (!tr->used[slot_of(i)] || !tr->slot_timed[slot_of(i)]) return BIH_ERR_INVALID;
+    const hipEvent_t base = tr->ev0[slot_of(0)];
+    for (uint32_t i = 0; i < n; ++i) {
+        const int k = slot_of(i);
+        hipError_t e = hipEventSynchronize(tr->evd[k]);
+        float a = 0.f, b = 0.f, c = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&a, base, tr->ev0[k]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&b, base, tr->ev1[k]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&c, base, tr->ev2[k]);
+        if (e != hipSuccess) return map_hip((int)e);
+        t[3 * i] = a;
+        t[3 * i + 1] = b;
+        t[3 * i + 2] = c;
+    }
+    return BIH_OK;
+}
+
+int bih_host_register(void *ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return BIH_ERR_INVALID;
+    if (bih_device_count() <= 0) return BIH_ERR_NO_DEVICE;
+    return map_hip((int)hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+}
+
+int bih_host_unregister(void *ptr) {
+    if (!ptr) return BIH_ERR_INVALID;
+    if (bih_device_count() <= 0) return BIH_ERR_NO_DEVICE;
+    return map_hip((int)hipHostUnregister(ptr));
 }
 
 int bih_bins_get_stats(const bih_tree *ctr, bih_bins_stats *out) {

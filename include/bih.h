@@ -34,8 +34,9 @@
 extern "C" {
 #endif
 
-#define BIH_ABI_VERSION 3   /* 2: bih_tree_info.device_allocs, bih_reserve, bih_tree_set_param;
-                               3: bih_whitted_work, BIH_PARAM_WHITTED_COUNTERS */
+#define BIH_ABI_VERSION 4   /* 2: bih_tree_info.device_allocs, bih_reserve, bih_tree_set_param;
+                               3: bih_whitted_work, BIH_PARAM_WHITTED_COUNTERS;
+                               4: bih_host_register / bih_host_unregister, bih_render_history */
 
 /* error codes */
 #define BIH_OK               0
@@ -79,9 +80,15 @@ typedef struct bih_framebuffer {
 
 /* Traversal flavours; both produce bit-identical RGBA.
  * BIH_TRAVERSE_REFERENCE visits exactly the nodes/leaves/triangles of
- * TraverseTree (CUDAKernels.cu:227-368); BIH_TRAVERSE_ANYHIT (default) runs
- * the same walk but stops at the first triangle that sets rec.triangleIdx,
- * which is all Color() (:370-389) consumes. */
+ * TraverseTree (CUDAKernels.cu:227-368).  BIH_TRAVERSE_ANYHIT (default)
+ * computes only the one bit per sample Color() (:370-389) consumes: does the
+ * reference walk reach a triangle that sets rec.triangleIdx.  It answers
+ * through the camera's frustum bins (per 4x4-pixel tile the triangles whose
+ * proven edge pre-test a sample can pass, each candidate hit verified against
+ * the reference walk's decisions on its root path),
+ * and whatever a tile list cannot decide -- or a render the bins do not
+ * cover -- takes the any-hit BIH walk, which stops at the first such
+ * triangle. */
 #define BIH_TRAVERSE_ANYHIT     0u
 #define BIH_TRAVERSE_REFERENCE  1u
 
@@ -257,6 +264,15 @@ int bih_render_whitted(const bih_scene *scene, const bih_tree *tree, const bih_c
 int bih_whitted_work(const bih_tree *tree, uint32_t rays[BIH_WHITTED_BOUNCES + 1],
                      uint64_t nodes[BIH_WHITTED_BOUNCES + 1], uint64_t tris[BIH_WHITTED_BOUNCES + 1]);
 
+/* The drop-in host loop (bih_render into a caller's framebuffer) ends in a
+ * device-to-host copy of w*h*4 bytes.  Into pageable memory the runtime
+ * stages it; page-locking the framebuffer once lets the copy run at DMA rate
+ * (the reference copies device-to-device into its GL buffer instead,
+ * src/Renderer.cpp:645-655).  Optional: any host buffer works without it.
+ * bih_host_unregister undoes it (before the buffer is freed). */
+int bih_host_register(void *ptr, size_t bytes);
+int bih_host_unregister(void *ptr);
+
 /* Per-render device timing (HIP events on the render stream around the main
  * render kernel and at the end of the render's device work), off by default:
  * the events cost host time on every render call.  bih_last_render_ms gives
@@ -269,6 +285,12 @@ int bih_last_render_ms(const bih_tree *tree, double *ms);
  * end to the end of the render call's device work (k_render_fallback, the
  * exact walk of packets the frustum-bin kernel left undecided). */
 int bih_last_render_times(const bih_tree *tree, double *kernel_ms, double *tail_ms);
+/* The last n renders (1 <= n <= 3; all issued with timing on), oldest first:
+ * t[3*i .. 3*i+2] = {main kernel start, main kernel end, end of the render's
+ * device work} in ms after the oldest one's kernel start.  Renders of a frame
+ * loop in flight on several streams overlap: the union of their kernel
+ * intervals is the loop's kernel time (bench.py's roofline). */
+int bih_render_history(const bih_tree *tree, uint32_t n, double *t);
 
 /* The frustum bins of the tree's current camera and image (any-hit renders):
  * usable = 1 when renders walk them; list entries over all tiles, entries of

@@ -40,7 +40,7 @@ def test_camera_reference_matches_oracle(bihrt_mod, oracle_mod):
 
 def test_errors_without_device(bihrt_mod):
     L = bihrt_mod._lib.load()
-    assert L.bih_abi_version() == 3
+    assert L.bih_abi_version() == 4
     assert L.bih_strerror(-2).decode().startswith("no HIP device")
     assert L.bih_strerror(12345).decode() == "unknown error"
     cam = bihrt_mod.Camera()
@@ -60,6 +60,14 @@ def test_errors_without_device(bihrt_mod):
     assert L.bih_reserve(None, 1920, 1080, 4, None, 16) == -1
     assert L.bih_tree_set_param(None, bihrt_mod.PARAM_ITEM_TILES, 1) == -1
     assert L.bih_tree_set_param(None, bihrt_mod.PARAM_STATIC_SOUP, 1) == -1
+    # ABI 4: host framebuffer registration and the render history
+    assert L.bih_host_register(None, 16) == -1
+    assert L.bih_host_unregister(None) == -1
+    hist = (C.c_double * 9)()
+    assert L.bih_render_history(None, 3, hist) == -1
+    if bihrt_mod.device_count() == 0:
+        buf = np.zeros(1024, np.uint32)
+        assert L.bih_host_register(C.c_void_p(buf.ctypes.data), buf.nbytes) == -2
     # the tree-info struct carries the allocation counter (ABI 2)
     assert bihrt_mod._lib.TreeInfo.device_allocs.offset + 8 == C.sizeof(bihrt_mod._lib.TreeInfo)
 

@@ -833,8 +833,11 @@ def test_steady_frame_loop_allocates_nothing(gpu, bihrt_mod):
 def test_reserved_share_calls_of_every_length_allocate_nothing(gpu, bihrt_mod):
     """A rank's share of an 8-way band split has few tiles, so a call's items
     are split over its frames, and the split count is not monotone in the
-    frame count (item_split).  bih_reserve(max_frames=16) sizes the split
-    start states for every call length 1..16: no allocation in the loop."""
+    frame count (item_split).  bih_reserve(max_frames=16) sizes what calls of
+    every length 1..16 need -- the XORWOW ring, the tile queues of every camera
+    set, the fallback records (one per packet and frame) and the stamps: no
+    allocation in the loop, on one stream (stamped state) or alternating two
+    (the ring)."""
     import torch
     from bihrt.tiling import band_rows
     tris = bihrt_mod.scenes.soup(100_000, seed=5)
@@ -852,6 +855,13 @@ def test_reserved_share_calls_of_every_length_allocate_nothing(gpu, bihrt_mod):
         r.render_device_frames(out.data_ptr(), f, m, rows.nrows * w, rows=rows)
         f += m
     r.sync()
+    assert g.info().device_allocs == a0
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    for k, m in enumerate([16, 4, 1, 16, 7, 2]):
+        r.render_device_frames(out.data_ptr(), f, m, rows.nrows * w, rows=rows, stream=streams[k % 2].cuda_stream)
+        f += m
+    torch.cuda.synchronize()
     assert g.info().device_allocs == a0
 
 
@@ -994,4 +1004,153 @@ def test_ring_advance_jump_tables_match_oracle(gpu, bihrt_mod, oracle_mod):
             ref, _ = ot.render(w, h, frame=f + j)
             got = b[j * stride:(j + 1) * stride].reshape(h, w)
             assert np.array_equal(got, ref), (f + j, int((got != ref).sum()), int((got == 0xFFFFFFFF).sum()))
+    g.close()
+
+
+@pytest.mark.gpu
+def test_reserve_growing_stamps_mid_stamped_run(gpu, bihrt_mod, oracle_mod):
+    """bih_reserve of a shape with more tiles (a higher spp: smaller packet
+    tiles) while a one-stream frame loop runs on the stamped XORWOW state:
+    the stamp array grows, and the stamped state is first folded back into
+    the ring, so the next frames continue the sequence (before the
+    fix the ring still held the state stamped mode started from).  Frames
+    before and after equal the oracle's."""
+    tris = bihrt_mod.scenes.soup(20_000, seed=12)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 96, 64
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, w, h)
+    imgs = {}
+    for f in range(6):                      # one stream: stamped from the fourth render on
+        imgs[f] = r.render(f)
+    g.reserve(w, h, 16, None, 4)            # 16 spp: 2x2 tiles, 4x the stamps
+    for f in range(6, 9):
+        imgs[f] = r.render(f)
+    g.reserve(w * 2, h, 64, None, 1)        # the ring grows too (more pixels): re-seeded
+    for f in (9, 10, 40):
+        imgs[f] = r.render(f)
+    for f, img in imgs.items():
+        ref, _ = ot.render(w, h, frame=f)
+        assert np.array_equal(img, ref), (f, int((img != ref).sum()))
+    g.close()
+
+
+@pytest.mark.gpu
+def test_one_stream_1m_1080p_stamped_across_syncs(gpu, bihrt_mod, oracle_mod, soup1m):
+    """The stamped XORWOW state at the BASELINE size: the
+    1M soup at 1920x1080 on ONE stream, 140 frames in calls of 1 and 16
+    frames -- stamped launches (k_render_bins<L, 4>) from the fourth render
+    on, two k_rng_sync runs (every 64 frames) -- as INTEGRATION.md's frame
+    loop issues them.  Frames 0, 70 and 139 equal the oracle on every row
+    (cudaRender's persistent per-pixel curandState, CUDAKernels.cu:391-423)."""
+    import torch
+    tris, ot = soup1m
+    w, h = 1920, 1080
+    d = torch.from_numpy(tris).cuda()
+    g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0])
+    g.reserve(w, h, 4, None, 16)
+    r = bihrt_mod.Renderer(g, w, h)
+    want = (0, 70, 139)
+    sizes = [1, 1, 1, 1, 16, 16, 1, 16, 16, 1, 1, 16, 16, 16, 1, 16]
+    plan, f = [], 0
+    while f < 140:
+        n = min(sizes[len(plan) % len(sizes)], 140 - f)
+        plan.append((f, n))
+        f += n
+    scratch = torch.zeros(16 * h * w, dtype=torch.int32, device="cuda")
+    kept = {}
+    torch.cuda.synchronize()
+    for f0, n in plan:
+        hit = [q for q in want if f0 <= q < f0 + n]
+        buf = torch.full((n * h * w,), -1, dtype=torch.int32, device="cuda") if hit else scratch
+        if hit:
+            torch.cuda.synchronize()       # (the fill, on torch's stream, before the library's)
+        if n == 1:
+            r.render_device(buf.data_ptr(), f0)
+        else:
+            r.render_device_frames(buf.data_ptr(), f0, n, h * w)
+        for q in hit:
+            kept[q] = (buf, q - f0)
+    r.sync()
+    assert g.bins_stats().usable
+    for q in want:
+        buf, j = kept[q]
+        got = buf[j * h * w:(j + 1) * h * w].cpu().numpy().view(np.uint32).reshape(h, w)
+        ref, _ = ot.render(w, h, frame=q, mode=oracle_mod.MODE_GPU_ANYHIT, threads=0)
+        assert np.array_equal(got, ref), (q, int((got != ref).sum()))
+    g.close()
+
+
+@pytest.mark.gpu
+def test_dynamic_soup_1m_540p_rebuild_equals_oracle(gpu, bihrt_mod, oracle_mod, soup1m):
+    """Geometry that changes every frame (bench `dynamic_rebuild`, VERDICT r5
+    item 5): the tree's device soup is overwritten with another 1M soup and
+    rebuilt (src/App.cpp:174-183 -> src/Renderer.cpp:415-501), and the next
+    frames -- whose camera structures must follow the new tree -- equal the
+    oracle of the new soup; then back to the first soup, frames in flight on
+    two streams."""
+    import torch
+    tris_a, ot_a = soup1m
+    tris_b = bihrt_mod.scenes.soup(1_000_000, seed=2)
+    ot_b = oracle_mod.OracleTree(tris_b)
+    w, h = 960, 540
+    d = torch.from_numpy(tris_a).cuda()
+    d_b = torch.from_numpy(tris_b).cuda()
+    d_a = d.clone()
+    g = bihrt_mod.GPUArrayManager.from_device(d.data_ptr(), tris_a.shape[0])
+    r = bihrt_mod.Renderer(g, w, h)
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.zeros(4 * h * w, dtype=torch.int32, device="cuda") for _ in range(6)]
+    torch.cuda.synchronize()
+    seq = [("A", 0, 1), ("A", 1, 4), ("B", 5, 1), ("B", 6, 4), ("A", 10, 4), ("B", 14, 1)]
+    cur = "A"
+    for k, (soup, f0, n) in enumerate(seq):
+        if soup != cur:
+            torch.cuda.synchronize()
+            d.copy_(d_b if soup == "B" else d_a)
+            torch.cuda.synchronize()
+            g.rebuild()
+            cur = soup
+        s = streams[k % 2].cuda_stream
+        if n == 1:
+            r.render_device(outs[k].data_ptr(), f0, stream=s)
+        else:
+            r.render_device_frames(outs[k].data_ptr(), f0, n, h * w, stream=s)
+    torch.cuda.synchronize()
+    for k, (soup, f0, n) in enumerate(seq):
+        ot = ot_b if soup == "B" else ot_a
+        for j in sorted({0, n - 1}):
+            got = outs[k][j * h * w:(j + 1) * h * w].cpu().numpy().view(np.uint32).reshape(h, w)
+            ref, _ = ot.render(w, h, frame=f0 + j, mode=oracle_mod.MODE_GPU_ANYHIT, threads=0)
+            assert np.array_equal(got, ref), (soup, f0 + j, int((got != ref).sum()))
+    g.close()
+
+
+@pytest.mark.gpu
+def test_host_loop_registered_framebuffer(gpu, bihrt_mod, oracle_mod):
+    """INTEGRATION.md's loop (bih_rebuild + bih_render into a host
+    framebuffer) into one reused buffer, pageable and then page-locked with
+    bih_host_register: every frame equals the oracle's."""
+    tris = bihrt_mod.scenes.soup(50_000, seed=4)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 320, 180
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, w, h)
+    fb = np.zeros((h, w), np.uint32)
+    for f in range(3):
+        g.rebuild()
+        r.render(f, out=fb)
+        ref, _ = ot.render(w, h, frame=f)
+        assert np.array_equal(fb, ref), f
+    bihrt_mod.host_register(fb)
+    try:
+        for f in range(3, 7):
+            g.rebuild()
+            r.render(f, out=fb)
+            ref, _ = ot.render(w, h, frame=f)
+            assert np.array_equal(fb, ref), f
+    finally:
+        bihrt_mod.host_unregister(fb)
+    with pytest.raises(ValueError):
+        r.render(7, out=np.zeros((h, w + 1), np.uint32))
     g.close()

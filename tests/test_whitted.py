@@ -172,6 +172,15 @@ def test_whitted_work_counters_match_oracle(scene, gpu, bihrt_mod, oracle_mod):
     # rays of bounce d = samples with at least d hits
     for d in range(9):
         assert wk["rays"][d] == int((dep >= d).sum()), d
+    # a second frame of the same camera: the frustum bins are usable from now
+    # on, and with counters on every primary sample is still walked, so the
+    # counts stay the oracle's
+    img2, hits2 = _whitted_device(bihrt_mod, g, w, h, 2)
+    wk2 = r.whitted_work()
+    ref2, st2, dep2 = ot.render_whitted(w, h, frame=2, depths=True)
+    assert np.array_equal(img2, ref2) and np.array_equal(hits2, dep2)
+    assert (sum(wk2["rays"]), sum(wk2["nodes"]), sum(wk2["tris"])) == (st2.slab_miss, st2.node_visits,
+                                                                        st2.tri_tests)
     g.set_param(bihrt_mod.PARAM_WHITTED_COUNTERS, 0)
     img0, _ = _whitted_device(bihrt_mod, g, w, h, 1)
     assert np.array_equal(img0, ref)
@@ -238,3 +247,35 @@ def test_whitted_4k_properties(gpu, bihrt_mod, oracle_mod):
     ref, _, dep = ot.render_whitted(w, h, rows=(0, 34, 64), depths=True)
     assert np.array_equal(img[0::64], ref), int((img[0::64] != ref).sum())
     assert np.array_equal(hs[0::64].reshape(-1), dep)
+
+
+@pytest.mark.gpu
+def test_whitted_frames_on_alternating_streams(gpu, bihrt_mod, oracle_mod):
+    """Whitted frames issued back to back on two streams, no host wait in
+    between: each call's bounce-0 mask render rewrites the tree's shared hit
+    mask only after the previous call's Whitted launch has read it (ADVICE
+    r5: the mask render waits on the last Whitted launch's event, and one
+    lock covers both phases).  Every frame, pixels and per-sample hit counts,
+    equals the oracle's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(60_000, seed=6)
+    g = bihrt_mod.GPUArrayManager(tris)
+    ot = oracle_mod.OracleTree(tris)
+    w, h, spp = 128, 72, 4
+    r = bihrt_mod.Renderer(g, w, h, spp=spp)
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    frames = list(range(6))
+    outs = [torch.zeros(h * w, dtype=torch.int32, device="cuda") for _ in frames]
+    hits = [torch.zeros(h * w * spp, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    for k, f in enumerate(frames):
+        r.render_whitted_device(outs[k].data_ptr(), f, hits_ptr=hits[k].data_ptr(),
+                                stream=streams[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for k, f in enumerate(frames):
+        ref, _, dep = ot.render_whitted(w, h, frame=f, depths=True)
+        img = outs[k].cpu().numpy().view(np.uint32).reshape(h, w)
+        hs = hits[k].cpu().numpy().astype(np.uint8)
+        assert np.array_equal(hs, dep), (f, int((hs != dep).sum()))
+        assert np.array_equal(img, ref), (f, int((img != ref).sum()))
+    g.close()
