@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <stdlib.h>
 #include <utility>
 #include <float.h>
 
@@ -87,7 +88,11 @@ __device__ __forceinline__ void axis_minmax(float x0, float x1, float x2, float 
 __global__ void __launch_bounds__(kThreads) k_prep(const float *__restrict__ v, uint32_t n,
                                                    float *__restrict__ lo, float *__restrict__ hi,
                                                    TreeHeader *hdr,
-                                                   unsigned long long *__restrict__ part) {
+                                                   unsigned long long *__restrict__ part,
+                                                   uint32_t *__restrict__ epoch) {
+    // the build's sequence number (scan_tag: the look-back tags of this
+    // build's scans); the kernels that read it run after this one
+    if (blockIdx.x == 0 && threadIdx.x == 0) *epoch += 1u;
     unsigned long long kmin[3] = {~0ull, ~0ull, ~0ull}, kmax[3] = {0ull, 0ull, 0ull};
     uint32_t bad = 0;
     uint32_t hx = 0u, hy = 0u;   // content hash (content_word): XOR of every word's term
@@ -353,10 +358,20 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *l
 // every tile a block waits for is resident or done.  The flag and the value
 // share one 64-bit word, so relaxed device-scope atomics suffice (no L2
 // writeback/invalidate fences: each block's output is its own).
+// Look-back tag of scan k (1..7) of the build whose sequence number k_prep
+// wrote (DeviceTree::epoch): unique per build and scan, non-zero, and the same
+// in every replay of a captured build graph's node -- the tag a node was
+// captured with is not (next_scan_tag is a host counter).  The build's status
+// words (DeviceTree::partials) only ever hold such tags.
+__device__ __forceinline__ uint32_t scan_tag(const uint32_t *epoch, uint32_t k) {
+    return epoch ? ((*epoch * 8u + k) & 0x3FFFFFFFu) : k;
+}
+
 __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, uint32_t *out, uint32_t n,
                                                            unsigned long long *status, uint32_t tag,
-                                                           uint32_t *total_out) {
+                                                           uint32_t *total_out, const uint32_t *epoch) {
     __shared__ uint32_t lds[4];
+    tag = scan_tag(epoch, tag);
     __shared__ uint32_t s_prefix;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
@@ -404,14 +419,15 @@ __global__ void __launch_bounds__(kThreads) k_scan_onepass(const uint32_t *in, u
 }
 
 
-// `partials`: scan_partials_words(n) u32 words, 8-byte aligned (status words)
+// `partials`: scan_partials_words(n) u32 words, 8-byte aligned (status words).
+// epoch (the builder's scans): tag = scan_tag(epoch, k); else a fresh host tag
 hipError_t exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t *partials,
-                          uint32_t *total_dev, hipStream_t st) {
+                          uint32_t *total_dev, hipStream_t st, const uint32_t *epoch = nullptr, uint32_t k = 0) {
     if (n == 0) return hipSuccess;
     const uint32_t nb = (n + kScanTile - 1) / kScanTile;
-    const uint32_t tag = next_scan_tag();
+    const uint32_t tag = epoch ? k : next_scan_tag();
     hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kThreads), 0, st, in, out, n,
-                       reinterpret_cast<unsigned long long *>(partials), tag, total_dev);
+                       reinterpret_cast<unsigned long long *>(partials), tag, total_dev, epoch);
     return hipGetLastError();
 }
 
@@ -555,8 +571,9 @@ __global__ void __launch_bounds__(kThreads) k_runs(const uint32_t *__restrict__ 
                                                    unsigned long long *status, uint32_t tag,
                                                    uint32_t *__restrict__ umc, int32_t *__restrict__ first,
                                                    uint32_t *__restrict__ run_end, uint32_t *__restrict__ leaf_of,
-                                                   TreeHeader *hdr) {
+                                                   TreeHeader *hdr, const uint32_t *epoch) {
     __shared__ uint32_t lds[4];
+    tag = scan_tag(epoch, tag);
     __shared__ uint32_t s_prefix;
     const uint32_t tile = blockIdx.x;
     const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
@@ -1083,6 +1100,7 @@ static void free_build_buffers(DeviceTree &t) {
 }
 
 void free_tree_device(DeviceTree &t) {
+    if (t.graph) (void)hipGraphExecDestroy(t.graph);
     free_build_buffers(t);
     if (t.hdr_host) (void)hipHostFree(t.hdr_host);
     if (t.ev0) (void)hipEventDestroy(t.ev0);
@@ -1123,9 +1141,10 @@ static hipError_t alloc_build_buffers(DeviceTree &t, uint64_t nn, uint64_t hist_
     BIH_TRY_E(dalloc(&t.tris_s, 9 * nn, t));
     BIH_TRY_E(dalloc(&t.hist, hist_n, t));
     BIH_TRY_E(dalloc(&t.partials, 2 * (uint64_t)max_parts + 2, t));   // k_scan_onepass status words
-    // + k_seg_build's arrival count (zero between launches)
-    BIH_TRY_E(dalloc(&t.prep_part, 8ull * kPrepBlocks + 2, t));
-    BIH_TRY_E(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 2 * sizeof(unsigned long long), st));
+    // + k_seg_build's arrival count (zero between launches) + the build's
+    // sequence number (k_prep; scan_tag)
+    BIH_TRY_E(dalloc(&t.prep_part, 8ull * kPrepBlocks + 3, t));
+    BIH_TRY_E(hipMemsetAsync(t.prep_part + 8ull * kPrepBlocks, 0, 3 * sizeof(unsigned long long), st));
     // look-back words (k_scan_onepass) start at tag 0 (never a call's tag):
     // stale data in fresh memory must not pass for a predecessor's published
     // prefix; afterwards every word carries an older call's (unique) tag
@@ -1134,78 +1153,52 @@ static hipError_t alloc_build_buffers(DeviceTree &t, uint64_t nn, uint64_t hist_
 }
 #undef BIH_TRY_E
 
-// Allocates (first call) and runs the whole build on `stream`; synchronises
-// at the end to read U back (Renderer.cpp:459 also reads the reduce_by_key
-// end pointer on the host).
-int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync) {
-    hipStream_t st = (hipStream_t)stream;
-    const uint32_t n = t.n;
-    const uint64_t nn = n ? n : 1;
+#define BIH_TRY_H(x)                                \
+    do {                                            \
+        hipError_t e__ = (x);                       \
+        if (e__ != hipSuccess) return e__;          \
+    } while (0)
+// The build's kernels for n > 0 triangles, in order, on `st` (issued
+// directly or captured into the tree's graph: build_tree_device).
+static hipError_t issue_build(DeviceTree &t, uint32_t n, hipStream_t st) {
+    const uint64_t nn = n;
     const uint32_t rs_blocks = (uint32_t)((nn + kRsTile - 1) / kRsTile);
     const uint64_t hist_n = (uint64_t)kRdBins * rs_blocks;
-    const uint32_t max_parts =
-        (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
-    if (!t.hdr) {
-        // all or nothing: a failure part-way frees what was allocated, so
-        // that the tree never holds a header without its buffers (the next
-        // build of it allocates them again)
-        const size_t bytes0 = t.bytes;
-        const hipError_t e = alloc_build_buffers(t, nn, hist_n, max_parts, st);
-        t.fail_alloc = 0;
-        if (e != hipSuccess) {
-            (void)hipStreamSynchronize(st);   // the memsets, if any were issued
-            (void)hipGetLastError();          // not sticky for the next build
-            free_build_buffers(t);
-            t.bytes = bytes0;
-            return (int)e;
-        }
-    }
-    // timing events and the pinned copy of the header: once per tree
-    if (!t.ev0) {
-        BIH_TRY(hipEventCreate(&t.ev0));
-        BIH_TRY(hipEventCreate(&t.ev1));
-        BIH_TRY(hipHostMalloc((void **)&t.hdr_host, sizeof(TreeHeader), hipHostMallocDefault));
-    }
-    BIH_TRY(hipEventRecord(t.ev0, st));
-
-    // header reset (no triangles; otherwise k_morton's block 0 writes the header)
-    if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
-
-    if (n > 0) {
+    {
         const uint32_t prep_blocks = blocks_for(n) < kPrepBlocks ? blocks_for(n) : kPrepBlocks;
+        uint32_t *epoch = reinterpret_cast<uint32_t *>(t.prep_part + 8ull * kPrepBlocks + 2);
         hipLaunchKernelGGL(k_prep, dim3(prep_blocks), dim3(kThreads), 0, st, t.v, n, t.tri_lo,
-                           t.tri_hi, t.hdr, t.prep_part);
+                           t.tri_hi, t.hdr, t.prep_part, epoch);
         // (the fold of the partials: every k_morton block for itself; in
         // k_prep's last block instead -- a device-scope fence per block: k_prep
         // 0.147 ms, r04a; an sc1 store / agent-add / sc1 load hand-off: 0.032
         // ms, r04e -- against 0.016 + 0.012 for k_prep + k_prep_final)
         hipLaunchKernelGGL(k_morton, dim3(rs_blocks), dim3(kRsBlock), 0, st, t.v, t.tri_lo, t.tri_hi, t.hdr, n,
-                           t.prep_part, prep_blocks, t.keys, t.vals, t.hist, rs_blocks);
+                           t.prep_part, prep_blocks, t.keys2, t.vals2, t.hist, rs_blocks);
         // 3 stable passes of 10-bit digits over the 30-bit codes (k_morton
-        // counted the first digit); the sorted pairs end in keys2 / vals2,
-        // which then become keys / vals
-        uint32_t *ka = t.keys, *va = t.vals, *kb = t.keys2, *vb = t.vals2;
+        // counted the first digit): keys2 -> keys -> keys2 -> keys, so the
+        // sorted pairs end in keys / vals and no pointer changes between
+        // builds (a captured graph replays the same buffers)
+        uint32_t *ka = t.keys2, *va = t.vals2, *kb = t.keys, *vb = t.vals;
         for (int p = 0; p < kRdPasses; ++p) {
             const int shift = kRdBits * p;
             if (p > 0)
                 hipLaunchKernelGGL(k_rs_hist10, dim3(rs_blocks), dim3(kRsBlock), 0, st, ka, n, shift, t.hist,
                                    rs_blocks);
-            BIH_TRY(exclusive_scan(t.hist, t.hist, (uint32_t)hist_n, t.partials, nullptr, st));
+            BIH_TRY_H(exclusive_scan(t.hist, t.hist, (uint32_t)hist_n, t.partials, nullptr, st, epoch, 1u + p));
             hipLaunchKernelGGL(k_rs_scatter10, dim3(rs_blocks), dim3(kRsBlock), 0, st, ka, va, n, shift, t.hist,
                                rs_blocks, kb, vb);
             uint32_t *tk = ka, *tv = va;
             ka = kb; va = vb; kb = tk; vb = tv;
         }
-        static_assert(kRdPasses % 2 == 1, "an odd pass count leaves the result in keys2 / vals2");
-        std::swap(t.keys, t.keys2);
-        std::swap(t.vals, t.vals2);
+        static_assert(kRdPasses % 2 == 1, "an odd pass count leaves the result in keys / vals");
         // runs: codes, first indices, ends (k_karras: counts), leaf of each
         // sorted triangle, U
         {
             const uint32_t nb = (n + kScanTile - 1) / kScanTile;
             hipLaunchKernelGGL(k_runs, dim3(nb), dim3(kThreads), 0, st, t.keys, n,
-                               reinterpret_cast<unsigned long long *>(t.partials), next_scan_tag(), t.unique_mc,
-                               t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr);
+                               reinterpret_cast<unsigned long long *>(t.partials), 4u, t.unique_mc,
+                               t.first_idx, t.dup_cnt, t.scan_tmp, t.hdr, epoch);
         }
         hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.unique_mc, t.hdr, t.first_idx,
                            t.dup_cnt, t.children, t.is_leaf, t.axis, t.parent, t.leaf_parent, t.fit_rng);
@@ -1228,7 +1221,92 @@ int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync) {
         hipLaunchKernelGGL(k_fit, dim3(blocks_for(n)), dim3(kThreads), 0, st, t.hdr, t.fit_rng, t.children,
                            t.axis, t.fit_seg, cap, nn, t.clip, t.is_leaf, t.first_idx, t.dup_cnt, t.nodes, t.v,
                            t.vals, n, t.tris_s, t.hdr_host);
-        BIH_TRY(hipGetLastError());
+    }
+    return hipGetLastError();
+}
+
+#undef BIH_TRY_H
+
+// Allocates (first call) and runs the whole build on `stream`; synchronises
+// at the end to read U back (Renderer.cpp:459 also reads the reduce_by_key
+// end pointer on the host).
+int build_tree_device(DeviceTree &t, void *stream, float *ms_out, bool sync) {
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t n = t.n;
+    const uint64_t nn = n ? n : 1;
+    const uint32_t rs_blocks = (uint32_t)((nn + kRsTile - 1) / kRsTile);
+    const uint64_t hist_n = (uint64_t)kRdBins * rs_blocks;
+    const uint32_t max_parts =
+        (uint32_t)(((hist_n > nn + 1 ? hist_n : nn + 1) + kScanTile - 1) / kScanTile);
+    if (!t.hdr) {
+        // all or nothing: a failure part-way frees what was allocated, so
+        // that the tree never holds a header without its buffers (the next
+        // build of it allocates them again)
+        const size_t bytes0 = t.bytes;
+        const hipError_t e = alloc_build_buffers(t, nn, hist_n, max_parts, st);
+        t.fail_alloc = 0;
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);   // the memsets, if any were issued
+            (void)hipGetLastError();          // not sticky for the next build
+            if (t.graph) (void)hipGraphExecDestroy(t.graph);
+            t.graph = nullptr;
+            free_build_buffers(t);
+            t.bytes = bytes0;
+            return (int)e;
+        }
+    }
+    // timing events and the pinned copy of the header: once per tree
+    if (!t.ev0) {
+        BIH_TRY(hipEventCreate(&t.ev0));
+        BIH_TRY(hipEventCreate(&t.ev1));
+        BIH_TRY(hipHostMalloc((void **)&t.hdr_host, sizeof(TreeHeader), hipHostMallocDefault));
+    }
+    BIH_TRY(hipEventRecord(t.ev0, st));
+
+    // header reset (no triangles; otherwise k_morton's block 0 writes the header)
+    if (n == 0) hipLaunchKernelGGL(k_hdr_init, dim3(1), dim3(64), 0, st, t.hdr, n);
+
+    if (n > 0) {
+        // The chain of ~15 dependent launches depends only on n and the tree's
+        // buffers: captured once per tree buffer into a hipGraph and replayed
+        // with one launch per build (host issue ~0.2 ms -> one call; the
+        // look-back tags come from the device epoch, scan_tag).
+        // BIH_BUILD_GRAPH=0: issued launch by launch (A/B).
+        static const bool use_graph = [] {
+            const char *e = getenv("BIH_BUILD_GRAPH");
+            return !(e && e[0] == '0');
+        }();
+        if (use_graph) {
+            if (t.graph && (t.graph_n != n || t.graph_v != t.v)) {
+                (void)hipGraphExecDestroy(t.graph);
+                t.graph = nullptr;
+            }
+            if (!t.graph && hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed) != hipSuccess) {
+                // (a stream that cannot be captured, e.g. the legacy default
+                // stream: launch by launch)
+                (void)hipGetLastError();
+                BIH_TRY(issue_build(t, n, st));
+            } else if (!t.graph) {
+                hipGraph_t g = nullptr;
+                const hipError_t ce = issue_build(t, n, st);
+                const hipError_t ee = hipStreamEndCapture(st, &g);
+                if (ce != hipSuccess || ee != hipSuccess) {
+                    if (g) (void)hipGraphDestroy(g);
+                    return (int)(ce != hipSuccess ? ce : ee);
+                }
+                const hipError_t ie = hipGraphInstantiate(&t.graph, g, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(g);
+                if (ie != hipSuccess) {
+                    t.graph = nullptr;
+                    return (int)ie;
+                }
+                t.graph_n = n;
+                t.graph_v = t.v;
+            }
+            if (t.graph) BIH_TRY(hipGraphLaunch(t.graph, st));
+        } else {
+            BIH_TRY(issue_build(t, n, st));
+        }
     }
     BIH_TRY(hipEventRecord(t.ev1, st));
     // the header comes back through pinned host memory that k_fit's first

@@ -228,6 +228,9 @@ struct DeviceTree {
     unsigned long long *prep_part = nullptr;        // k_prep per-block AABB keys
     TreeHeader *hdr_host = nullptr;                 // pinned host copy of hdr (k_fit writes it)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;        // build timing (build_ms)
+    hipGraphExec_t graph = nullptr;                 // the build's kernels for graph_n triangles of graph_v
+    uint32_t graph_n = 0;
+    const float *graph_v = nullptr;
     uint32_t fail_alloc = 0;                        // tests (BIH_PARAM_TEST_ALLOC_FAIL): the k-th
                                                     // buffer allocation of the next build fails
 };
