@@ -138,12 +138,18 @@ static uint32_t dbg_bits() {
 
 struct bih_tree {
     bih::DeviceTree t;
-    // Rebuilds write the other tree and swap (double buffering): renders of
-    // the current tree still in flight keep reading theirs while the next one
-    // is built.  gen counts swaps; slot_gen[k] = the generation render slot k
-    // read, so a rebuild waits only for the renders that read `back`.
-    bih::DeviceTree back;
+    // Rebuilds write the oldest of three tree buffers and rotate (back[0] =
+    // the previous generation, back[1] = the one before): renders of the
+    // trees still in flight keep reading theirs while the next one is built,
+    // and two asynchronous rebuilds can run at once (pipelined frames: frame
+    // k+1's build beside frame k's, on the other build stream).  gen counts
+    // rotations; DeviceTree::gen is the generation a buffer holds and
+    // slot_gen[k] the one render slot k read, so a rebuild waits only for the
+    // renders that read its target buffer.
+    bih::DeviceTree back[2];
     uint32_t gen = 0;
+    hipStream_t bstream = nullptr;   // the second build stream (asynchronous rebuilds alternate)
+    uint32_t bpar = 0;               // asynchronous rebuilds so far (stream parity)
     uint32_t slot_gen[kSlots] = {};
     hipStream_t slot_stream[kSlots] = {};   // the stream render slot k was issued on
     TreeParams prm = env_params();
@@ -350,14 +356,20 @@ int prepare_chunk_order(bih_tree *tr, uint32_t w, uint32_t spp, const bih_rows &
     return BIH_OK;
 }
 
-// Orders `st` after every render in flight that read a tree of an older
-// generation than the current one (the buffers `back` holds).
-int wait_old_tree_readers(bih_tree *tr, hipStream_t st) {
+// Orders `st` after every render in flight that read generation g (the
+// buffer a rebuild is about to overwrite), and after that buffer's own last
+// build (it may have run on the other build stream).
+int wait_tree_buffer(bih_tree *tr, const bih::DeviceTree &b, hipStream_t st) {
+    if (!b.hdr) return BIH_OK;   // never built: no reader
     for (int k = 0; k < kSlots; ++k)
-        if (tr->used[k] && tr->slot_gen[k] != tr->gen) {
+        if (tr->used[k] && tr->slot_gen[k] == b.gen && hipEventQuery(tr->evd[k]) != hipSuccess) {
             hipError_t e = hipStreamWaitEvent(st, tr->evd[k], 0);
             if (e != hipSuccess) return map_hip((int)e);
         }
+    if (b.ev1 && hipEventQuery(b.ev1) != hipSuccess) {
+        hipError_t e = hipStreamWaitEvent(st, b.ev1, 0);
+        if (e != hipSuccess) return map_hip((int)e);
+    }
     return BIH_OK;
 }
 
@@ -368,6 +380,7 @@ int finish_build(bih_tree *tr) {
     const uint64_t old_content = tr->t.content;
     const uint32_t old_n = tr->t.n, old_u = tr->t.u;
     int e = 0;
+    hipStream_t bst = tr->stream;   // the stream the build runs on (ev_tree follows it)
     // tests: the next build that allocates its buffers fails part-way
     auto arm_fail = [&](bih::DeviceTree &d) {
         if (tr->prm.test_alloc_fail && !d.hdr) {
@@ -383,30 +396,47 @@ int finish_build(bih_tree *tr) {
         arm_fail(tr->t);
         e = bih::build_tree_device(tr->t, tr->stream, &ms);
     } else {
-        // rebuild into `back` (allocated by its first build): only the
-        // renders that read it -- older generations -- are waited for; the
-        // renders of the current tree run on beside the build
-        int rc = wait_old_tree_readers(tr, tr->stream);
-        if (rc) return rc;
-        bih::DeviceTree &b = tr->back;
-        if (!b.owns_v) b.v = tr->t.v;   // the same soup (the owning copy is t's or b's)
-        b.n = tr->t.n;
-        b.device = tr->t.device;
+        // rebuild into the oldest buffer (allocated by its first build): only
+        // the renders that read it are waited for; the renders of the newer
+        // trees run on beside the build
+        bih::DeviceTree &b = tr->back[1];
         // a soup that cannot have changed since the last build (the tree's own
         // copy, or BIH_PARAM_STATIC_SOUP) gives the same tree, header and
         // content hash bit for bit: nothing to read back, so the host does not
-        // wait for the build -- it runs on the tree's stream behind the
-        // renders in flight, and the next render orders after it (ev_tree)
+        // wait for the build -- it runs behind the renders in flight, and the
+        // next render orders after it (ev_tree).  Consecutive asynchronous
+        // rebuilds alternate between the tree's stream and a second build
+        // stream, so frame k+1's build runs beside frame k's (each chain of
+        // ~15 short kernels leaves most of the GPU idle); each render still
+        // waits for its own frame's tree.  BIH_BUILD_PIPE=0: one stream (A/B).
         async = tr->owns_soup || tr->prm.static_soup;
+        static const bool pipe = [] {
+            const char *v = getenv("BIH_BUILD_PIPE");
+            return !(v && v[0] == '0');
+        }();
+        if (async && pipe && (tr->bpar++ & 1u)) {
+            if (!tr->bstream && hipStreamCreateWithFlags(&tr->bstream, hipStreamNonBlocking) != hipSuccess) {
+                (void)hipGetLastError();
+                tr->bstream = nullptr;
+            }
+            if (tr->bstream) bst = tr->bstream;
+        }
+        int rc = wait_tree_buffer(tr, b, bst);
+        if (rc) return rc;
+        if (!b.owns_v) b.v = tr->t.v;   // the same soup (the owning copy is one buffer's)
+        b.n = tr->t.n;
+        b.device = tr->t.device;
         if (async) {
             b.u = tr->t.u;
             b.content = tr->t.content;
         }
         arm_fail(b);
-        e = bih::build_tree_device(b, tr->stream, &ms, !async);
+        e = bih::build_tree_device(b, bst, &ms, !async);
         if (e == 0 || e == -1000) {
-            std::swap(tr->t, tr->back);
-            ++tr->gen;
+            // rotate: the new tree becomes current, the current the previous
+            std::swap(tr->back[1], tr->back[0]);   // back[1] = previous-previous, back[0] = the new one
+            std::swap(tr->back[0], tr->t);         // t = the new one, back[0] = previous
+            tr->t.gen = ++tr->gen;
         }
     }
     tr->build_ms = ms;
@@ -429,7 +459,7 @@ int finish_build(bih_tree *tr) {
     // render and camera build waits on ev_tree).  A first build waited for
     // every render, so it also follows the last advance of the XORWOW ring;
     // a rebuild did not, and leaves ev_rng to the renders
-    hipError_t he = hipEventRecord(tr->ev_tree, tr->stream);
+    hipError_t he = hipEventRecord(tr->ev_tree, bst);
     if (he == hipSuccess && !had) he = hipEventRecord(tr->ev_rng, tr->stream);
     if (he != hipSuccess) return map_hip((int)he);
     if (!had) tr->rng_pending = true;
@@ -602,8 +632,11 @@ void bih_free(bih_tree *tr) {
     // a bins readback into bins_host may still be in flight (a failed render)
     for (CamSet &c : tr->cs)
         if (c.bins_pending) (void)hipEventSynchronize(c.ev_bins);
+    if (tr->bstream) (void)hipStreamSynchronize(tr->bstream);
     bih::free_tree_device(tr->t);
-    bih::free_tree_device(tr->back);   // (the soup is freed by whichever tree owns it)
+    bih::free_tree_device(tr->back[0]);   // (the soup is freed by whichever buffer owns it)
+    bih::free_tree_device(tr->back[1]);
+    if (tr->bstream) (void)hipStreamDestroy(tr->bstream);
     if (tr->rng) (void)hipFree(tr->rng);
     if (tr->fb) (void)hipFree(tr->fb);
     if (tr->work) (void)hipFree(tr->work);
@@ -651,7 +684,7 @@ static int wait_async_build(const bih_tree *tr) {
 int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     if (!tr || !info) return BIH_ERR_INVALID;
     DeviceGuard g(tr->t.device);
-    // a rebuild swaps t and back under the same lock: never read a half-swapped tree
+    // a rebuild rotates the tree buffers under the same lock: never read a half-rotated tree
     std::lock_guard<std::mutex> lk(tr->mu);
     if (int rc = wait_async_build(tr)) return rc;
     bih::TreeHeader h;
@@ -673,14 +706,14 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // records, and the per-slot tile queues, spill areas and chunk orders
     size_t cam = 0;
     for (const CamSet &c : tr->cs) cam += c.prim_cap + c.bins_mem_cap + c.bin_list_cap * kEntryBytes + c.q_cap;
-    info->device_bytes = tr->t.bytes + tr->back.bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
+    info->device_bytes = tr->t.bytes + tr->back[0].bytes + tr->back[1].bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
                           (tr->q_count ? (size_t)kSlots * 2 * bih::kBinSetWords : 0) +
                           (size_t)kSlots * tr->fbq_cap * 8) * 4 +
                          (tr->wh_mem ? bih::whitted_bytes(tr->wh_rays) : 0) + tr->wh_mask_cap * 8 + tr->stamp_cap * 8;
     info->build_ms = tr->build_ms;
-    info->device_allocs = tr->allocs + tr->t.allocs + tr->back.allocs;
+    info->device_allocs = tr->allocs + tr->t.allocs + tr->back[0].allocs + tr->back[1].allocs;
     return BIH_OK;
 }
 
@@ -1750,6 +1783,13 @@ int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
         return BIH_OK;
     case BIH_PARAM_STATIC_SOUP:
         if (value > 1) return BIH_ERR_INVALID;
+        // the caller may write the soup from now on: no asynchronous rebuild
+        // (which reads it) may still be running on the second build stream
+        if (!value && tr->bstream) {
+            DeviceGuard g(tr->t.device);
+            const hipError_t e = hipStreamSynchronize(tr->bstream);
+            if (e != hipSuccess) return map_hip((int)e);
+        }
         tr->prm.static_soup = (uint32_t)value;
         return BIH_OK;
     case BIH_PARAM_TEST_ALLOC_FAIL:

@@ -203,6 +203,7 @@ struct DeviceTree {
     int device = 0;
     uint32_t n = 0, u = 0;
     uint64_t content = 0;          // TreeHeader::content of the last build
+    uint32_t gen = 0;              // the tree generation this buffer holds (bih_capi.cpp)
     size_t bytes = 0;
     uint64_t allocs = 0;           // hipMalloc calls made for this tree (bih_tree_info.device_allocs)
     float *v = nullptr;            // input soup f32[9N] (device copy)

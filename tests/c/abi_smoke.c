@@ -61,6 +61,10 @@ static void check_errors(void) {
     bih_scene bad;
     uint32_t line = 0;
     CHECK(bih_scene_load_obj("/nonexistent/x.obj", &bad, &line) == BIH_ERR_IO, "missing OBJ -> IO");
+    CHECK(bih_host_register(NULL, 16) == BIH_ERR_INVALID && bih_host_unregister(NULL) == BIH_ERR_INVALID,
+          "bih_host_register(NULL) -> INVALID");
+    double hist[3];
+    CHECK(bih_render_history(NULL, 1, hist) == BIH_ERR_INVALID, "bih_render_history(NULL) -> INVALID");
 }
 
 int main(int argc, char **argv) {
@@ -119,6 +123,19 @@ int main(int argc, char **argv) {
     int rc2 = bih_render(&scene, tree, &cam, &fb2);
     CHECK(rc == BIH_OK && rc2 == BIH_OK && !memcmp(img, golden, (size_t)w * h * 4),
           "bih_rebuild + bih_render(frame %u) equals golden", frame);
+
+    /* INTEGRATION.md's frame loop into a page-locked framebuffer: rebuild +
+       render, several frames, the frame of the golden last */
+    rc = bih_host_register(img, (size_t)w * h * 4);
+    CHECK(rc == BIH_OK, "bih_host_register: %s", bih_strerror(rc));
+    for (uint32_t f = (frame >= 3 ? frame - 3 : 0); f <= frame && rc == BIH_OK; ++f) {
+        rc = bih_rebuild(tree);
+        bih_framebuffer fl = {w, h, 4, f, 1984u, img};
+        if (rc == BIH_OK) rc = bih_render(&scene, tree, &cam, &fl);
+    }
+    CHECK(rc == BIH_OK && !memcmp(img, golden, (size_t)w * h * 4),
+          "rebuild + render loop into a registered framebuffer ends on the golden frame: %s", bih_strerror(rc));
+    CHECK(bih_host_unregister(img) == BIH_OK, "bih_host_unregister");
 
     /* errors that need a tree */
     bih_framebuffer bad = {w, h, 0, 0, 1984u, img};
