@@ -1155,3 +1155,44 @@ def test_host_loop_registered_framebuffer(gpu, bihrt_mod, oracle_mod):
     with pytest.raises(ValueError):
         r.render(7, out=np.zeros((h, w + 1), np.uint32))
     g.close()
+
+
+@pytest.mark.gpu
+def test_recycled_stream_handles_keep_order(gpu, bihrt_mod, oracle_mod):
+    """Stamped mode and the shared-grid rule key on the raw hipStream_t of
+    the last render.  A stream the caller destroys and
+    creates again may come back with the same handle: the library must not
+    rely on that identity for ordering (every render waits on ev_rng, the
+    event after the last stamped launch or ring advance).  One-frame calls
+    on a stream (stamped from the fourth on), the stream destroyed and a new
+    one created (often the same handle) for the next frames, then a frame on
+    a fresh stream: every frame equals the oracle's."""
+    import torch
+    tris = bihrt_mod.scenes.soup(30_000, seed=13)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 128, 96
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, w, h)
+    outs = [torch.full((h * w,), -1, dtype=torch.int32, device="cuda") for _ in range(16)]
+    torch.cuda.synchronize()
+    f = 0
+    plan = []
+    for rnd in range(3):
+        s = torch.cuda.Stream()
+        for _ in range(5):
+            r.render_device(outs[f].data_ptr(), f, stream=s.cuda_stream)
+            plan.append(f)
+            f += 1
+        s.synchronize()
+        del s                                  # (the handle may be reused by the next stream)
+    for k in range(1):
+        a = torch.cuda.Stream()
+        r.render_device(outs[f].data_ptr(), f, stream=a.cuda_stream)
+        plan.append(f)
+        f += 1
+    torch.cuda.synchronize()
+    for f in plan:
+        got = outs[f].cpu().numpy().view(np.uint32).reshape(h, w)
+        ref, _ = ot.render(w, h, frame=f)
+        assert np.array_equal(got, ref), (f, int((got != ref).sum()))
+    g.close()
