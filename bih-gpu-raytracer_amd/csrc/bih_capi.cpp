@@ -2101,9 +2101,9 @@ int bih_sync(const bih_tree *tr, void *stream) {
             const unsigned long long *cb = reinterpret_cast<const unsigned long long *>(c + 48);
             fprintf(stderr,
                     "bin-counters packets %u lanes %u entries %u mt %u found %u verified %u"
-                    " unverified %u packets-with-miss %u planned %u plan-disagrees %u"
+                    " unverified %u packets-with-miss %u planned %u plan-disagrees %u cache-hits %u"
                     " | cycles walk %llu verify %llu\n",
-                    c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], c[39], c[38], cb[0], cb[1]);
+                    c[40], c[41], c[42], c[43], c[44], c[45], c[46], c[47], c[39], c[38], c[52], cb[0], cb[1]);
             const unsigned long long *ph = reinterpret_cast<const unsigned long long *>(c + 64);
             fprintf(stderr,
                     "bin-phases (wave cycles) queue %llu background %llu setup %llu walk %llu verify %llu"

@@ -680,6 +680,24 @@ __device__ __forceinline__ bool prim_hit(const sf32x16 r, float dx, float dy, fl
     return ok_u && !(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX;
 }
 
+// prim_hit with the record in this lane's registers (each lane its own
+// triangle: the lane's hit in the previous frame of an item, k_render_bins'
+// hit cache): the same f32 expressions in the same order, no wave-level
+// early-outs.  r0..r2 = record words 0..11, t = word 12 (tnum).
+__device__ __forceinline__ bool prim_hit_lane(const float4 r0, const float4 r1, const float4 r2, float tn, float dx,
+                                              float dy, float dz) {
+    const float e1x = r0.x, e1y = r0.y, e1z = r0.z, e2x = r0.w, e2y = r1.x, e2z = r1.y;
+    const float px = dy * e2z - e2y * dz;            // pvec = cross(D, e2)
+    const float py = dz * e2x - e2z * dx;
+    const float pz = dx * e2y - e2x * dy;
+    const float det = (e1x * px + e1y * py) + e1z * pz;
+    const float inv = 1.0f / det;
+    const float u = ((r1.z * px + r1.w * py) + r2.x * pz) * inv;
+    const float v = ((dx * r2.y + dy * r2.z) + dz * r2.w) * inv;
+    const float t = tn * inv;
+    return !(det <= kDetEps) && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && t > 0.0f && t < FLT_MAX;
+}
+
 template <bool ANYHIT, bool STATS, int LOG2SPP>
 __global__ void __launch_bounds__(kThreads) k_render_packet(const RenderArgs a) {
     constexpr uint32_t SPP = 1u << LOG2SPP;
@@ -1654,6 +1672,13 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #ifndef BIH_BIN_SETBITS
 #define BIH_BIN_SETBITS 1   // 0: the per-entry mask check (v_readlane + scalar test per entry)
 #endif
+#ifndef BIH_HIT_CACHE
+#define BIH_HIT_CACHE 1   // 0: every frame of an item walks the tile's list from its start (A/B)
+#endif
+constexpr uint32_t kNoCache = 0xFFFFFFFFu;
+#ifndef BIH_PATHV_SKIP
+#define BIH_PATHV_SKIP 0
+#endif
 #ifndef BIH_BIN_LOOP2
 #define BIH_BIN_LOOP2 1   // 0: the entry loop tests todo && rem every entry (A/B)
 #endif
@@ -1984,6 +2009,9 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
     if (cand >> 31) return true;
     meta &= 0xFFFFu;                   // (bits 16-31: the entry's pixel mask)
     const uint32_t n = meta & 3u;
+#if BIH_PATHV_SKIP
+    if (n == 3u) return true;   // timing experiment only: wrong pixels
+#endif
     if (n == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
     // the triangle's plan values (its k_bin_fp record; the same in every list)
     const float4 v = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * cent + 3];
@@ -2204,6 +2232,9 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
     constexpr uint32_t TW = TileShape<LOG2SPP>::TW, TH = TileShape<LOG2SPP>::TH;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     __shared__ uint32_t s_rs[5][kThreads];   // each lane's XORWOW state between the frames of an item
+#if BIH_HIT_CACHE
+    __shared__ uint32_t s_hc[3][kThreads];   // each lane's hit of the item's previous frame: {record, leaf, plan}
+#endif
 #if BIH_REC_LDS
     // per wave: the intersector records (tri_prim, 13 of 16 words) of its
     // item's first 64 list entries, loaded once and read by every frame of
@@ -2373,6 +2404,9 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
 #pragma unroll
             for (int i = 0; i < 5; ++i) s_rs[i][tid] = v[i];
         }
+#if BIH_HIT_CACHE
+        s_hc[0][tid] = kNoCache;
+#endif
         uint32_t lrec_n = 0;
 #if BIH_REC_LDS
         if (nf - f0 >= 2u) {
@@ -2452,9 +2486,34 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
             const bool bins_ok = *a.bin_gstat != kBinsUnusable;
             if (live && sc.U > 1 && bins_ok && !(a.dbg & 8u)) {
                 uint32_t cand = 0, cmeta = 0, cent = 0, fc_ent = 0, fc_mt = 0, pf = 0;
-                const unsigned long long found = bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
-                    a, prims, bin, uf, vf, dx, dy, dz, live, lane, cand, cmeta, cent, fc_ent, fc_mt, pf, lrec,
-                    lrec_n);
+                // Hit cache (frames after an item's first): a lane first tests
+                // the triangle it hit in the item's previous frame -- the exact
+                // intersector on the new ray, then that candidate's verification
+                // plan.  Any verified candidate proves the hit Color() needs
+                // (a lane of the reference walk that reaches an accepting
+                // triangle), whatever the order the candidates are tried in; a
+                // lane it does not prove walks the list as before, and only a
+                // full walk proves a miss.  The jitter moves a sample within its
+                // pixel, so most lanes hit the same small triangle again.
+                unsigned long long chit = 0ull;
+#if BIH_HIT_CACHE
+                if (fj > f0 && !(a.dbg & 20u)) {
+                    const uint32_t cti = s_hc[0][tid];
+                    bool okc = false;
+                    if (in_box && cti != kNoCache) {
+                        const float4 *rp = reinterpret_cast<const float4 *>(a.tri_prim) + 4ull * cti;
+                        const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+                        const float tn = reinterpret_cast<const float *>(rp)[12];
+                        okc = prim_hit_lane(r0, r1, r2, tn, dx, dy, dz) &&
+                              plan_verify(a, s_hc[1][tid], s_hc[2][tid], cti, ix, iy, iz, tMin, tMax);
+                    }
+                    chit = __ballot(okc);
+                }
+#endif
+                const unsigned long long wlive = live & ~chit;
+                const unsigned long long found = wlive ? bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
+                    a, prims, bin, uf, vf, dx, dy, dz, wlive, lane, cand, cmeta, cent, fc_ent, fc_mt, pf, lrec,
+                    lrec_n) : 0ull;
                 if (COST) work += fc_ent + 4u * fc_mt;
 #if BIH_BINS_TIMELINE
                 tl_ent += fc_ent;
@@ -2475,8 +2534,19 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
 #endif
                 const bool ok = ((found >> lane) & 1ull) &&
                                 ((a.dbg & 16u) || plan_verify(a, cand, cmeta, cent, ix, iy, iz, tMin, tMax));
-                hits = __ballot(ok);
-                undecided = live & found & ~hits;
+                hits = __ballot(ok) | chit;
+                undecided = wlive & found & ~hits;
+#if BIH_HIT_CACHE
+                // the next frame of the item tries this one first (also a hit
+                // among the list's first entries: every lane the cache settles
+                // leaves the walk, whose pixel masks then skip more entries --
+                // caching only hits past the 4th / 12th entry was slower, r06l)
+                if (ok && fj + 1u < nf) {
+                    s_hc[0][tid] = cent;
+                    s_hc[1][tid] = cand;
+                    s_hc[2][tid] = cmeta;
+                }
+#endif
                 BIH_PH(4);
 #if BIH_FAST_COUNTERS
                 {   // bin counters (bih_sync prints them): candidates decided by a
@@ -2495,7 +2565,8 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                         atomicAdd(a.work + 44, (uint32_t)__popcll(found));
                         atomicAdd(a.work + 45, (uint32_t)__popcll(hits));
                         atomicAdd(a.work + 46, (uint32_t)__popcll(undecided));
-                        atomicAdd(a.work + 47, found != live ? 1u : 0u);
+                        atomicAdd(a.work + 47, found != wlive ? 1u : 0u);
+                        atomicAdd(a.work + 52, (uint32_t)__popcll(chit));
                     }
                 }
 #endif
