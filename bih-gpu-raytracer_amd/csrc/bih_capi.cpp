@@ -94,6 +94,13 @@ struct CamSet {
     uint32_t q_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t *q_list = nullptr, *q_hdr = nullptr;
     bool q_cost = false;             // the queue is ordered by measured tile costs (launch_bin_queue's cost)
+    // k_render_bins' hit cache across launches (RenderArgs::hcache): hc_tiles x
+    // 64 lanes' last hit triangles, then hc_tiles stamps (zeroed when
+    // allocated); valid for a tile while its stamp equals hseq, which changes
+    // whenever the queue's key (image, rows, bins generation) does
+    uint32_t *hc = nullptr;
+    size_t hc_tiles = 0;
+    uint32_t hseq = 0;
     uint32_t uses = 0;               // frustum-bin renders since these bins were built
     // the last launch that measured tile costs (bins.cost) was over q_key ==
     // cost_key: the next queue of those rows is built from them
@@ -219,6 +226,7 @@ struct bih_tree {
     int cs_cur = 0;                  // set of the latest render's camera
     int slot_cs[kSlots] = {};        // set the slot's last render read
     uint32_t bins_gen = 0;           // incremented by every bins build (any set)
+    uint32_t hseq_ctr = 0;           // the camera sets' hit-cache sequence numbers (CamSet::hseq), never 0
     // per render slot two sets of 8 band heads (32 words apart): a launch
     // draws from set q_par[slot] and zeroes the other for the slot's next launch
     uint32_t *q_count = nullptr;
@@ -647,6 +655,7 @@ void bih_free(bih_tree *tr) {
         if (c.bins_mem) (void)hipFree(c.bins_mem);
         if (c.bin_list) (void)hipFree(c.bin_list);
         if (c.q_mem) (void)hipFree(c.q_mem);
+        if (c.hc) (void)hipFree(c.hc);
         if (c.ev_bins) (void)hipEventDestroy(c.ev_bins);
         if (c.bins_host) (void)hipHostFree(c.bins_host);
     }
@@ -705,7 +714,8 @@ int bih_tree_get_info(const bih_tree *tr, bih_tree_info *info) {
     // per-slot accumulators, the host-path framebuffer, the per-camera
     // records, and the per-slot tile queues, spill areas and chunk orders
     size_t cam = 0;
-    for (const CamSet &c : tr->cs) cam += c.prim_cap + c.bins_mem_cap + c.bin_list_cap * kEntryBytes + c.q_cap;
+    for (const CamSet &c : tr->cs)
+        cam += c.prim_cap + c.bins_mem_cap + c.bin_list_cap * kEntryBytes + c.q_cap + c.hc_tiles * 65 * 4;
     info->device_bytes = tr->t.bytes + tr->back[0].bytes + tr->back[1].bytes + (tr->rng_cap * (5 * kRngBufs + kSlots) + tr->fb_cap) * 4 + cam +
                          ((size_t)kSlots * (bih::kWorkWords + tr->spill_per_slot) +
                           (size_t)kSlots * 2 * tr->chunk_cap +
@@ -990,6 +1000,16 @@ static bool cost_queue_enabled() {
     return on;
 }
 
+// k_render_bins' hit cache across launches unless BIH_HIT_CACHE_XL=0 (A/B);
+// it never changes a pixel.
+static bool hit_cache_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("BIH_HIT_CACHE_XL");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 // Frustum bins are on unless BIH_BINS=0 (A-B); they never change a pixel.
 static bool bins_enabled() {
     static const bool on = [] {
@@ -1204,7 +1224,19 @@ static void resolve_bins(CamSet &c, bool block) {
 
 // A camera set's tile-queue memory for `ntiles` tiles (its renders in
 // flight may read the old one).
-static int ensure_queue_mem(bih_tree *tr, CamSet &c, uint32_t ntiles) {
+static int ensure_queue_mem(bih_tree *tr, CamSet &c, uint32_t ntiles, hipStream_t st) {
+    if (c.hc_tiles < ntiles) {
+        // the hit cache: its stamps start at 0, which no queue's hseq is
+        int rc = drain_renders(tr);
+        if (rc) return rc;
+        if (c.hc) (void)hipFree(c.hc);
+        c.hc = nullptr;
+        c.hc_tiles = 0;
+        hipError_t e = tree_malloc(tr, &c.hc, (size_t)ntiles * 65 * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(c.hc + (size_t)ntiles * 64, 0, (size_t)ntiles * sizeof(uint32_t), st);
+        if (e != hipSuccess) return map_hip((int)e);
+        c.hc_tiles = ntiles;
+    }
     const size_t need = bih::bin_queue_bytes(ntiles);
     if (c.q_cap >= need) return BIH_OK;
     int rc = drain_renders(tr);
@@ -1244,8 +1276,13 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
         // measured the costs)
         rc = wait_set_readers(tr, ci, st);
         if (rc) return rc;
-        rc = ensure_queue_mem(tr, c, ntiles);
+        rc = ensure_queue_mem(tr, c, ntiles, st);
         if (rc) return rc;
+        if (!c.q_valid || memcmp(key, c.q_key, sizeof key) != 0) {
+            // other tiles, rows or bins: the cached hits of the old queue are void
+            c.hseq = ++tr->hseq_ctr;
+            if (c.hseq == 0) c.hseq = ++tr->hseq_ctr;
+        }
         int le = bih::launch_bin_queue(c.bins.off, c.bins.gcount + 1, c.bins.bins_x, tiles_x, ntiles, rows.row0,
                                        rows.band_h, rows.band_step, th, c.q_mem, &c.q_list, &c.q_hdr,
                                        st, measured ? c.bins.cost : nullptr);
@@ -1271,6 +1308,11 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
     a.bin_queue = c.q_list;
     a.bin_qhdr = c.q_hdr;
+    if (hit_cache_enabled() && c.hc && c.hc_tiles >= ntiles) {
+        a.hcache = c.hc;
+        a.hstamp = c.hc + c.hc_tiles * 64;
+        a.hseq = c.hseq;
+    }
     // timing experiments (BIH_DBG bits: skip phases or checks; they change
     // pixels, so only a BIH_DEBUG_KNOBS=1 build reads them) and the fallback
     // test mode (routes packets to the exact walk: same pixels)
@@ -1748,7 +1790,7 @@ int bih_reserve(bih_tree *tr, uint32_t w, uint32_t h, uint32_t spp, const bih_ro
     uint32_t tw = 0, th = 0;
     tile_shape(spp, &tw, &th);
     const uint32_t ntiles = ((w + tw - 1) / tw) * ((rows.nrows + th - 1) / th);
-    for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles);
+    for (int k = 0; k < cam_sets() && !rc; ++k) rc = ensure_queue_mem(tr, tr->cs[k], ntiles, tr->stream);
     if (!rc) rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, (size_t)ntiles * max_frames, 8);
     if (!rc && stamps_enabled()) rc = ensure_stamps(tr, ntiles, tr->stream);
     if (rc) return rc;

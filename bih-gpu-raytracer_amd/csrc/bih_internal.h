@@ -151,6 +151,13 @@ struct RenderArgs {
     // the gap).  null: rng_in (the k_rng_advance ring).
     unsigned long long *stamps = nullptr;
     uint32_t *st_buf0 = nullptr, *st_buf1 = nullptr;
+    // k_render_bins' hit cache across launches: per local tile 64 lanes'
+    // last hit triangles (hcache) and a stamp (hstamp) -- valid while it
+    // equals hseq, the camera set's queue sequence number (bih_capi.cpp); null:
+    // the cache lives within an item only
+    uint32_t *hcache = nullptr;
+    uint32_t *hstamp = nullptr;
+    uint32_t hseq = 0;
     uint32_t st_f0 = 0;     // the launch's first frame
     uint32_t st_seq = 0;    // this launch's sequence number (1 .. 1023)
 };

@@ -1676,6 +1676,9 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #define BIH_HIT_CACHE 1   // 0: every frame of an item walks the tile's list from its start (A/B)
 #endif
 constexpr uint32_t kNoCache = 0xFFFFFFFFu;
+#ifndef BIH_CACHE_MINLEN
+#define BIH_CACHE_MINLEN 16   // list entries from which a tile's items use the hit cache
+#endif
 #ifndef BIH_PATHV_SKIP
 #define BIH_PATHV_SKIP 0
 #endif
@@ -2406,6 +2409,25 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
         }
 #if BIH_HIT_CACHE
         s_hc[0][tid] = kNoCache;
+        // (tiles with short lists: the walk finds a lane's triangle about as
+        // fast as the cache test would -- a record gather and a full
+        // intersector call per lane -- so they walk every frame)
+        const bool use_cache = ((const uint32_t *)a.bin_off)[bin + 1] - ((const uint32_t *)a.bin_off)[bin] >=
+                               BIH_CACHE_MINLEN;
+        // the lane's hit of the tile's last item (an earlier launch of this
+        // camera set's current queue, RenderArgs::hcache): valid while the
+        // tile's stamp is the queue's sequence number; the triangle's leaf
+        // word and plan come from its record (the words every list entry of
+        // the triangle carries)
+        if (use_cache && a.hcache && valid && a.hstamp[tile] == a.hseq) {
+            const uint32_t ti = a.hcache[(uint64_t)tile * 64 + lane];
+            if (ti < a.hdr_n_tris) {
+                const float4 m = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * ti + 2];
+                s_hc[0][tid] = ti;
+                s_hc[1][tid] = __float_as_uint(m.z);
+                s_hc[2][tid] = __float_as_uint(m.w);
+            }
+        }
 #endif
         uint32_t lrec_n = 0;
 #if BIH_REC_LDS
@@ -2497,7 +2519,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 // pixel, so most lanes hit the same small triangle again.
                 unsigned long long chit = 0ull;
 #if BIH_HIT_CACHE
-                if (fj > f0 && !(a.dbg & 20u)) {
+                if (use_cache && !(a.dbg & 20u)) {
                     const uint32_t cti = s_hc[0][tid];
                     bool okc = false;
                     if (in_box && cti != kNoCache) {
@@ -2541,7 +2563,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 // among the list's first entries: every lane the cache settles
                 // leaves the walk, whose pixel masks then skip more entries --
                 // caching only hits past the 4th / 12th entry was slower, r06l)
-                if (ok && fj + 1u < nf) {
+                if (use_cache && ok) {
                     s_hc[0][tid] = cent;
                     s_hc[1][tid] = cand;
                     s_hc[2][tid] = cmeta;
@@ -2596,6 +2618,12 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
             BIH_PH(5);
         }
         if (COST && lane == 0) a.bin_cost[bin] = (work << 8) / (nf - f0);
+#if BIH_HIT_CACHE
+        if (use_cache && a.hcache) {   // for the tile's next item (a later launch)
+            if (valid) a.hcache[(uint64_t)tile * 64 + lane] = s_hc[0][tid];
+            if (lane == 0) a.hstamp[tile] = a.hseq;
+        }
+#endif
         if (STAMP && nf == a.nframes && lane == 0) {
             // (the item ending at the launch's last frame) the tile's new stamp
             const StampBase sb = stamp_base(a.stamps[tile], a.st_seq);
