@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=4)
-    ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--band", type=int, default=4,
+                    help="rows per band of the N > 1 row split (a multiple of the 4-row packet tile; 4 balances the ranks best: 1080 rows = 270 bands)")
     ap.add_argument("--in-flight", type=int, default=3,
                     help="frames in flight: consecutive frames on this many streams, so the "
                          "next frame fills the tail of the one before (1 = one frame at a time)")
@@ -913,6 +914,24 @@ def main():
             alg["bytes_per_frame"] = alg_bytes / gl
             alg["window_gbs"] = alg_bytes / gl / (kpf * 1e-3) / 1e9
             alg["window_compulsory_gbs"] = comp_bytes / gl / (kpf * 1e-3) / 1e9
+        # What the kernel itself addresses per frame at the headline's call
+        # shape (counter build, a 16-frame call with the hit cache warm): the
+        # entries it pre-tests (48 B), its packet-level intersector records
+        # (64 B), each live lane's hit-cache record (52 B) and the per-pixel RNG
+        # and framebuffer words (24 B) -- a lower bound (whole 64-entry chunks
+        # are loaded).  Since round 6's hit cache most lanes no longer walk
+        # their tile's list, so the model above (every list entry once per
+        # frame, kept from earlier rounds for comparability) counts far more
+        # than the kernel reads.
+        hs = bc.get("headline_shape")
+        if hs and window:
+            per = (48 * hs["entries"] + 64 * hs["mt"] + 52 * hs["lanes"]) / G + 24 * pix
+            alg["addressed_bytes_per_frame"] = per
+            alg["addressed_gbs"] = per / (window["kernel_ms_per_frame"] * 1e-3) / 1e9
+            alg["addressed_terms_per_frame"] = {k: hs[k] / G for k in ("entries", "mt", "lanes", "cache-hits")
+                                                if k in hs}
+            alg["addressed_formula"] = ("(48 x entries pre-tested + 64 x intersector calls + 52 x live lanes) per "
+                                        "frame of a 16-frame call + 24 x pixels (counter build)")
     # the issue roofline of the same kernel: VALU wave-instructions (PMC,
     # SQ_INSTS_VALU per launch of the headline shape) at 2 cycles each on a
     # SIMD (a wave64 VALU op issues over 2 cycles: MI355X_MICROARCH.md), over
@@ -1018,6 +1037,7 @@ def main():
                 "window": window,
                 "issue": issue,
                 "frac_isolated_launches": alg["gbs"] / HBM_PEAK_GBS if alg else None,
+                "frac_addressed": (alg["addressed_gbs"] / HBM_PEAK_GBS) if alg and "addressed_gbs" in alg else None,
                 "fallback_ms": (sum(tails_iso) / len(tails_iso)) if tails_iso else None,
                 "frames_per_launch": G if trav == 0 else 1,
                 "launch_ms_source": (f"HIP events around the render kernel on its stream "
@@ -1356,18 +1376,27 @@ def bin_counters(args, env):
     import subprocess
     if not os.path.exists(FC_LIB):
         return None
-    cmd = [sys.executable, os.path.join(ROOT, "tools", "fast_counters.py"), "--frames", "2",
-           "--tris", str(args.tris), "--width", str(args.width), "--height", str(args.height)]
-    try:
-        p = subprocess.run(cmd, env=dict(env, BIH_LIB=FC_LIB), capture_output=True, text=True,
-                           timeout=300)
-    except (OSError, subprocess.TimeoutExpired):
-        return None
-    lines = [l for l in p.stderr.splitlines() if l.startswith("bin-counters")]
-    if p.returncode != 0 or not lines:
-        return None
-    tok = lines[-1].split("|")[0].split()[1:]
-    return {k: int(v) for k, v in zip(tok[0::2], tok[1::2])}
+
+    def run(extra):
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "fast_counters.py"), "--tris", str(args.tris),
+               "--width", str(args.width), "--height", str(args.height)] + extra
+        try:
+            p = subprocess.run(cmd, env=dict(env, BIH_LIB=FC_LIB), capture_output=True, text=True,
+                               timeout=300)
+        except (OSError, subprocess.TimeoutExpired):
+            return None
+        lines = [l for l in p.stderr.splitlines() if l.startswith("bin-counters")]
+        if p.returncode != 0 or not lines:
+            return None
+        tok = lines[-1].split("|")[0].split()[1:]
+        return {k: int(v) for k, v in zip(tok[0::2], tok[1::2])}
+
+    res = run(["--frames", "2"])
+    if res is not None and args.group > 1:
+        # the headline's call shape: the third call of G frames (hit cache
+        # warm), totals over its G frames
+        res["headline_shape"] = run(["--frames", "3", "--group", str(args.group)])
+    return res
 
 
 if __name__ == "__main__":
