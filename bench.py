@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[2]): 1,000,000-triangle
 random soup (splitmix64 seed 1), 1920x1080, 4 jittered primary rays per
 pixel, reference camera, cuRAND-XORWOW seed 1984.  One step = one frame
 pass.  With N GPUs (the north star's decomposition) every frame is
-cut into interleaved 8-row bands dealt round-robin to the ranks; each rank
+cut into interleaved 4-row bands dealt round-robin to the ranks; each rank
 renders its bands with global pixel indices (so the frame is byte-identical
 to a one-GPU render) and ONE RCCL gather per frame brings the bands to rank 0,
 which lays them out in frame order (bihrt.tiling.BandGather) -- strong
