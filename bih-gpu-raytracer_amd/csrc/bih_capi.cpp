@@ -819,6 +819,20 @@ static bool share_alternating() {
     return on;
 }
 
+// Items per multi-frame k_render_bins launch the kernel aims at from the
+// queue's live tile count (RenderArgs::live_items; BIH_LIVE_ITEMS for A/B,
+// 0: item_split's count of all tiles decides).  A/B (r06u, 16 frames per
+// call): 1M soup at 1080p (24k live tiles) one item per tile either way;
+// the 69k torus (7.3k live) 0.0255 -> 0.0221 ms per frame in items of 8
+// frames; 30000 (items of 4) 0.0229
+static uint32_t live_items_target() {
+    static const uint32_t n = [] {
+        const char *e = getenv("BIH_LIVE_ITEMS");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 16384u;
+    }();
+    return n;
+}
+
 // k_render_bins' static queue rounds in one-frame launches (BinQueue;
 // BIH_STATIC_ROUNDS for A/B: one-frame calls 1 round 0.0824 ms, 2 0.0822,
 // 3 0.086, 5 0.106 -- a wave cannot hand on its later static items, r05n)
@@ -1303,6 +1317,7 @@ static int prepare_bin_queue(bih_tree *tr, CamSet &c, int ci, uint32_t w, uint32
     a.hsplit = a.nsplit;
     if (c.q_cost && nframes >= 4)
         a.hsplit = std::max(a.nsplit, std::min(nframes, a.nsplit * (nframes >= 8 ? 4u : 2u)));
+    if (a.live_items && c.q_cost && nframes >= 4) a.live_items |= 0x80000000u;   // (the kernel's split: heavy tiles too)
     rc = ensure_per_slot(tr, &tr->fb_mem, &tr->fbq_cap, nrec, 8);
     if (rc) return rc;
     a.bin_fb = tr->fb_mem + (size_t)slot * tr->fbq_cap * 8;
@@ -1580,6 +1595,7 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         // bands, 8 frames per call: items of 8 frames 0.0107 ms per frame, of
         // 2 0.0078; 16 per call, items of 4: 0.0069)
         item_split(tr, w, rows.nrows, spp, nframes, &a.fpi, &a.nsplit);
+        a.live_items = live_items_target();
     } else {
         a.fpi = nframes;
         a.nsplit = 1;

@@ -133,6 +133,10 @@ struct RenderArgs {
     // item so that the items still outnumber the waves
     uint32_t fpi = 1;
     uint32_t nsplit = 1;
+    // (non-zero) k_render_bins chooses the split itself from the queue's live
+    // tile count: about live_items items per launch (fpi / nsplit above
+    // only serve without it); bit 31: heavy tiles split further (hsplit)
+    uint32_t live_items = 0;
     // k_render_bins: queue rounds each wave takes without atomics (BinQueue)
     uint32_t static_rounds = 1;
     // one-frame k_render_bins (config C4's primary rays): per local tile the

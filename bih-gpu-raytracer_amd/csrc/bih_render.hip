@@ -1676,6 +1676,9 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #define BIH_HIT_CACHE 1   // 0: every frame of an item walks the tile's list from its start (A/B)
 #endif
 constexpr uint32_t kNoCache = 0xFFFFFFFFu;
+#ifndef BIH_HC_EARLY
+#define BIH_HC_EARLY 0   // loads ahead of use: 1 stamp and entry together, 2 the record before the ray (A/B r06r-s: within noise)
+#endif
 #ifndef BIH_CACHE_MINLEN
 #define BIH_CACHE_MINLEN 16   // list entries from which a tile's items use the hit cache
 #endif
@@ -2001,6 +2004,24 @@ __device__ __forceinline__ bool scene_slab(const SceneU &sc, float dx, float dy,
 #define BIH_SLAB_AGAIN 0   // 1: 72 VGPRs, 7 waves, but 0.0420 vs 0.0413 ms per frame (A/B r04n)
 #endif
 
+// A plan's 1-2 critical comparisons (meta & 3 of them) on its values v
+__device__ __forceinline__ bool plan_values_check(uint32_t meta, const float4 v, float ix, float iy, float iz,
+                                                  float tMin, float tMax) {
+    const uint32_t n = meta & 3u;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) {
+        if (c >= n) break;
+        const uint32_t m = meta >> (2 + 6 * c);
+        const float vk = c ? v.z : v.x, vp = c ? v.w : v.y;
+        const float tk = vk * sel3(m & 3u, ix, iy, iz);
+        const bool is_exit = (m & 4u) != 0u;
+        const float tp = (m & 32u) ? (is_exit ? tMin : tMax) : vp * sel3((m >> 3) & 3u, ix, iy, iz);
+        ok = ok && (is_exit ? (tk > tp) : !(tk > tp));
+    }
+    return ok;
+}
+
 // The candidate's verification plan (triangle_plan, bih_bins.hip): the
 // entry's leaf carries bit 31 when every decision on its root path is
 // proven; otherwise meta & 3 = 1-2 critical comparisons, each t_k against
@@ -2017,19 +2038,21 @@ __device__ __forceinline__ bool plan_verify(const RenderArgs &a, uint32_t cand, 
 #endif
     if (n == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
     // the triangle's plan values (its k_bin_fp record; the same in every list)
-    const float4 v = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * cent + 3];
-    bool ok = true;
-#pragma unroll
-    for (uint32_t c = 0; c < 2; ++c) {
-        if (c >= n) break;
-        const uint32_t m = meta >> (2 + 6 * c);
-        const float vk = c ? v.z : v.x, vp = c ? v.w : v.y;
-        const float tk = vk * sel3(m & 3u, ix, iy, iz);
-        const bool is_exit = (m & 4u) != 0u;
-        const float tp = (m & 32u) ? (is_exit ? tMin : tMax) : vp * sel3((m >> 3) & 3u, ix, iy, iz);
-        ok = ok && (is_exit ? (tk > tp) : !(tk > tp));
-    }
-    return ok;
+    return plan_values_check(meta, reinterpret_cast<const float4 *>(a.bin_rec)[4ull * cent + 3], ix, iy, iz,
+                             tMin, tMax);
+}
+
+// plan_verify with the plan values already loaded (the hit cache's
+// candidate: loaded before the frame's ray is made)
+__device__ __forceinline__ bool plan_verify_v(const RenderArgs &a, uint32_t cand, uint32_t meta, const float4 v,
+                                              float ix, float iy, float iz, float tMin, float tMax) {
+    if (cand >> 31) return true;
+    meta &= 0xFFFFu;
+#if BIH_PATHV_SKIP
+    if ((meta & 3u) == 3u) return true;
+#endif
+    if ((meta & 3u) == 3u) return path_verify(a.bin_path, cand, ix, iy, iz, tMin, tMax);
+    return plan_values_check(meta, v, ix, iy, iz, tMin, tMax);
 }
 
 // ---------------------------------------------------------------------------
@@ -2276,6 +2299,24 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
     q.ns = a.nsplit;   // an item covers a tile in a.fpi consecutive frames of the launch
     q.hs = a.hsplit;
     q.hv = 0;
+    uint32_t fpi = a.fpi;
+    if (a.live_items && a.nframes > 1u) {
+        // items per live tile from the queue's live count (the same in every
+        // wave): a launch over few live tiles -- a small mesh, a rank's bands
+        // -- splits its tiles' frames so that the items still outnumber the
+        // waves; one over many keeps every frame of a tile in one item
+        uint32_t live = 0;
+        for (uint32_t b = 0; b < 8u; ++b) live += q.hdr[b].y;
+        const uint32_t target = a.live_items & 0x7FFFFFFFu;
+        uint32_t ns = live ? (target + live / 2u) / live : a.nframes;
+        ns = ns < 1u ? 1u : (ns > a.nframes ? a.nframes : ns);
+        fpi = (a.nframes + ns - 1u) / ns;
+        ns = (a.nframes + fpi - 1u) / fpi;
+        const uint32_t hx = ns * (a.nframes >= 8u ? 4u : 2u);
+        q.ns = ns;
+        q.hs = (a.live_items >> 31) ? (hx < a.nframes ? hx : a.nframes) : ns;
+        if (q.hs < ns) q.hs = ns;
+    }
     const uint32_t fhv = (a.nframes + q.hs - 1u) / q.hs;   // frames per item of a heavy tile
     uint32_t it = 0;
 #if BIH_QUEUE_STATIC
@@ -2338,8 +2379,8 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 if (k < nx) {
                     const uint32_t j = k / q.ns, sp = k - j * q.ns;
                     it = q.hv + j;
-                    f0 = sp * a.fpi;
-                    nf = f0 + a.fpi < a.nframes ? f0 + a.fpi : a.nframes;
+                    f0 = sp * fpi;
+                    nf = f0 + fpi < a.nframes ? f0 + fpi : a.nframes;
                 } else {
                     it = hb.y + (k - nx);
                 }
@@ -2419,8 +2460,17 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
         // tile's stamp is the queue's sequence number; the triangle's leaf
         // word and plan come from its record (the words every list entry of
         // the triangle carries)
+#if BIH_HC_EARLY & 1
+        // (stamp and entry read together, the entry discarded unless the
+        // stamp matches: one round trip, not two)
+        if (use_cache && a.hcache && valid) {
+            const uint32_t st = a.hstamp[tile];
+            const uint32_t ti0 = a.hcache[(uint64_t)tile * 64 + lane];
+            const uint32_t ti = st == a.hseq ? ti0 : kNoCache;
+#else
         if (use_cache && a.hcache && valid && a.hstamp[tile] == a.hseq) {
             const uint32_t ti = a.hcache[(uint64_t)tile * 64 + lane];
+#endif
             if (ti < a.hdr_n_tris) {
                 const float4 m = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * ti + 2];
                 s_hc[0][tid] = ti;
@@ -2464,6 +2514,25 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
         for (uint32_t fj = f0; fj < nf; ++fj, dfr += 2u * SPP * kWeyl) {
             uint32_t *const fout = a.out + (uint64_t)fj * a.out_stride;
             float dx = 0.f, dy = 0.f, dz = 1.f, uf = 0.f, vf = 0.f;
+#if BIH_HIT_CACHE && (BIH_HC_EARLY & 2)
+            // the cached candidate's intersector record and plan values,
+            // requested before the ray is made (they depend on the lane's
+            // last hit only), so that their round trip overlaps the jitter
+            uint32_t cti = kNoCache;
+            float4 cr0 = make_float4(0.f, 0.f, 0.f, 0.f), cr1 = cr0, cr2 = cr0, cv = cr0;
+            float ctn = 0.f;
+            if (use_cache && valid) {
+                cti = s_hc[0][tid];
+                if (cti != kNoCache) {
+                    const float4 *rp = reinterpret_cast<const float4 *>(a.tri_prim) + 4ull * cti;
+                    cr0 = rp[0];
+                    cr1 = rp[1];
+                    cr2 = rp[2];
+                    ctn = reinterpret_cast<const float *>(rp)[12];
+                    cv = reinterpret_cast<const float4 *>(a.bin_rec)[4ull * cti + 3];
+                }
+            }
+#endif
             if (valid) {
                 // the frame's 2*SPP draws on every lane (uniform control
                 // flow); rs ends at the next frame's state
@@ -2520,6 +2589,10 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 unsigned long long chit = 0ull;
 #if BIH_HIT_CACHE
                 if (use_cache && !(a.dbg & 20u)) {
+#if BIH_HC_EARLY & 2
+                    const bool okc = in_box && cti != kNoCache && prim_hit_lane(cr0, cr1, cr2, ctn, dx, dy, dz) &&
+                                     plan_verify_v(a, s_hc[1][tid], s_hc[2][tid], cv, ix, iy, iz, tMin, tMax);
+#else
                     const uint32_t cti = s_hc[0][tid];
                     bool okc = false;
                     if (in_box && cti != kNoCache) {
@@ -2529,6 +2602,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                         okc = prim_hit_lane(r0, r1, r2, tn, dx, dy, dz) &&
                               plan_verify(a, s_hc[1][tid], s_hc[2][tid], cti, ix, iy, iz, tMin, tMax);
                     }
+#endif
                     chit = __ballot(okc);
                 }
 #endif

@@ -17,11 +17,12 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--group", type=int, default=1, help="frames per call (bih_render_device_frames)")
+    ap.add_argument("--scene", default="soup", choices=["soup", "torus"])
     a = ap.parse_args()
     import torch
     import bihrt
     s = torch.cuda.Stream()
-    tris = bihrt.scenes.soup(a.tris, seed=1)
+    tris = bihrt.scenes.soup(a.tris, seed=1) if a.scene == "soup" else bihrt.scenes.torus()
     d = torch.from_numpy(tris).cuda()
     g = bihrt.GPUArrayManager.from_device(d.data_ptr(), tris.shape[0], stream=s.cuda_stream)
     r = bihrt.Renderer(g, a.width, a.height)
@@ -33,6 +34,8 @@ def main():
         else:
             r.render_device(out.data_ptr(), f, stream=s.cuda_stream)
         r.sync(s.cuda_stream)
+    st = g.bins_stats()
+    print("scene %s bins: %s" % (a.scene, {k: getattr(st, k) for k, _ in st._fields_}), flush=True)
 
 
 if __name__ == "__main__":
