@@ -1158,6 +1158,39 @@ def test_host_loop_registered_framebuffer(gpu, bihrt_mod, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_destroyed_streams_keep_order(gpu, bihrt_mod, oracle_mod):
+    """Streams created and destroyed through the HIP runtime (not torch's
+    pool), each destroyed with its renders possibly still queued and the next
+    created at once (the handle may come back): the library orders every
+    render after the last one's state by events, never by stream identity, so
+    every frame equals the oracle's."""
+    import ctypes
+    import torch
+    torch.cuda.init()
+    hip = ctypes.CDLL("libamdhip64.so.7")          # (the runtime torch loaded)
+    tris = bihrt_mod.scenes.soup(30_000, seed=17)
+    ot = oracle_mod.OracleTree(tris)
+    w, h = 128, 96
+    g = bihrt_mod.GPUArrayManager(tris)
+    r = bihrt_mod.Renderer(g, w, h)
+    outs = [torch.full((h * w,), -1, dtype=torch.int32, device="cuda") for _ in range(20)]
+    torch.cuda.synchronize()
+    f = 0
+    for rnd in range(4):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        for _ in range(5):
+            r.render_device(outs[f].data_ptr(), f, stream=s.value)
+            f += 1
+        assert hip.hipStreamDestroy(s) == 0     # (its renders may still be queued)
+    torch.cuda.synchronize()
+    for k in range(f):
+        got = outs[k].cpu().numpy().view(np.uint32).reshape(h, w)
+        ref, _ = ot.render(w, h, frame=k)
+        assert np.array_equal(got, ref), (k, int((got != ref).sum()))
+    g.close()
+
+
 def test_recycled_stream_handles_keep_order(gpu, bihrt_mod, oracle_mod):
     """Stamped mode and the shared-grid rule key on the raw hipStream_t of
     the last render.  A stream the caller destroys and
