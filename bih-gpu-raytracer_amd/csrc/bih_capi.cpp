@@ -115,6 +115,7 @@ struct CamSet {
 // never on the render path.
 struct TreeParams {
     uint32_t item_tiles = 65536u;     // BIH_PARAM_ITEM_TILES
+    bool item_tiles_set = false;      // (set: item_split's rule decides, not the live count)
     uint32_t pair_cap = 0xFFFFFFFFu;  // BIH_PARAM_PAIR_CAP (~0: sized from N)
     uint64_t bins_cap = 0;            // BIH_PARAM_BINS_CAP (0: no cap)
     uint32_t force_fallback = 0;      // BIH_PARAM_FORCE_FALLBACK
@@ -125,7 +126,10 @@ struct TreeParams {
 static const TreeParams &env_params() {
     static const TreeParams p = [] {
         TreeParams q;
-        if (const char *v = getenv("BIH_ITEM_TILES")) q.item_tiles = (uint32_t)strtoul(v, nullptr, 10);
+        if (const char *v = getenv("BIH_ITEM_TILES")) {
+            q.item_tiles = (uint32_t)strtoul(v, nullptr, 10);
+            q.item_tiles_set = true;
+        }
         if (const char *v = getenv("BIH_PAIR_CAP")) q.pair_cap = (uint32_t)strtoul(v, nullptr, 10);
         if (const char *v = getenv("BIH_BINS_CAP")) q.bins_cap = (uint64_t)strtoull(v, nullptr, 10);
         if (const char *v = getenv("BIH_BINS_FORCE_FALLBACK")) q.force_fallback = v[0] == '1';
@@ -1595,7 +1599,8 @@ static int render_device_impl(bih_tree *tr, const bih_camera *cam, uint32_t w, u
         // bands, 8 frames per call: items of 8 frames 0.0107 ms per frame, of
         // 2 0.0078; 16 per call, items of 4: 0.0069)
         item_split(tr, w, rows.nrows, spp, nframes, &a.fpi, &a.nsplit);
-        a.live_items = live_items_target();
+        // (a caller's BIH_PARAM_ITEM_TILES keeps item_split's rule)
+        a.live_items = tr->prm.item_tiles_set ? 0u : live_items_target();
     } else {
         a.fpi = nframes;
         a.nsplit = 1;
@@ -1820,6 +1825,7 @@ int bih_tree_set_param(bih_tree *tr, int param, uint64_t value) {
     case BIH_PARAM_ITEM_TILES:
         if (value == 0 || value > 0xFFFFFFFFull) return BIH_ERR_INVALID;
         tr->prm.item_tiles = (uint32_t)value;
+        tr->prm.item_tiles_set = true;
         return BIH_OK;
     case BIH_PARAM_PAIR_CAP: {
         const uint32_t v = (uint32_t)std::min<uint64_t>(value, 0xFFFFFFFFull);

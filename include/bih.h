@@ -210,7 +210,9 @@ int bih_reserve(bih_tree *tree, uint32_t w, uint32_t h, uint32_t spp, const bih_
  * once per process from the environment variable of the same name
  * (BIH_ITEM_TILES, ...), never on the render path. */
 #define BIH_PARAM_ITEM_TILES      1  /* tile count below which a multi-frame
-                                        launch splits an item's frames (65536) */
+                                        launch splits an item's frames (65536);
+                                        unset, the render kernel splits by the
+                                        launch's live tiles (~16384 items)     */
 #define BIH_PARAM_PAIR_CAP        2  /* (triangle, tile) pair-result slots of
                                         the bins build (tests: 0 = recompute)  */
 #define BIH_PARAM_BINS_CAP        3  /* cap on bin list entries (tests: force

@@ -534,6 +534,35 @@ def test_c2_torus_1080p(gpu, bihrt_mod, oracle_mod):
     assert (imgs[0] != imgs[0][0, 0]).any()   # the torus is in view
 
 
+def test_c2_torus_calls_of_16_frames(gpu, bihrt_mod, oracle_mod):
+    """Config C2's call shape: the torus's ~7.3k live tiles make
+    k_render_bins split each tile's 16 frames into items of 8 itself
+    (RenderArgs::live_items, from the queue's live count), and from the
+    second call on (measured tile costs) split its heavy tiles further.
+    Three calls of 16 frames: frames 0, 15, 16, 31 and 47 equal the reference
+    walk's one-frame renders of the same indices, frame 47 the oracle on every
+    16th row."""
+    import torch
+    tris = bihrt_mod.scenes.torus()
+    g = bihrt_mod.GPUArrayManager(tris)
+    w, h = 1920, 1080
+    P = w * h
+    r = bihrt_mod.Renderer(g, w, h)
+    out = torch.full((16 * P,), -1, dtype=torch.int32, device="cuda")
+    got = {}
+    for c in range(3):
+        r.render_device_frames(out.data_ptr(), 16 * c, 16, P)
+        r.sync()
+        o = out.cpu().numpy().view(np.uint32).reshape(16, h, w)
+        for j in (0, 15):
+            got[16 * c + j] = o[j].copy()
+    for f in (0, 15, 16, 31, 47):
+        ref = _device_render(bihrt_mod, g, w, h, 4, f, bihrt_mod.TRAVERSE_REFERENCE)
+        assert np.array_equal(got[f], ref), (f, int((got[f] != ref).sum()))
+    oref, _ = oracle_mod.OracleTree(tris).render(w, h, frame=47, rows=(0, (h + 15) // 16, 16))
+    assert np.array_equal(got[47][::16], oref)
+
+
 def test_bins_list_total_past_u32_renders_without_bins(gpu, bihrt_mod):
     """33,500 front-facing triangles that each cover the whole 1080p image:
     the frustum-bin lists would hold 33,500 x 129,600 > 2^32 entries.  The
