@@ -1676,6 +1676,12 @@ __device__ __forceinline__ unsigned long long prim_hits_pre(const sf32x16 r, flo
 #define BIH_HIT_CACHE 1   // 0: every frame of an item walks the tile's list from its start (A/B)
 #endif
 constexpr uint32_t kNoCache = 0xFFFFFFFFu;
+#ifndef BIH_ENT_LDS
+#define BIH_ENT_LDS 1   // bin_walk's pre-tests read their entry from LDS (broadcast), not by v_readlane
+#endif
+#if BIH_ENT_LDS && !BIH_BIN_SETBITS
+#error "BIH_ENT_LDS writes the chunk where the set-bits walk ballots it"
+#endif
 #ifndef BIH_HC_EARLY
 #define BIH_HC_EARLY 0   // loads ahead of use: 1 stamp and entry together, 2 the record before the ray (A/B r06r-s: within noise)
 #endif
@@ -1724,7 +1730,8 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                                                       uint32_t lane, uint32_t &cand, uint32_t &cmeta,
                                                       uint32_t &cent, uint32_t &fc_ent,
                                                       uint32_t &fc_mt, uint32_t &pf,
-                                                      const float4 *lrec = nullptr, uint32_t lrec_n = 0) {
+                                                      const float4 *lrec = nullptr, uint32_t lrec_n = 0,
+                                                      float4 *lent = nullptr) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
     const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
@@ -1765,6 +1772,17 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
             // the entries the per-entry mask check below would pre-test
             const uint32_t pm = __float_as_uint(d2.w) >> 16;
             unsigned long long todo = __ballot(lane < n && (!PMASK || (pm & rpix)));
+#if BIH_ENT_LDS
+            // the chunk's entries in the wave's LDS slots (lane j: entry j):
+            // each pre-test then reads its entry's 9 plane words as one
+            // broadcast instead of 9 v_readlane (12 fewer VALU per entry)
+            lent[3 * lane] = d0;
+            lent[3 * lane + 1] = d1;
+            lent[3 * lane + 2] = d2;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 #if BIH_BIN_PREFETCH
             if (e + 64u < end) bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
 #endif
@@ -1788,12 +1806,20 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
 #endif
                 if (PMASK && !((__builtin_amdgcn_readlane(__float_as_uint(d2.w), j) >> 16) & rpix)) continue;
 #endif
+#if BIH_ENT_LDS
+                const float4 q0 = lent[3 * j], q1 = lent[3 * j + 1];
+                const float q2x = reinterpret_cast<const float *>(lent + 3 * j + 2)[0];
+                const float f0 = __builtin_fmaf(q0.z, vf, __builtin_fmaf(q0.y, uf, q0.x));
+                const float f1 = __builtin_fmaf(q1.y, vf, __builtin_fmaf(q1.x, uf, q0.w));
+                const float f2 = __builtin_fmaf(q2x, vf, __builtin_fmaf(q1.w, uf, q1.z));
+#else
                 const float f0 = __builtin_fmaf(lane_f(d0.z, j), vf,
                                                 __builtin_fmaf(lane_f(d0.y, j), uf, lane_f(d0.x, j)));
                 const float f1 = __builtin_fmaf(lane_f(d1.y, j), vf,
                                                 __builtin_fmaf(lane_f(d1.x, j), uf, lane_f(d0.w, j)));
                 const float f2 = __builtin_fmaf(lane_f(d2.x, j), vf,
                                                 __builtin_fmaf(lane_f(d1.w, j), uf, lane_f(d1.z, j)));
+#endif
                 const unsigned long long in =
                     rem & __ballot(!(f0 < 0.0f) && !(f1 < 0.0f) && !(f2 < 0.0f));
                 BIH_FC(++fc_ent);
@@ -2261,6 +2287,12 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
 #if BIH_HIT_CACHE
     __shared__ uint32_t s_hc[3][kThreads];   // each lane's hit of the item's previous frame: {record, leaf, plan}
 #endif
+#if BIH_ENT_LDS
+    __shared__ float4 s_ent[kThreads / 64][64 * 3];   // per wave: the list chunk bin_walk pre-tests
+    float4 *const lent = s_ent[tid >> 6];
+#else
+    float4 *const lent = nullptr;
+#endif
 #if BIH_REC_LDS
     // per wave: the intersector records (tri_prim, 13 of 16 words) of its
     // item's first 64 list entries, loaded once and read by every frame of
@@ -2609,7 +2641,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 const unsigned long long wlive = live & ~chit;
                 const unsigned long long found = wlive ? bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
                     a, prims, bin, uf, vf, dx, dy, dz, wlive, lane, cand, cmeta, cent, fc_ent, fc_mt, pf, lrec,
-                    lrec_n) : 0ull;
+                    lrec_n, lent) : 0ull;
                 if (COST) work += fc_ent + 4u * fc_mt;
 #if BIH_BINS_TIMELINE
                 tl_ent += fc_ent;
