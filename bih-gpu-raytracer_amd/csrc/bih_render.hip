@@ -1679,6 +1679,12 @@ constexpr uint32_t kNoCache = 0xFFFFFFFFu;
 #ifndef BIH_ENT_LDS
 #define BIH_ENT_LDS 1   // bin_walk's pre-tests read their entry from LDS (broadcast), not by v_readlane
 #endif
+#ifndef BIH_ENT_KEEP
+#define BIH_ENT_KEEP BIH_ENT_LDS   // the tile list's first chunk stays in LDS across an item's frames
+#endif
+#if BIH_ENT_KEEP && !(BIH_ENT_LDS && BIH_BIN_PREFETCH)
+#error "BIH_ENT_KEEP needs BIH_ENT_LDS and BIH_BIN_PREFETCH"
+#endif
 #if BIH_ENT_LDS && !BIH_BIN_SETBITS
 #error "BIH_ENT_LDS writes the chunk where the set-bits walk ballots it"
 #endif
@@ -1731,7 +1737,7 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                                                       uint32_t &cent, uint32_t &fc_ent,
                                                       uint32_t &fc_mt, uint32_t &pf,
                                                       const float4 *lrec = nullptr, uint32_t lrec_n = 0,
-                                                      float4 *lent = nullptr) {
+                                                      float4 *lent = nullptr, uint32_t *ltag = nullptr) {
     const cu32_t *off = (const cu32_t *)(const void *)a.bin_off;
     const float4 *ents = reinterpret_cast<const float4 *>(a.bin_list);
     uint32_t e = off[bin], end = off[bin + 1];
@@ -1743,9 +1749,16 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
     // before its pre-test
     uint32_t rpix = PMASK ? pixels_of(rem) : 0xFFFFu;
     for (int part = 0; part < 2; ++part) {
+#if BIH_ENT_KEEP
+        // the tile list's first chunk is still in the wave's LDS slots from
+        // the previous frame of this tile (*ltag: the bin it belongs to)
+        bool kept = part == 0 && *ltag == bin;
+#else
+        constexpr bool kept = false;
+#endif
 #if BIH_BIN_PREFETCH
         float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
-        if (e < end) bin_chunk_load(ents, e, end, lane, c0, c1, c2);
+        if (e < end && !kept) bin_chunk_load(ents, e, end, lane, c0, c1, c2);
 #endif
         while (e < end && rem) {
 #if BIH_BIN_PREFETCH
@@ -1770,18 +1783,28 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
             // has a lane, as one ballot (lane j: entry j), walked in order by
             // find-first-set; a hit shrinks rpix and re-filters the rest --
             // the entries the per-entry mask check below would pre-test
+#if BIH_ENT_KEEP
+            const uint32_t pm =
+                (kept ? reinterpret_cast<const uint32_t *>(lent + 3 * lane + 2)[3] : __float_as_uint(d2.w)) >> 16;
+#else
             const uint32_t pm = __float_as_uint(d2.w) >> 16;
+#endif
             unsigned long long todo = __ballot(lane < n && (!PMASK || (pm & rpix)));
 #if BIH_ENT_LDS
             // the chunk's entries in the wave's LDS slots (lane j: entry j):
             // each pre-test then reads its entry's 9 plane words as one
             // broadcast instead of 9 v_readlane (12 fewer VALU per entry)
-            lent[3 * lane] = d0;
-            lent[3 * lane + 1] = d1;
-            lent[3 * lane + 2] = d2;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (!kept) {
+                lent[3 * lane] = d0;
+                lent[3 * lane + 1] = d1;
+                lent[3 * lane + 2] = d2;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if BIH_ENT_KEEP
+                *ltag = (part == 0 && e == e_first) ? bin : ~0u;
+#endif
+            }
 #endif
 #if BIH_BIN_PREFETCH
             if (e + 64u < end) bin_chunk_load(ents, e + 64u, end, lane, c0, c1, c2);
@@ -1827,7 +1850,13 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 if (!in) continue;
                 BIH_FC(++fc_mt);
                 if (COUNT && !BIH_FAST_COUNTERS) ++fc_mt;
+#if BIH_ENT_LDS
+                // the entry's words 9-11 (triangle, leaf, plan | pixel mask), broadcast
+                const float4 q2 = lent[3 * j + 2];
+                const uint32_t ti = (a.dbg & 1024u) ? 0u : __builtin_amdgcn_readfirstlane(__float_as_uint(q2.y));
+#else
                 const uint32_t ti = (a.dbg & 1024u) ? 0u : __builtin_amdgcn_readlane(__float_as_uint(d2.y), j);
+#endif
                 sf32x16 r;
                 const uint32_t rel = e + j - e_first;          // (part 0: the tile's list)
                 if (BIH_REC_LDS && part == 0 && rel < lrec_n) {
@@ -1851,8 +1880,13 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
                 }
                 const unsigned long long h = prim_hits_pre(r, dx, dy, dz, in);
                 if (h & me) {
+#if BIH_ENT_LDS
+                    cand = __float_as_uint(q2.z);
+                    cmeta = __float_as_uint(q2.w);
+#else
                     cand = __builtin_amdgcn_readlane(__float_as_uint(d2.z), j);
                     cmeta = __builtin_amdgcn_readlane(__float_as_uint(d2.w), j);
+#endif
                     cent = ti;
                 }
                 rem &= ~h;
@@ -1870,6 +1904,9 @@ __device__ __forceinline__ unsigned long long bin_walk(const RenderArgs &a, cons
 #endif
             }
             e += 64u;
+#if BIH_ENT_KEEP
+            kept = false;
+#endif
         }
         if (!rem) break;
         ents = reinterpret_cast<const float4 *>(a.bin_glist);
@@ -2293,6 +2330,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
 #else
     float4 *const lent = nullptr;
 #endif
+    uint32_t ltag = ~0u;   // the bin whose list's first chunk is in lent (BIH_ENT_KEEP)
 #if BIH_REC_LDS
     // per wave: the intersector records (tri_prim, 13 of 16 words) of its
     // item's first 64 list entries, loaded once and read by every frame of
@@ -2641,7 +2679,7 @@ BIH_BINS_SGPR_ATTR k_render_bins(const RenderArgs a) {
                 const unsigned long long wlive = live & ~chit;
                 const unsigned long long found = wlive ? bin_walk<LOG2SPP == 2, COST || BIH_BINS_TIMELINE>(
                     a, prims, bin, uf, vf, dx, dy, dz, wlive, lane, cand, cmeta, cent, fc_ent, fc_mt, pf, lrec,
-                    lrec_n, lent) : 0ull;
+                    lrec_n, lent, &ltag) : 0ull;
                 if (COST) work += fc_ent + 4u * fc_mt;
 #if BIH_BINS_TIMELINE
                 tl_ent += fc_ent;
